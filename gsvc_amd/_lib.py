@@ -1,0 +1,111 @@
+"""ctypes binding of the C ABI in include/gsvc_amd.h (libgsvc_amd.so).
+
+This is the MI355X counterpart of the reference's backend loader
+(gsplat/gsplat/cuda/_backend.py:54-98), which imported the compiled torch
+extension or JIT-compiled it with nvcc and otherwise set ``_C = None``.  Here
+the library is prebuilt in-tree for gfx950 (gsvc_amd/build.py).  There is no
+CPU fallback: if the library is missing, or a tensor is not on a HIP device,
+the call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (loads torch's libamdhip64 first; the library reuses it)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libgsvc_amd.so")
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_U = ctypes.c_uint
+_F = ctypes.c_float
+_SZ = ctypes.c_size_t
+
+# name -> argtypes (restype int unless listed in _RESTYPE)
+_SIGS = {
+    "gsvc_abi_version": [],
+    "gsvc_last_error": [],
+    "gsvc_project_gaussians_2d_forward": [_I, _P, _P, _U, _U, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P],
+    "gsvc_project_gaussians_2d_backward": [_I, _P, _P, _U, _U, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "gsvc_compute_cov2d_bounds": [_I, _P, _P, _P, _P],
+    "gsvc_cumsum_workspace_bytes": [_I],
+    "gsvc_compute_cumulative_intersects": [_I, _P, _P, _P, _P, _P, _SZ, _P],
+    "gsvc_map_gaussian_to_intersects": [_I, _I, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P],
+    "gsvc_sort_pairs_workspace_bytes": [_I],
+    "gsvc_sort_isect_pairs": [_I, _P, _P, _P, _P, _I, _I, _P, _SZ, _P],
+    "gsvc_get_tile_bin_edges": [_I, _P, _P, _I, _P],
+    "gsvc_bin_tiles_workspace_bytes": [_I, _I, _I],
+    "gsvc_bin_and_sort_tiles": [_I, _I, _P, _P, _P, _P, _I, _I, _P, _P, _I, _P, _P, _SZ, _P],
+    "gsvc_rasterize_sum_forward": [_I, _I, _I, _I, _I, _I, _U, _U, _U, _P, _P, _P, _P, _P, _P, _P,
+                                   _P, _P, _P, _P],
+    "gsvc_rasterize_sum_backward": [_U, _U, _U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                    _P, _P],
+    "gsvc_rasterize_forward": [_I, _I, _I, _I, _I, _I, _U, _U, _U, _P, _P, _P, _P, _P, _P, _P,
+                               _P, _P, _P, _P],
+    "gsvc_rasterize_backward": [_U, _U, _U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                _P, _P],
+}
+_RESTYPE = {
+    "gsvc_last_error": ctypes.c_char_p,
+    "gsvc_cumsum_workspace_bytes": _SZ,
+    "gsvc_sort_pairs_workspace_bytes": _SZ,
+    "gsvc_bin_tiles_workspace_bytes": _SZ,
+}
+
+ABI_VERSION = 1
+
+_lib = None
+_lock = threading.Lock()
+
+
+def symbols():
+    """Names of every entry point declared in include/gsvc_amd.h."""
+    return list(_SIGS)
+
+
+def load():
+    """Load libgsvc_amd.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"gsvc_amd: {LIB_PATH} not found; build it with `python -m gsvc_amd.build` "
+                    "(there is no CPU fallback)")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, args in _SIGS.items():
+                fn = getattr(lib, name)
+                fn.argtypes = args
+                fn.restype = _RESTYPE.get(name, _I)
+            v = lib.gsvc_abi_version()
+            if v != ABI_VERSION:
+                raise RuntimeError(f"gsvc_amd: ABI version {v} != {ABI_VERSION}; rebuild the library")
+            _lib = lib
+    return _lib
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        msg = load().gsvc_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (status {rc}): {msg}")
+
+
+def size(name: str, *args) -> int:
+    return int(getattr(load(), name)(*args))
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream(device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

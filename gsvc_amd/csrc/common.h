@@ -1,0 +1,70 @@
+// Shared device helpers for the gfx950 kernels of gsvc_amd.
+//
+// Floating-point contract: the library is compiled with
+// -ffp-contract=off, so every fused multiply-add below is an explicit fmaf();
+// division and sqrt are IEEE; exp(-s) is v_exp_f32(s * -log2(e)).  The CPU
+// oracle (oracle/oracle.c) follows the same op sequence.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gsvc_amd.h"
+
+namespace gsvc {
+
+constexpr int kTile = 16;          // BLOCK_X = BLOCK_Y (reference config.h:1-2)
+constexpr int kTilePix = 256;      // BLOCK_SIZE (config.h:3): entries blended per tile
+constexpr float kNegLog2e = -1.4426950408889634f;
+constexpr float kAlphaMin = 1.0f / 255.0f;
+
+// Host-side error plumbing -------------------------------------------------
+int set_error(int code, const char *fmt, ...);
+int check_launch(const char *what);
+
+// XCD-aware block -> work-item remap.  Blocks b and b+8 share an XCD (they are
+// dealt round-robin over the 8 XCDs), so give each XCD a contiguous range of
+// tiles: neighbouring tiles share splats, which then hit the same L2.  Speed
+// only; any placement gives the same results.  Bijective for any count
+// (cdna_hip_programming.md §5, "XCD swizzle must be bijective").
+__device__ __forceinline__ int xcd_remap(int orig, int count) {
+    const int q = count >> 3, r = count & 7, xcd = orig & 7;
+    const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + (orig >> 3);
+}
+
+// v_cvt_i32_f32 semantics: truncate, saturate, NaN -> 0.
+__device__ __forceinline__ int cvt_i32(float f) {
+    if (f != f) return 0;
+    if (f >= 2147483648.0f) return 2147483647;
+    if (f <= -2147483648.0f) return (-2147483647 - 1);
+    return (int)f;
+}
+
+// helpers.cuh:11-43: tile bbox of a splat, [min, max) in tile units, clamped.
+__device__ __forceinline__ void tile_bbox(float cx, float cy, float radius, int tbx, int tby,
+                                          unsigned &x0, unsigned &y0, unsigned &x1, unsigned &y1) {
+    const float tcx = cx / (float)kTile, tcy = cy / (float)kTile;
+    const float tr = radius / (float)kTile;
+    int a;
+    a = cvt_i32(tcx - tr);          x0 = min((unsigned)max(a, 0), (unsigned)tbx);
+    a = cvt_i32((tcx + tr) + 1.0f); x1 = min((unsigned)max(a, 0), (unsigned)tbx);
+    a = cvt_i32(tcy - tr);          y0 = min((unsigned)max(a, 0), (unsigned)tby);
+    a = cvt_i32((tcy + tr) + 1.0f); y1 = min((unsigned)max(a, 0), (unsigned)tby);
+}
+
+// sigma of forward.cu:595-597 in the build's fixed op order.
+__device__ __forceinline__ float splat_sigma_h(float ha, float b, float hc, float dx, float dy) {
+    const float cq = (hc * dy) * dy;
+    const float bdy = b * dy;
+    const float q = fmaf(ha, dx, bdy);
+    return fmaf(q, dx, cq);
+}
+
+__device__ __forceinline__ float exp_neg(float s) {
+    return __builtin_amdgcn_exp2f(s * kNegLog2e);
+}
+
+__host__ __device__ __forceinline__ int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+}  // namespace gsvc

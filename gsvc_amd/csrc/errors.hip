@@ -1,0 +1,29 @@
+// Error reporting of the C ABI: a per-thread message for gsvc_last_error().
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "common.h"
+
+namespace gsvc {
+
+static thread_local char g_last_error[512] = "";
+
+int set_error(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int check_launch(const char *what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(GSVC_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+    return GSVC_OK;
+}
+
+}  // namespace gsvc
+
+extern "C" int gsvc_abi_version(void) { return 1; }
+
+extern "C" const char *gsvc_last_error(void) { return gsvc::g_last_error; }

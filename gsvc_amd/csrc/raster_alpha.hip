@@ -1,0 +1,291 @@
+// Front-to-back alpha-compositing rasterizer (rasterize_gaussians), gfx950.
+//
+// Reference: gsplat/gsplat/cuda/csrc/forward.cu:252-374 (rasterize_forward),
+// backward.cu:138-315 (rasterize_backward_kernel), bindings.cu:332-398,631-704;
+// Python glue rasterize.py:89-253.  Not used by GSVC's scripts, but named by
+// the north star; it shares the binning and the LDS-staged tile layout of the
+// sum path.
+//
+// Semantics kept: alpha = min(0.999, o exp(-sigma)) in the forward and
+// min(0.99, ...) in the backward (forward.cu:339 vs backward.cu:244); a pixel
+// stops at the entry whose next_T <= 1e-4 (that entry is not blended); every
+// entry of the tile is visited (no 256 cap); out = acc + T * background.
+//
+// Forward: one wave64 per tile, 4 pixels per lane (as the sum forward), the
+// wave leaves the tile when every lane's 4 pixels are done.
+// Backward: the transmittance recursion runs per pixel from the back, so it
+// is PIXEL-parallel: 256 threads = 256 pixels; per entry each wave reduces
+// its 9 partial gradients with shuffles, adds them to an LDS record with LDS
+// float atomics (4 waves), and once per 256-entry chunk the tile's records go
+// to HBM as one 64-byte atomic request per (splat, tile).
+#include "common.h"
+
+namespace gsvc {
+
+constexpr int kAChunk = 64;
+
+__global__ __launch_bounds__(64) void raster_alpha_fwd_kernel(
+    int tbx, int img_w, int img_h, int ntiles, const int *__restrict__ ids,
+    const int2 *__restrict__ bins, const float2 *__restrict__ xys, const float *__restrict__ conics,
+    const float *__restrict__ colors, const float *__restrict__ opac, const float *__restrict__ bg,
+    float *__restrict__ out, float *__restrict__ final_Ts, int *__restrict__ final_idx) {
+    __shared__ float4 s_geo[kAChunk];  // x, y, 0.5a, b
+    __shared__ float4 s_col[kAChunk];  // 0.5c, opacity, r, g
+    __shared__ float s_blu[kAChunk];
+    const int tile = xcd_remap(blockIdx.x, ntiles);
+    const int ty = tile / tbx, tx = tile - ty * tbx;
+    const int lane = threadIdx.x;
+    const int pi = ty * kTile + (lane >> 2);
+    const int pj = tx * kTile + ((lane & 3) << 2);
+    const float py = (float)pi;
+    const int2 range = bins[tile];
+    const int n = max(range.y - range.x, 0);
+
+    float T[4] = {1.f, 1.f, 1.f, 1.f};
+    float ar[4] = {0.f, 0.f, 0.f, 0.f}, ag[4] = {0.f, 0.f, 0.f, 0.f}, ab[4] = {0.f, 0.f, 0.f, 0.f};
+    int last[4] = {0, 0, 0, 0};
+    bool done[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) done[q] = !(pi < img_h && pj + q < img_w);
+
+    for (int base = 0; base < n; base += kAChunk) {
+        if (__all(done[0] && done[1] && done[2] && done[3])) break;
+        const int cnt = min(kAChunk, n - base);
+        if (lane < cnt) {
+            const int g = ids[range.x + base + lane];
+            const float2 xy = xys[g];
+            const float a = conics[3 * g], b = conics[3 * g + 1], c = conics[3 * g + 2];
+            s_geo[lane] = make_float4(xy.x, xy.y, 0.5f * a, b);
+            s_col[lane] = make_float4(0.5f * c, opac[g], colors[3 * g], colors[3 * g + 1]);
+            s_blu[lane] = colors[3 * g + 2];
+        }
+        __syncthreads();
+        for (int t = 0; t < cnt; ++t) {
+            const float4 G = s_geo[t];
+            const float4 C = s_col[t];
+            const float dy = G.y - py;
+            const float cq = (C.x * dy) * dy;
+            const float bdy = G.w * dy;
+            const int k = range.x + base + t;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (done[q]) continue;
+                const float dx = G.x - (float)(pj + q);
+                const float s = fmaf(fmaf(G.z, dx, bdy), dx, cq);
+                const float al = fminf(0.999f, C.y * exp_neg(s));
+                if (s < 0.0f || al < kAlphaMin) continue;
+                const float next_T = T[q] * (1.0f - al);
+                if (next_T <= 1e-4f) {
+                    done[q] = true;
+                    continue;
+                }
+                const float vis = al * T[q];
+                ar[q] = fmaf(C.z, vis, ar[q]);
+                ag[q] = fmaf(C.w, vis, ag[q]);
+                ab[q] = fmaf(s_blu[t], vis, ab[q]);
+                T[q] = next_T;
+                last[q] = k;
+            }
+        }
+        __syncthreads();
+    }
+    if (pi >= img_h) return;
+    const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (pj + q < img_w) {
+            const size_t p = (size_t)pi * (size_t)img_w + (size_t)(pj + q);
+            out[3 * p] = fmaf(T[q], bg0, ar[q]);
+            out[3 * p + 1] = fmaf(T[q], bg1, ag[q]);
+            out[3 * p + 2] = fmaf(T[q], bg2, ab[q]);
+            final_Ts[p] = T[q];
+            final_idx[p] = last[q];
+        }
+    }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void raster_alpha_bwd_kernel(
+    int tbx, int img_w, int img_h, int ntiles, const int *__restrict__ ids,
+    const int2 *__restrict__ bins, const float2 *__restrict__ xys, const float *__restrict__ conics,
+    const float *__restrict__ colors, const float *__restrict__ opac, const float *__restrict__ bg,
+    const float *__restrict__ final_Ts, const int *__restrict__ final_idx,
+    const float *__restrict__ v_out, const float *__restrict__ v_out_alpha,
+    float *__restrict__ grad) {
+    __shared__ float4 s_geo[kTilePix];  // x, y, a, b
+    __shared__ float4 s_col[kTilePix];  // c, opacity, r, g
+    __shared__ float s_blu[kTilePix];
+    __shared__ int s_gid[kTilePix];
+    __shared__ float s_acc[kTilePix][9];
+    __shared__ int s_max[4];
+    const int tile = xcd_remap(blockIdx.x, ntiles);
+    const int ty = tile / tbx, tx = tile - ty * tbx;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int pi = ty * kTile + (tid >> 4), pj = tx * kTile + (tid & 15);
+    const bool inside = pi < img_h && pj < img_w;
+    const float px = (float)pj, py = (float)pi;
+    // backward.cu:160: out-of-image threads clamp to the last pixel; they are
+    // never valid, so only their loads matter.
+    const size_t p = inside ? (size_t)pi * (size_t)img_w + (size_t)pj : 0;
+    const float T_final = inside ? final_Ts[p] : 1.0f;
+    float T = T_final;
+    float buf0 = 0.f, buf1 = 0.f, buf2 = 0.f;
+    const int bin_final = inside ? final_idx[p] : (-2147483647 - 1);
+    const float vo0 = inside ? v_out[3 * p] : 0.f, vo1 = inside ? v_out[3 * p + 1] : 0.f;
+    const float vo2 = inside ? v_out[3 * p + 2] : 0.f;
+    const float voa = inside ? v_out_alpha[p] : 0.f;
+    const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
+    int f = bin_final;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) f = max(f, __shfl_xor(f, off, 64));
+    if (lane == 0) s_max[tid >> 6] = f;
+    __syncthreads();
+    const int maxf = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
+    const int2 range = bins[tile];
+    const int kend = min(range.y, maxf == (-2147483647 - 1) ? maxf : maxf + 1);
+
+    // chunks of <= 256 entries, back to front
+    for (int ce = kend; ce > range.x; ce -= kTilePix) {
+        const int cs = max(range.x, ce - kTilePix);
+        const int n = ce - cs;
+        if (tid < n) {
+            const int g = ids[cs + tid];
+            s_gid[tid] = g;
+            const float2 xy = xys[g];
+            s_geo[tid] = make_float4(xy.x, xy.y, conics[3 * g], conics[3 * g + 1]);
+            s_col[tid] = make_float4(conics[3 * g + 2], opac[g], colors[3 * g], colors[3 * g + 1]);
+            s_blu[tid] = colors[3 * g + 2];
+#pragma unroll
+            for (int c = 0; c < 9; ++c) s_acc[tid][c] = 0.f;
+        }
+        __syncthreads();
+        for (int t = n - 1; t >= 0; --t) {
+            const int k = cs + t;
+            bool valid = inside && k <= bin_final;
+            float4 G, C;
+            float dx = 0.f, dy = 0.f, vis = 0.f, al = 0.f;
+            if (valid) {
+                G = s_geo[t];
+                C = s_col[t];
+                dx = G.x - px;
+                dy = G.y - py;
+                const float s = splat_sigma_h(0.5f * G.z, G.w, 0.5f * C.x, dx, dy);
+                vis = exp_neg(s);
+                al = fminf(0.99f, C.y * vis);
+                if (s < 0.0f || al < kAlphaMin) valid = false;
+            }
+            if (!__any(valid)) continue;
+            float g_r = 0.f, g_g = 0.f, g_b = 0.f, g_c0 = 0.f, g_c1 = 0.f, g_c2 = 0.f;
+            float g_x = 0.f, g_y = 0.f, g_o = 0.f;
+            if (valid) {
+                const float ra = 1.0f / (1.0f - al);
+                T = T * ra;
+                const float fac = al * T;
+                const float r = C.z, gg = C.w, bb = s_blu[t];
+                const float tfra = T_final * ra;
+                float v_alpha = (r * T - buf0 * ra) * vo0;
+                v_alpha = fmaf(gg * T - buf1 * ra, vo1, v_alpha);
+                v_alpha = fmaf(bb * T - buf2 * ra, vo2, v_alpha);
+                v_alpha = fmaf(tfra, voa, v_alpha);
+                v_alpha = fmaf(-tfra * bg0, vo0, v_alpha);
+                v_alpha = fmaf(-tfra * bg1, vo1, v_alpha);
+                v_alpha = fmaf(-tfra * bg2, vo2, v_alpha);
+                buf0 = fmaf(r, fac, buf0);
+                buf1 = fmaf(gg, fac, buf1);
+                buf2 = fmaf(bb, fac, buf2);
+                const float v_sigma = (-C.y * vis) * v_alpha;
+                g_r = fac * vo0;
+                g_g = fac * vo1;
+                g_b = fac * vo2;
+                const float hs = 0.5f * v_sigma;
+                g_c0 = (hs * dx) * dx;
+                g_c1 = (hs * dx) * dy;
+                g_c2 = (hs * dy) * dy;
+                g_x = v_sigma * fmaf(G.z, dx, G.w * dy);
+                g_y = v_sigma * fmaf(G.w, dx, C.x * dy);
+                g_o = vis * v_alpha;
+            }
+            g_x = wave_sum(g_x);
+            g_y = wave_sum(g_y);
+            g_c0 = wave_sum(g_c0);
+            g_c1 = wave_sum(g_c1);
+            g_c2 = wave_sum(g_c2);
+            g_r = wave_sum(g_r);
+            g_g = wave_sum(g_g);
+            g_b = wave_sum(g_b);
+            g_o = wave_sum(g_o);
+            if (lane == 0) {
+                atomicAdd(&s_acc[t][0], g_x);
+                atomicAdd(&s_acc[t][1], g_y);
+                atomicAdd(&s_acc[t][2], g_c0);
+                atomicAdd(&s_acc[t][3], g_c1);
+                atomicAdd(&s_acc[t][4], g_c2);
+                atomicAdd(&s_acc[t][5], g_r);
+                atomicAdd(&s_acc[t][6], g_g);
+                atomicAdd(&s_acc[t][7], g_b);
+                atomicAdd(&s_acc[t][8], g_o);
+            }
+        }
+        __syncthreads();
+        for (int q = tid; q < n * 16; q += kTilePix) {
+            const int e2 = q >> 4, c = q & 15;
+            if (c < 9) unsafeAtomicAdd(grad + (size_t)s_gid[e2] * 16 + c, s_acc[e2][c]);
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace gsvc
+
+using namespace gsvc;
+
+extern "C" int gsvc_rasterize_forward(int tbx, int tby, int tbz, int block_x, int block_y,
+                                      int block_z, unsigned img_width, unsigned img_height,
+                                      unsigned img_depth, const int *gaussian_ids_sorted,
+                                      const int *tile_bins, const float *xys, const float *conics,
+                                      const float *colors, const float *opacities,
+                                      const float *background, float *out_img, float *final_Ts,
+                                      int *final_idx, void *stream) {
+    (void)tbz; (void)block_z; (void)img_depth;
+    if (block_x != kTile || block_y != kTile)
+        return set_error(GSVC_ERR_ARG, "rasterize_forward: only 16x16 tiles are supported");
+    if (tbx != ceil_div((int)img_width, kTile) || tby != ceil_div((int)img_height, kTile))
+        return set_error(GSVC_ERR_ARG, "rasterize_forward: tile_bounds do not match the image");
+    const int ntiles = tbx * tby;
+    if (ntiles == 0) return GSVC_OK;
+    hipLaunchKernelGGL(raster_alpha_fwd_kernel, dim3(ntiles), dim3(64), 0, (hipStream_t)stream, tbx,
+                       (int)img_width, (int)img_height, ntiles, gaussian_ids_sorted,
+                       (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacities,
+                       background, out_img, final_Ts, final_idx);
+    return check_launch("rasterize_forward");
+}
+
+extern "C" int gsvc_rasterize_backward(unsigned img_height, unsigned img_width, unsigned block_h,
+                                       unsigned block_w, int num_points,
+                                       const int *gaussian_ids_sorted, const int *tile_bins,
+                                       const float *xys, const float *conics, const float *colors,
+                                       const float *opacities, const float *background,
+                                       const float *final_Ts, const int *final_idx,
+                                       const float *v_output, const float *v_output_alpha,
+                                       float *grad_records, void *stream) {
+    if (block_h != (unsigned)kTile || block_w != (unsigned)kTile)
+        return set_error(GSVC_ERR_ARG, "rasterize_backward: only 16x16 tiles are supported");
+    if (num_points < 0) return set_error(GSVC_ERR_ARG, "rasterize_backward: bad num_points");
+    hipStream_t s = (hipStream_t)stream;
+    if (num_points > 0 &&
+        hipMemsetAsync(grad_records, 0, sizeof(float) * 16 * (size_t)num_points, s) != hipSuccess)
+        return set_error(GSVC_ERR_HIP, "rasterize_backward: memset failed");
+    const int tbx = ceil_div((int)img_width, kTile), tby = ceil_div((int)img_height, kTile);
+    const int ntiles = tbx * tby;
+    if (ntiles == 0 || num_points == 0) return GSVC_OK;
+    hipLaunchKernelGGL(raster_alpha_bwd_kernel, dim3(ntiles), dim3(256), 0, s, tbx, (int)img_width,
+                       (int)img_height, ntiles, gaussian_ids_sorted, (const int2 *)tile_bins,
+                       (const float2 *)xys, conics, colors, opacities, background, final_Ts,
+                       final_idx, v_output, v_output_alpha, grad_records);
+    return check_launch("rasterize_backward");
+}

@@ -1,0 +1,309 @@
+"""Native op table: the MI355X replacement of the reference's ``gsplat.cuda``.
+
+Each function keeps the name, positional signature, dtypes and return tuple of
+the op the reference bound in gsplat/gsplat/cuda/csrc/ext.cpp:6-23 (wrappers
+in bindings.cu) and exposed lazily through gsplat/gsplat/cuda/__init__.py:14-30,
+and calls the gfx950 C ABI (include/gsvc_amd.h) on the tensors' device and
+current stream.  Outputs are fresh tensors from the PyTorch caching allocator,
+as with the reference's ``torch::zeros`` (bindings.cu:808-817 etc.).
+
+Differences from the reference, all documented in DESIGN.md §3:
+  * ``rasterize_sum_forward`` returns ``final_Ts`` as an expanded constant 1
+    view (the sum kernel never changes T, forward.cu:579,617);
+  * the rasterizer backward ops return the four gradients as strided views of
+    one [N, 16] record tensor (one 64-byte atomic record per splat);
+  * ``get_tile_bin_edges`` returns max(M, last tile + 1) rows instead of M
+    (the reference wrote past its M-row allocation when M < #tiles);
+  * ``nd_rasterize_*`` (C != 3) are not provided: out of scope, and the
+    reference did not export ``nd_rasterize_sum_*`` either (AttributeError).
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+
+from . import _lib as L
+
+TILE = 16
+
+
+def _dev(t: torch.Tensor, name: str) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{name} must be a CUDA tensor (gsvc_amd has no CPU path)")
+
+
+def _f32(t: torch.Tensor, name: str) -> torch.Tensor:
+    _dev(t, name)
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name}: expected scalar type Float but found {t.dtype}")
+    return t.contiguous()
+
+
+def _i32(t: torch.Tensor, name: str) -> torch.Tensor:
+    _dev(t, name)
+    if t.dtype != torch.int32:
+        raise RuntimeError(f"{name}: expected scalar type Int but found {t.dtype}")
+    return t.contiguous()
+
+
+def _i64(t: torch.Tensor, name: str) -> torch.Tensor:
+    _dev(t, name)
+    if t.dtype != torch.int64:
+        raise RuntimeError(f"{name}: expected scalar type Long but found {t.dtype}")
+    return t.contiguous()
+
+
+def _tb(tile_bounds) -> Tuple[int, int, int]:
+    tb = tuple(int(x) for x in tile_bounds)
+    if len(tb) != 3:
+        raise ValueError("tile_bounds must be a (x, y, z) tuple")
+    return tb
+
+
+# ---------------------------------------------------------------------------
+# 2D projection (bindings.cu:781-839, 902-949)
+
+def project_gaussians_2d_forward(num_points, means2d, L_elements, img_height, img_width,
+                                 tile_bounds, clip_thresh):
+    means2d = _f32(means2d, "means2d")
+    L_elements = _f32(L_elements, "L_elements")
+    n = int(num_points)
+    dev = means2d.device
+    tb = _tb(tile_bounds)
+    xys = torch.empty((n, 2), dtype=torch.float32, device=dev)
+    depths = torch.empty((n,), dtype=torch.float32, device=dev)
+    radii = torch.empty((n,), dtype=torch.int32, device=dev)
+    conics = torch.empty((n, 3), dtype=torch.float32, device=dev)
+    nth = torch.empty((n,), dtype=torch.int32, device=dev)
+    L.call("gsvc_project_gaussians_2d_forward", n, L.ptr(means2d), L.ptr(L_elements),
+           int(img_height), int(img_width), tb[0], tb[1], tb[2], float(clip_thresh),
+           L.ptr(xys), L.ptr(depths), L.ptr(radii), L.ptr(conics), L.ptr(nth), L.stream(dev))
+    return xys, depths, radii, conics, nth
+
+
+def project_gaussians_2d_backward(num_points, means2d, L_elements, img_height, img_width, radii,
+                                  conics, v_xy, v_depth, v_conic):
+    L_elements = _f32(L_elements, "L_elements")
+    radii = _i32(radii, "radii")
+    conics = _f32(conics, "conics")
+    v_xy = _f32(v_xy, "v_xy")
+    v_conic = _f32(v_conic, "v_conic")
+    n = int(num_points)
+    dev = L_elements.device
+    v_cov2d = torch.empty((n, 3), dtype=torch.float32, device=dev)
+    v_mean2d = torch.empty((n, 2), dtype=torch.float32, device=dev)
+    v_L = torch.empty((n, 3), dtype=torch.float32, device=dev)
+    L.call("gsvc_project_gaussians_2d_backward", n, L.ptr(means2d), L.ptr(L_elements),
+           int(img_height), int(img_width), L.ptr(radii), L.ptr(conics), L.ptr(v_xy), None,
+           L.ptr(v_conic), L.ptr(v_cov2d), L.ptr(v_mean2d), L.ptr(v_L), L.stream(dev))
+    return v_cov2d, v_mean2d, v_L
+
+
+def compute_cov2d_bounds(num_pts, covs2d):
+    covs2d = _f32(covs2d, "covs2d")
+    n = int(num_pts)
+    dev = covs2d.device
+    conics = torch.empty((n, 3), dtype=torch.float32, device=dev)
+    radii = torch.empty((n, 1), dtype=torch.float32, device=dev)
+    L.call("gsvc_compute_cov2d_bounds", n, L.ptr(covs2d), L.ptr(conics), L.ptr(radii), L.stream(dev))
+    return conics, radii
+
+
+# ---------------------------------------------------------------------------
+# Binning (bindings.cu:274-330 and the torch glue of utils.py:99-167)
+
+def cumulative_intersects(num_tiles_hit, depths=None):
+    """int32 inclusive cumsum (utils.py:116) and a device int32[4] meta record
+    {M, OR of depth bits, AND of depth bits, #emitting splats}."""
+    num_tiles_hit = _i32(num_tiles_hit, "num_tiles_hit")
+    n = num_tiles_hit.numel()
+    dev = num_tiles_hit.device
+    if depths is not None:
+        depths = _f32(depths, "depths")
+    cum = torch.empty((n,), dtype=torch.int32, device=dev)
+    meta = torch.empty((4,), dtype=torch.int32, device=dev)
+    ws = torch.empty((L.size("gsvc_cumsum_workspace_bytes", n),), dtype=torch.uint8, device=dev)
+    L.call("gsvc_compute_cumulative_intersects", n, L.ptr(num_tiles_hit), L.ptr(depths), L.ptr(cum),
+           L.ptr(meta), L.ptr(ws), ws.numel(), L.stream(dev))
+    return cum, meta
+
+
+def map_gaussian_to_intersects(num_points, num_intersects, xys, depths, radii, cum_tiles_hit,
+                               tile_bounds):
+    xys = _f32(xys, "xys")
+    depths = _f32(depths, "depths")
+    radii = _i32(radii, "radii")
+    cum_tiles_hit = _i32(cum_tiles_hit, "cum_tiles_hit")
+    tb = _tb(tile_bounds)
+    m = int(num_intersects)
+    dev = xys.device
+    isect = torch.empty((m,), dtype=torch.int64, device=dev)
+    gids = torch.empty((m,), dtype=torch.int32, device=dev)
+    L.call("gsvc_map_gaussian_to_intersects", int(num_points), m, L.ptr(xys), L.ptr(depths),
+           L.ptr(radii), L.ptr(cum_tiles_hit), tb[0], tb[1], tb[2], L.ptr(isect), L.ptr(gids),
+           L.stream(dev))
+    return isect, gids
+
+
+def sort_isect_pairs(isect_ids, gaussian_ids, begin_bit=0, end_bit=64):
+    """torch.sort(isect_ids) + torch.gather(gaussian_ids) (utils.py:164-165) as
+    one stable radix sort; ties keep input order."""
+    isect_ids = _i64(isect_ids, "isect_ids")
+    gaussian_ids = _i32(gaussian_ids, "gaussian_ids")
+    m = isect_ids.numel()
+    dev = isect_ids.device
+    ko = torch.empty_like(isect_ids)
+    vo = torch.empty_like(gaussian_ids)
+    ws = torch.empty((L.size("gsvc_sort_pairs_workspace_bytes", m),), dtype=torch.uint8, device=dev)
+    L.call("gsvc_sort_isect_pairs", m, L.ptr(isect_ids), L.ptr(gaussian_ids), L.ptr(ko), L.ptr(vo),
+           int(begin_bit), int(end_bit), L.ptr(ws), ws.numel(), L.stream(dev))
+    return ko, vo
+
+
+def get_tile_bin_edges(num_intersects, isect_ids_sorted, num_rows=None):
+    isect_ids_sorted = _i64(isect_ids_sorted, "isect_ids_sorted")
+    m = int(num_intersects)
+    dev = isect_ids_sorted.device
+    if num_rows is None:
+        last_tile = int(isect_ids_sorted[m - 1].item() >> 32) if m > 0 else -1
+        num_rows = max(m, last_tile + 1)
+    bins = torch.empty((int(num_rows), 2), dtype=torch.int32, device=dev)
+    L.call("gsvc_get_tile_bin_edges", m, L.ptr(isect_ids_sorted), L.ptr(bins), int(num_rows),
+           L.stream(dev))
+    return bins
+
+
+def bin_and_sort_tiles(num_points, num_intersects, xys, depths, radii, cum_tiles_hit, tile_bounds,
+                       want_isect_ids=False):
+    """Fused hot-path binning (valid when all emitting splats share their depth
+    bits): returns (gaussian_ids_sorted, tile_bins[#tiles, 2], isect_ids_sorted|None)."""
+    xys = _f32(xys, "xys")
+    radii = _i32(radii, "radii")
+    cum_tiles_hit = _i32(cum_tiles_hit, "cum_tiles_hit")
+    depths = _f32(depths, "depths") if depths is not None else None
+    tb = _tb(tile_bounds)
+    n, m = int(num_points), int(num_intersects)
+    ntiles = tb[0] * tb[1]
+    dev = xys.device
+    gids = torch.empty((m,), dtype=torch.int32, device=dev)
+    bins = torch.empty((ntiles, 2), dtype=torch.int32, device=dev)
+    isect = torch.empty((m,), dtype=torch.int64, device=dev) if want_isect_ids else None
+    ws = torch.empty((L.size("gsvc_bin_tiles_workspace_bytes", n, m, ntiles),), dtype=torch.uint8,
+                     device=dev)
+    L.call("gsvc_bin_and_sort_tiles", n, m, L.ptr(xys), L.ptr(depths), L.ptr(radii),
+           L.ptr(cum_tiles_hit), tb[0], tb[1], L.ptr(gids), L.ptr(bins), ntiles, L.ptr(isect),
+           L.ptr(ws), ws.numel(), L.stream(dev))
+    return gids, bins, isect
+
+
+# ---------------------------------------------------------------------------
+# Rasterizers (bindings.cu:332-469, 631-779)
+
+def _bins_for(tile_bins: torch.Tensor, ntiles: int) -> torch.Tensor:
+    tile_bins = _i32(tile_bins, "tile_bins")
+    if tile_bins.dim() != 2 or tile_bins.shape[1] != 2:
+        raise RuntimeError("tile_bins must have shape (rows, 2)")
+    if tile_bins.shape[0] < ntiles:  # reference-style M-row table: pad with empty tiles
+        pad = torch.zeros((ntiles - tile_bins.shape[0], 2), dtype=torch.int32, device=tile_bins.device)
+        tile_bins = torch.cat([tile_bins, pad])
+    return tile_bins
+
+
+def _raster_fwd(sym, tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys, conics,
+                colors, opacities, background, want_Ts):
+    tb = _tb(tile_bounds)
+    blk = _tb(block)
+    img_w, img_h, img_d = (int(x) for x in img_size)
+    gids = _i32(gaussian_ids_sorted, "gaussian_ids_sorted")
+    xys = _f32(xys, "xys")
+    conics = _f32(conics, "conics")
+    colors = _f32(colors, "colors")
+    opacities = _f32(opacities, "opacities")
+    background = _f32(background, "background")
+    if colors.dim() != 2 or colors.shape[1] != 3:
+        raise RuntimeError("colors must have shape (N, 3)")
+    bins = _bins_for(tile_bins, tb[0] * tb[1])
+    dev = xys.device
+    out = torch.empty((img_h, img_w, 3), dtype=torch.float32, device=dev)
+    idx = torch.empty((img_h, img_w), dtype=torch.int32, device=dev)
+    Ts = torch.empty((img_h, img_w), dtype=torch.float32, device=dev) if want_Ts else None
+    L.call(sym, tb[0], tb[1], tb[2], blk[0], blk[1], blk[2], img_w, img_h, img_d, L.ptr(gids),
+           L.ptr(bins), L.ptr(xys), L.ptr(conics), L.ptr(colors), L.ptr(opacities),
+           L.ptr(background), L.ptr(out), L.ptr(Ts), L.ptr(idx), L.stream(dev))
+    return out, Ts, idx
+
+
+def rasterize_sum_forward(tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys,
+                          conics, colors, opacities, background):
+    out, _, idx = _raster_fwd("gsvc_rasterize_sum_forward", tile_bounds, block, img_size,
+                              gaussian_ids_sorted, tile_bins, xys, conics, colors, opacities,
+                              background, want_Ts=False)
+    final_Ts = torch.ones((1, 1), dtype=torch.float32, device=out.device).expand(out.shape[0],
+                                                                              out.shape[1])
+    return out, final_Ts, idx
+
+
+def rasterize_forward(tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys, conics,
+                      colors, opacities, background):
+    return _raster_fwd("gsvc_rasterize_forward", tile_bounds, block, img_size, gaussian_ids_sorted,
+                       tile_bins, xys, conics, colors, opacities, background, want_Ts=True)
+
+
+def split_grad_records(rec: torch.Tensor):
+    """(v_xy [N,2], v_conic [N,3], v_colors [N,3], v_opacity [N,1]) views."""
+    return rec[:, 0:2], rec[:, 2:5], rec[:, 5:8], rec[:, 8:9]
+
+
+def _raster_bwd(sym, img_height, img_width, BLOCK_H, BLOCK_W, gaussian_ids_sorted, tile_bins, xys,
+                conics, colors, opacities, background, final_Ts, final_idx, v_output,
+                v_output_alpha):
+    xys = _f32(xys, "xys")
+    colors = _f32(colors, "colors")
+    if xys.dim() != 2 or xys.shape[1] != 2:
+        raise RuntimeError("xys must have dimensions (num_points, 2)")
+    if colors.dim() != 2 or colors.shape[1] != 3:
+        raise RuntimeError("colors must have 2 dimensions")
+    h, w = int(img_height), int(img_width)
+    tb = ((w + int(BLOCK_W) - 1) // int(BLOCK_W), (h + int(BLOCK_H) - 1) // int(BLOCK_H))
+    gids = _i32(gaussian_ids_sorted, "gaussian_ids_sorted")
+    bins = _bins_for(tile_bins, tb[0] * tb[1])
+    conics = _f32(conics, "conics")
+    opacities = _f32(opacities, "opacities")
+    background = _f32(background, "background")
+    final_idx = _i32(final_idx, "final_idx")
+    v_output = _f32(v_output, "v_output")
+    Ts = _f32(final_Ts, "final_Ts") if sym == "gsvc_rasterize_backward" else None
+    v_alpha = (_f32(v_output_alpha, "v_output_alpha")
+               if sym == "gsvc_rasterize_backward" else None)
+    n = xys.shape[0]
+    rec = torch.empty((n, 16), dtype=torch.float32, device=xys.device)
+    L.call(sym, h, w, int(BLOCK_H), int(BLOCK_W), n, L.ptr(gids), L.ptr(bins), L.ptr(xys),
+           L.ptr(conics), L.ptr(colors), L.ptr(opacities), L.ptr(background), L.ptr(Ts),
+           L.ptr(final_idx), L.ptr(v_output), L.ptr(v_alpha), L.ptr(rec), L.stream(xys.device))
+    return split_grad_records(rec)
+
+
+def rasterize_sum_backward(img_height, img_width, BLOCK_H, BLOCK_W, gaussian_ids_sorted, tile_bins,
+                           xys, conics, colors, opacities, background, final_Ts, final_idx,
+                           v_output, v_output_alpha):
+    return _raster_bwd("gsvc_rasterize_sum_backward", img_height, img_width, BLOCK_H, BLOCK_W,
+                       gaussian_ids_sorted, tile_bins, xys, conics, colors, opacities, background,
+                       final_Ts, final_idx, v_output, v_output_alpha)
+
+
+def rasterize_backward(img_height, img_width, BLOCK_H, BLOCK_W, gaussian_ids_sorted, tile_bins,
+                       xys, conics, colors, opacities, background, final_Ts, final_idx, v_output,
+                       v_output_alpha):
+    return _raster_bwd("gsvc_rasterize_backward", img_height, img_width, BLOCK_H, BLOCK_W,
+                       gaussian_ids_sorted, tile_bins, xys, conics, colors, opacities, background,
+                       final_Ts, final_idx, v_output, v_output_alpha)
+
+
+__all__ = [
+    "project_gaussians_2d_forward", "project_gaussians_2d_backward", "compute_cov2d_bounds",
+    "map_gaussian_to_intersects", "get_tile_bin_edges", "rasterize_sum_forward",
+    "rasterize_sum_backward", "rasterize_forward", "rasterize_backward",
+]

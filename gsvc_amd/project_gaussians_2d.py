@@ -1,0 +1,68 @@
+"""2D projection operator, same API as gsplat/gsplat/project_gaussians_2d.py.
+
+``project_gaussians_2d`` (reference :12-57) and its autograd Function
+(reference :59-141) keep the signature, saved tensors and gradient routing of
+the reference; the kernels are gsvc_amd/csrc/project2d.hip.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+from torch import Tensor
+from torch.autograd import Function
+
+from . import ops as _C
+
+
+def project_gaussians_2d(
+    means2d: Tensor,
+    L_elements: Tensor,
+    img_height: int,
+    img_width: int,
+    tile_bounds: Tuple[int, int, int],
+    clip_thresh: float = 0.01,
+):
+    """Project 2D Gaussians given by centre (NDC, [-1, 1]) and Cholesky factor
+    (l11, l21, l22) to pixel space.
+
+    Differentiable w.r.t. ``means2d`` and ``L_elements``.
+
+    Returns (xys [N,2], depths [N] (zeros), radii [N] int32, conics [N,3],
+    num_tiles_hit [N] int32).
+    """
+    return _ProjectGaussians2d.apply(
+        means2d.contiguous(),
+        L_elements.contiguous(),
+        img_height,
+        img_width,
+        tile_bounds,
+        clip_thresh,
+    )
+
+
+class _ProjectGaussians2d(Function):
+    """Project 2D gaussians (reference project_gaussians_2d.py:59-141)."""
+
+    @staticmethod
+    def forward(ctx, means2d, L_elements, img_height, img_width, tile_bounds, clip_thresh=0.01):
+        num_points = means2d.shape[-2]
+        xys, depths, radii, conics, num_tiles_hit = _C.project_gaussians_2d_forward(
+            num_points, means2d, L_elements, img_height, img_width, tile_bounds, clip_thresh)
+        ctx.img_height = img_height
+        ctx.img_width = img_width
+        ctx.num_points = num_points
+        ctx.save_for_backward(means2d, L_elements, radii, conics)
+        ctx.mark_non_differentiable(radii, num_tiles_hit)
+        return xys, depths, radii, conics, num_tiles_hit
+
+    @staticmethod
+    def backward(ctx, v_xys, v_depths, v_radii, v_conics, v_num_tiles_hit):
+        means2d, L_elements, radii, conics = ctx.saved_tensors
+        if v_xys is None:
+            v_xys = means2d.new_zeros((ctx.num_points, 2))
+        if v_conics is None:
+            v_conics = means2d.new_zeros((ctx.num_points, 3))
+        _v_cov2d, v_mean2d, v_L_elements = _C.project_gaussians_2d_backward(
+            ctx.num_points, means2d, L_elements, ctx.img_height, ctx.img_width, radii, conics,
+            v_xys, v_depths, v_conics)
+        return v_mean2d, v_L_elements, None, None, None, None

@@ -1,0 +1,158 @@
+"""Sum rasterizer operator (GSVC's renderer), same API as gsplat/gsplat/rasterize_sum.py.
+
+``rasterize_gaussians_sum`` (reference :14-86) and ``_RasterizeGaussiansSum``
+(reference :89-254) keep the reference's argument checks, M < 1 background
+branch, saved tensors and gradient routing.  Binning uses the fused hot path of
+``utils.bin_and_sort_for_raster``; the blend is gsvc_amd/csrc/raster_sum.hip.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+from torch import Tensor
+from torch.autograd import Function
+
+from . import ops as _C
+from .utils import bin_and_sort_for_raster
+
+
+def rasterize_gaussians_sum(
+    xys: Tensor,
+    depths: Tensor,
+    radii: Tensor,
+    conics: Tensor,
+    num_tiles_hit: Tensor,
+    colors: Tensor,
+    opacity: Tensor,
+    img_height: int,
+    img_width: int,
+    BLOCK_H: int = 16,
+    BLOCK_W: int = 16,
+    background: Optional[Tensor] = None,
+    return_alpha: Optional[bool] = False,
+):
+    """Rasterize 2D gaussians by summing colour * min(1, opacity * exp(-sigma))
+    over each tile's first 256 sorted splats (reference forward.cu:512-627).
+
+    Differentiable w.r.t. ``xys``, ``conics``, ``colors`` and ``opacity``.
+
+    Returns out_img [H, W, 3] (and out_alpha [H, W] = 1 - final_Ts = 0 when
+    ``return_alpha``).
+    """
+    if colors.dtype == torch.uint8:
+        colors = colors.float() / 255
+
+    if background is not None:
+        assert background.shape[0] == colors.shape[-1], (
+            f"incorrect shape of background color tensor, expected shape {colors.shape[-1]}")
+    else:
+        background = torch.ones(colors.shape[-1], dtype=torch.float32, device=colors.device)
+
+    if xys.ndimension() != 2 or xys.size(1) != 2:
+        raise ValueError("xys must have dimensions (N, 2)")
+
+    if colors.ndimension() != 2:
+        raise ValueError("colors must have dimensions (N, D)")
+
+    return _RasterizeGaussiansSum.apply(
+        xys.contiguous(),
+        depths.contiguous(),
+        radii.contiguous(),
+        conics.contiguous(),
+        num_tiles_hit.contiguous(),
+        colors.contiguous(),
+        opacity.contiguous(),
+        img_height,
+        img_width,
+        BLOCK_H,
+        BLOCK_W,
+        background.contiguous(),
+        return_alpha,
+    )
+
+
+class _RasterizeGaussiansSum(Function):
+    """Rasterizes 2D gaussians (reference rasterize_sum.py:89-254)."""
+
+    @staticmethod
+    def forward(ctx, xys, depths, radii, conics, num_tiles_hit, colors, opacity, img_height,
+                img_width, BLOCK_H=16, BLOCK_W=16, background=None, return_alpha=False):
+        num_points = xys.size(0)
+        BLOCK_X, BLOCK_Y = BLOCK_W, BLOCK_H
+        tile_bounds = ((img_width + BLOCK_X - 1) // BLOCK_X, (img_height + BLOCK_Y - 1) // BLOCK_Y, 1)
+        block = (BLOCK_X, BLOCK_Y, 1)
+        img_size = (img_width, img_height, 1)
+
+        if colors.shape[-1] != 3:
+            # the reference dispatched to _C.nd_rasterize_sum_forward, which its
+            # extension never exported (ext.cpp:6-23): AttributeError there too
+            raise AttributeError("nd_rasterize_sum_forward: only 3-channel colors are supported")
+
+        num_intersects, gaussian_ids_sorted, tile_bins = bin_and_sort_for_raster(
+            num_points, xys, depths, radii, num_tiles_hit, tile_bounds)
+
+        if num_intersects < 1:
+            out_img = (torch.ones(img_height, img_width, colors.shape[-1], device=xys.device)
+                       * background)
+            gaussian_ids_sorted = torch.zeros(0, 1, device=xys.device)
+            tile_bins = torch.zeros(0, 2, device=xys.device)
+            final_Ts = torch.zeros(img_height, img_width, device=xys.device)
+            final_idx = torch.zeros(img_height, img_width, device=xys.device)
+        else:
+            out_img, final_Ts, final_idx = _C.rasterize_sum_forward(
+                tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys, conics, colors,
+                opacity, background)
+
+        ctx.img_width = img_width
+        ctx.img_height = img_height
+        ctx.BLOCK_H = BLOCK_H
+        ctx.BLOCK_W = BLOCK_W
+        ctx.num_intersects = num_intersects
+        ctx.save_for_backward(gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
+                              background, final_Ts, final_idx)
+
+        if return_alpha:
+            out_alpha = 1 - final_Ts
+            return out_img, out_alpha
+        return out_img
+
+    @staticmethod
+    def backward(ctx, v_out_img, v_out_alpha=None):
+        img_height = ctx.img_height
+        img_width = ctx.img_width
+        num_intersects = ctx.num_intersects
+
+        if v_out_alpha is None:
+            v_out_alpha = torch.zeros_like(v_out_img[..., 0])
+
+        (gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background, final_Ts,
+         final_idx) = ctx.saved_tensors
+
+        if num_intersects < 1:
+            v_xy = torch.zeros_like(xys)
+            v_conic = torch.zeros_like(conics)
+            v_colors = torch.zeros_like(colors)
+            v_opacity = torch.zeros_like(opacity)
+        else:
+            v_xy, v_conic, v_colors, v_opacity = _C.rasterize_sum_backward(
+                img_height, img_width, ctx.BLOCK_H, ctx.BLOCK_W, gaussian_ids_sorted, tile_bins,
+                xys, conics, colors, opacity, background, final_Ts, final_idx, v_out_img,
+                v_out_alpha)
+            v_opacity = v_opacity.reshape(opacity.shape) if opacity.dim() != 2 else v_opacity
+
+        return (
+            v_xy,  # xys
+            None,  # depths
+            None,  # radii
+            v_conic,  # conics
+            None,  # num_tiles_hit
+            v_colors,  # colors
+            v_opacity,  # opacity
+            None,  # img_height
+            None,  # img_width
+            None,  # block_w
+            None,  # block_h
+            None,  # background
+            None,  # return_alpha
+        )

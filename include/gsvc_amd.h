@@ -1,0 +1,194 @@
+/*
+ * gsvc_amd.h -- C ABI of the MI355X-native 2D Gaussian-splat rasterizer.
+ *
+ * This is the drop-in boundary for the hot path of ac-freeman/GSVC: the ops
+ * that the reference's torch extension ``gsplat.csrc`` exports
+ * (gsplat/gsplat/cuda/csrc/ext.cpp:6-23, prototypes bindings.h:16-301) for the
+ * 2D path, plus the binning glue the reference ran in PyTorch
+ * (gsplat/gsplat/utils.py:99-167).  Every entry point takes plain device
+ * pointers and sizes; no torch types cross it.  The Python mirror of the
+ * reference operator API (gsvc_amd/, re-exported as the ``gsplat`` package)
+ * binds these with ctypes; INTEGRATION.md shows the binding a maintainer of
+ * the reference would add.
+ *
+ * Conventions
+ *   - All pointers are device (HBM) pointers unless stated otherwise.
+ *   - ``stream`` is a hipStream_t (NULL = legacy default stream); every entry
+ *     point is asynchronous on it and never synchronises the device, so calls
+ *     can be captured in a hipGraph.
+ *   - Return value: 0 on success, otherwise a gsvc_status code; the message of
+ *     the last failure on the calling thread is gsvc_last_error().  Bad
+ *     arguments are rejected before any launch (the reference raised
+ *     c10::Error through TORCH_CHECK / AT_ERROR, bindings.h:9-14).
+ *   - Outputs are fully written by the call (no caller-side zeroing needed)
+ *     unless a comment says otherwise.
+ *   - Images are row-major HWC float32, pixel (j, i) evaluated at (j, i).
+ *   - Only 16x16 tiles are supported (the reference kernels hard-code
+ *     BLOCK_X = BLOCK_Y = 16, config.h:1-4).
+ */
+#ifndef GSVC_AMD_H
+#define GSVC_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum gsvc_status {
+    GSVC_OK = 0,
+    GSVC_ERR_ARG = 1,       /* invalid argument (shape, size, tile size) */
+    GSVC_ERR_WORKSPACE = 2, /* workspace too small */
+    GSVC_ERR_HIP = 3        /* HIP runtime / launch error */
+};
+
+/* Library identity and error reporting. */
+int gsvc_abi_version(void);
+const char *gsvc_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * 2D projection.
+ * Replaces _C.project_gaussians_2d_forward
+ *   (bindings.cu:781-839 -> foward2d.cu:12-69; Python project_gaussians_2d.py:63-103).
+ * means2d [N,2], L_elements [N,3] (l11, l21, l22) in; xys [N,2], depths [N]
+ * (all 0), radii [N] int32, conics [N,3], num_tiles_hit [N] int32 out.
+ * clip_thresh is accepted and unused, as in the reference.
+ */
+int gsvc_project_gaussians_2d_forward(
+    int num_points, const float *means2d, const float *L_elements,
+    unsigned img_height, unsigned img_width,
+    int tile_bounds_x, int tile_bounds_y, int tile_bounds_z, float clip_thresh,
+    float *xys, float *depths, int *radii, float *conics, int *num_tiles_hit,
+    void *stream);
+
+/* Replaces _C.project_gaussians_2d_backward
+ *   (bindings.cu:902-949 -> backward2d.cu:8-51; Python project_gaussians_2d.py:105-141).
+ * v_depth is accepted and unused, as in the reference.  The L gradient keeps
+ * the reference's doubled off-diagonal term (backward2d.cu:39-41). */
+int gsvc_project_gaussians_2d_backward(
+    int num_points, const float *means2d, const float *L_elements,
+    unsigned img_height, unsigned img_width,
+    const int *radii, const float *conics,
+    const float *v_xy, const float *v_depth, const float *v_conic,
+    float *v_cov2d, float *v_mean2d, float *v_L_elements,
+    void *stream);
+
+/* Replaces _C.compute_cov2d_bounds (bindings.cu:41-60 -> :21-39).
+ * covs2d [N,3] upper-triangular in; conics [N,3], radii [N] float out. */
+int gsvc_compute_cov2d_bounds(int num_pts, const float *covs2d, float *conics,
+                              float *radii, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Binning.  Replaces the torch glue of utils.py:99-167 and the two binning
+ * ops _C.map_gaussian_to_intersects / _C.get_tile_bin_edges.
+ */
+
+/* torch.cumsum(num_tiles_hit, dtype=int32) of utils.py:116, plus a 4-int
+ * device record ``meta`` = {M = cum[N-1], OR of depth bits, AND of depth bits,
+ * splats with num_tiles_hit > 0} over the splats that emit intersections.
+ * ``depths`` may be NULL (then meta[1] = meta[2] = 0).  Reading meta[0] on the
+ * host is the one device->host sync of the forward (utils.py:117 ``.item()``). */
+size_t gsvc_cumsum_workspace_bytes(int num_points);
+int gsvc_compute_cumulative_intersects(
+    int num_points, const int *num_tiles_hit, const float *depths,
+    int *cum_tiles_hit, int *meta, void *workspace, size_t workspace_bytes,
+    void *stream);
+
+/* Replaces _C.map_gaussian_to_intersects (bindings.cu:274-313 -> forward.cu:100-136).
+ * isect_ids [M] int64 = tile_id << 32 | sign-extended depth bits, gaussian_ids [M] int32. */
+int gsvc_map_gaussian_to_intersects(
+    int num_points, int num_intersects, const float *xys, const float *depths,
+    const int *radii, const int *cum_tiles_hit,
+    int tile_bounds_x, int tile_bounds_y, int tile_bounds_z,
+    int64_t *isect_ids, int *gaussian_ids, void *stream);
+
+/* Replaces torch.sort(isect_ids) + torch.gather(gaussian_ids) (utils.py:164-165):
+ * stable LSD radix sort of signed int64 keys on bits [begin_bit, end_bit)
+ * (pass 0, 64 for a full sort).  Keys equal on those bits keep input order. */
+size_t gsvc_sort_pairs_workspace_bytes(int n);
+int gsvc_sort_isect_pairs(
+    int n, const int64_t *keys_in, const int *vals_in,
+    int64_t *keys_out, int *vals_out, int begin_bit, int end_bit,
+    void *workspace, size_t workspace_bytes, void *stream);
+
+/* Replaces _C.get_tile_bin_edges (bindings.cu:315-330 -> forward.cu:141-163).
+ * tile_bins [rows,2] int32 is zeroed then filled; rows must exceed every tile
+ * id present (the reference allocated M rows, which overflowed when M < tiles). */
+int gsvc_get_tile_bin_edges(int num_intersects, const int64_t *isect_ids_sorted,
+                            int *tile_bins, int rows, void *stream);
+
+/* Fused hot-path binning used by rasterize_gaussians_sum (utils.py:121-167 in
+ * one call): emit (tile, splat) pairs in splat order, stable radix sort on the
+ * ceil(log2(tiles)) tile bits only, and bin edges.  Valid when every emitting
+ * splat has the same depth bits (meta[1] == meta[2]; always true for the 2D
+ * projection, which writes depth 0), which makes the reference's 64-bit order
+ * equal to the tile order.  gaussian_ids_sorted [M]; tile_bins [rows,2] with
+ * rows >= tiles; isect_ids_sorted [M] optional (NULL to skip). */
+size_t gsvc_bin_tiles_workspace_bytes(int num_points, int num_intersects, int num_tiles);
+int gsvc_bin_and_sort_tiles(
+    int num_points, int num_intersects, const float *xys, const float *depths,
+    const int *radii, const int *cum_tiles_hit,
+    int tile_bounds_x, int tile_bounds_y,
+    int *gaussian_ids_sorted, int *tile_bins, int tile_bins_rows,
+    int64_t *isect_ids_sorted, void *workspace, size_t workspace_bytes,
+    void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Sum rasterizer (the GSVC renderer, rasterize_sum.py).
+ * Replaces _C.rasterize_sum_forward (bindings.cu:400-469 -> forward.cu:512-627):
+ * out[p] = sum over the first <= 256 sorted entries k of p's tile of
+ * colors[g_k] * min(1, opac[g_k] * exp(-sigma)), skipping sigma < 0 and
+ * alpha < 1/255; final_idx[p] = last contributing k (0 if none); final_Ts = 1.
+ * final_Ts may be NULL (it is identically 1; the Python layer returns an
+ * expanded constant).  background is accepted and unused, as in the reference. */
+int gsvc_rasterize_sum_forward(
+    int tile_bounds_x, int tile_bounds_y, int tile_bounds_z,
+    int block_x, int block_y, int block_z,
+    unsigned img_width, unsigned img_height, unsigned img_depth,
+    const int *gaussian_ids_sorted, const int *tile_bins,
+    const float *xys, const float *conics, const float *colors,
+    const float *opacities, const float *background,
+    float *out_img, float *final_Ts, int *final_idx, void *stream);
+
+/* Replaces _C.rasterize_sum_backward (bindings.cu:706-779 -> backward.cu:696-862).
+ * Gradients are written into one 64-byte record per splat,
+ * grad_records [N,16] float: [0:2] v_xy, [2:5] v_conic, [5:8] v_colors,
+ * [8] v_opacity, [9:16] unused (zeroed).  The Python layer returns strided
+ * views of it.  v_output [H,W,3]; v_output_alpha, background and final_Ts are
+ * accepted and unused, as in the reference sum kernel. */
+int gsvc_rasterize_sum_backward(
+    unsigned img_height, unsigned img_width, unsigned block_h, unsigned block_w,
+    int num_points, const int *gaussian_ids_sorted, const int *tile_bins,
+    const float *xys, const float *conics, const float *colors,
+    const float *opacities, const float *background, const float *final_Ts,
+    const int *final_idx, const float *v_output, const float *v_output_alpha,
+    float *grad_records, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Alpha-compositing rasterizer (rasterize.py; north_star's front-to-back path).
+ * Replaces _C.rasterize_forward (bindings.cu:332-398 -> forward.cu:252-374). */
+int gsvc_rasterize_forward(
+    int tile_bounds_x, int tile_bounds_y, int tile_bounds_z,
+    int block_x, int block_y, int block_z,
+    unsigned img_width, unsigned img_height, unsigned img_depth,
+    const int *gaussian_ids_sorted, const int *tile_bins,
+    const float *xys, const float *conics, const float *colors,
+    const float *opacities, const float *background,
+    float *out_img, float *final_Ts, int *final_idx, void *stream);
+
+/* Replaces _C.rasterize_backward (bindings.cu:631-704 -> backward.cu:138-315).
+ * Same grad_records layout as gsvc_rasterize_sum_backward. */
+int gsvc_rasterize_backward(
+    unsigned img_height, unsigned img_width, unsigned block_h, unsigned block_w,
+    int num_points, const int *gaussian_ids_sorted, const int *tile_bins,
+    const float *xys, const float *conics, const float *colors,
+    const float *opacities, const float *background, const float *final_Ts,
+    const int *final_idx, const float *v_output, const float *v_output_alpha,
+    float *grad_records, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSVC_AMD_H */

@@ -1,0 +1,244 @@
+"""ctypes/numpy wrapper around oracle/liboracle.so.
+
+TEST INFRASTRUCTURE ONLY: the parity checker for the HIP path.  Only tests/,
+``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg may import it.
+
+Every function mirrors one reference operator (paths relative to
+/root/reference/gsplat/gsplat):
+  project_2d_forward / backward   project_gaussians_2d.py:63-141 -> cuda/csrc/foward2d.cu, backward2d.cu
+  cumulative_intersects           utils.py:99-118
+  map_intersects                  utils.py:12-50 -> cuda/csrc/forward.cu:100-136
+  sort_pairs                      utils.py:164-165 (torch.sort + gather)
+  tile_bin_edges                  utils.py:53-74 -> cuda/csrc/forward.cu:141-163
+  bin_and_sort                    utils.py:121-167
+  raster_sum_forward / backward   rasterize_sum.py:92-254 -> forward.cu:512-627, backward.cu:696-862
+  raster_forward / backward       rasterize.py:89-253 -> forward.cu:252-374, backward.cu:138-315
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+F32 = np.float32
+I32 = np.int32
+I64 = np.int64
+F64 = np.float64
+
+
+def build() -> str:
+    """Compile liboracle.so with the committed Makefile (gcc)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH) or (
+            os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "oracle.c"))
+        ):
+            build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+    return _lib
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+def tile_bounds(img_h: int, img_w: int, block: int = 16):
+    return ((img_w + block - 1) // block, (img_h + block - 1) // block, 1)
+
+
+def project_2d_forward(means2d, L, img_h, img_w, tb):
+    means2d = _c(means2d, F32)
+    L = _c(L, F32)
+    n = means2d.shape[0]
+    xys = np.zeros((n, 2), F32)
+    depths = np.zeros((n,), F32)
+    radii = np.zeros((n,), I32)
+    conics = np.zeros((n, 3), F32)
+    nth = np.zeros((n,), I32)
+    lib().oracle_project_2d_forward(
+        ctypes.c_int(n), _p(means2d), _p(L), ctypes.c_int(img_h), ctypes.c_int(img_w),
+        ctypes.c_int(tb[0]), ctypes.c_int(tb[1]),
+        _p(xys), _p(depths), _p(radii), _p(conics), _p(nth))
+    return xys, depths, radii, conics, nth
+
+
+def project_2d_backward(L, img_h, img_w, radii, conics, v_xy, v_conic):
+    L = _c(L, F32)
+    radii = _c(radii, I32)
+    conics = _c(conics, F32)
+    v_xy = _c(v_xy, F32)
+    v_conic = _c(v_conic, F32)
+    n = L.shape[0]
+    v_cov2d = np.zeros((n, 3), F32)
+    v_mean2d = np.zeros((n, 2), F32)
+    v_L = np.zeros((n, 3), F32)
+    lib().oracle_project_2d_backward(
+        ctypes.c_int(n), _p(L), ctypes.c_int(img_h), ctypes.c_int(img_w), _p(radii), _p(conics),
+        _p(v_xy), _p(v_conic), _p(v_cov2d), _p(v_mean2d), _p(v_L))
+    return v_cov2d, v_mean2d, v_L
+
+
+def cov2d_bounds(covs):
+    covs = _c(covs, F32)
+    n = covs.shape[0]
+    conics = np.zeros((n, 3), F32)
+    radii = np.zeros((n, 1), F32)
+    lib().oracle_cov2d_bounds(ctypes.c_int(n), _p(covs), _p(conics), _p(radii))
+    return conics, radii
+
+
+def cumulative_intersects(num_tiles_hit):
+    """utils.py:99-118: int32 inclusive cumsum and its last element."""
+    cum = np.cumsum(np.asarray(num_tiles_hit, dtype=np.int64)).astype(I32)
+    m = int(cum[-1]) if cum.size else 0
+    return m, cum
+
+
+def map_intersects(xys, depths, radii, cum, tb, m):
+    xys = _c(xys, F32)
+    depths = _c(depths, F32)
+    radii = _c(radii, I32)
+    cum = _c(cum, I32)
+    n = xys.shape[0]
+    isect = np.zeros((m,), I64)
+    gids = np.zeros((m,), I32)
+    lib().oracle_map_intersects(
+        ctypes.c_int(n), _p(xys), _p(depths), _p(radii), _p(cum),
+        ctypes.c_int(tb[0]), ctypes.c_int(tb[1]), _p(isect), _p(gids))
+    return isect, gids
+
+
+def sort_pairs(keys, vals):
+    keys = _c(keys, I64)
+    vals = _c(vals, I32)
+    m = keys.shape[0]
+    ko = np.zeros((m,), I64)
+    vo = np.zeros((m,), I32)
+    lib().oracle_sort_pairs(ctypes.c_int(m), _p(keys), _p(vals), _p(ko), _p(vo))
+    return ko, vo
+
+
+def tile_bin_edges(isect_sorted, rows):
+    isect_sorted = _c(isect_sorted, I64)
+    bins = np.zeros((rows, 2), I32)
+    lib().oracle_tile_bin_edges(ctypes.c_int(isect_sorted.shape[0]), _p(isect_sorted), _p(bins),
+                                ctypes.c_int(rows))
+    return bins
+
+
+def bin_and_sort(xys, depths, radii, cum, tb, m):
+    """utils.py:121-167.  tile_bins gets max(M, num_tiles) rows."""
+    isect, gids = map_intersects(xys, depths, radii, cum, tb, m)
+    isect_sorted, gids_sorted = sort_pairs(isect, gids)
+    rows = max(m, tb[0] * tb[1])
+    bins = tile_bin_edges(isect_sorted, rows)
+    return isect, gids, isect_sorted, gids_sorted, bins
+
+
+def raster_sum_forward(tb, img_h, img_w, gids_sorted, bins, xys, conics, colors, opac):
+    out = np.zeros((img_h, img_w, 3), F32)
+    Ts = np.zeros((img_h, img_w), F32)
+    idx = np.zeros((img_h, img_w), I32)
+    args = [_c(gids_sorted, I32), _c(bins, I32), _c(xys, F32), _c(conics, F32),
+            _c(colors, F32), _c(opac, F32)]
+    lib().oracle_raster_sum_forward(
+        ctypes.c_int(tb[0]), ctypes.c_int(tb[1]), ctypes.c_int(img_w), ctypes.c_int(img_h),
+        *[_p(a) for a in args], _p(out), _p(Ts), _p(idx))
+    return out, Ts, idx
+
+
+def raster_sum_backward(tb, img_h, img_w, gids_sorted, bins, xys, conics, colors, opac,
+                        final_idx, v_out):
+    n = np.asarray(xys).shape[0]
+    v_xy = np.zeros((n, 2), F64)
+    v_conic = np.zeros((n, 3), F64)
+    v_rgb = np.zeros((n, 3), F64)
+    v_opac = np.zeros((n, 1), F64)
+    args = [_c(gids_sorted, I32), _c(bins, I32), _c(xys, F32), _c(conics, F32),
+            _c(colors, F32), _c(opac, F32), _c(final_idx, I32), _c(v_out, F32)]
+    lib().oracle_raster_sum_backward(
+        ctypes.c_int(tb[0]), ctypes.c_int(tb[1]), ctypes.c_int(img_w), ctypes.c_int(img_h),
+        ctypes.c_int(n), *[_p(a) for a in args], _p(v_xy), _p(v_conic), _p(v_rgb), _p(v_opac))
+    return v_xy, v_conic, v_rgb, v_opac
+
+
+def raster_forward(tb, img_h, img_w, gids_sorted, bins, xys, conics, colors, opac, bg):
+    out = np.zeros((img_h, img_w, 3), F32)
+    Ts = np.zeros((img_h, img_w), F32)
+    idx = np.zeros((img_h, img_w), I32)
+    args = [_c(gids_sorted, I32), _c(bins, I32), _c(xys, F32), _c(conics, F32),
+            _c(colors, F32), _c(opac, F32), _c(bg, F32)]
+    lib().oracle_raster_forward(
+        ctypes.c_int(tb[0]), ctypes.c_int(tb[1]), ctypes.c_int(img_w), ctypes.c_int(img_h),
+        *[_p(a) for a in args], _p(out), _p(Ts), _p(idx))
+    return out, Ts, idx
+
+
+def raster_backward(tb, img_h, img_w, gids_sorted, bins, xys, conics, colors, opac, bg,
+                    final_Ts, final_idx, v_out, v_out_alpha):
+    n = np.asarray(xys).shape[0]
+    v_xy = np.zeros((n, 2), F64)
+    v_conic = np.zeros((n, 3), F64)
+    v_rgb = np.zeros((n, 3), F64)
+    v_opac = np.zeros((n, 1), F64)
+    args = [_c(gids_sorted, I32), _c(bins, I32), _c(xys, F32), _c(conics, F32),
+            _c(colors, F32), _c(opac, F32), _c(bg, F32), _c(final_Ts, F32), _c(final_idx, I32),
+            _c(v_out, F32), _c(v_out_alpha, F32)]
+    lib().oracle_raster_backward(
+        ctypes.c_int(tb[0]), ctypes.c_int(tb[1]), ctypes.c_int(img_w), ctypes.c_int(img_h),
+        ctypes.c_int(n), *[_p(a) for a in args], _p(v_xy), _p(v_conic), _p(v_rgb), _p(v_opac))
+    return v_xy, v_conic, v_rgb, v_opac
+
+
+def sum_min_margin(tb, img_h, img_w, gids_sorted, bins, xys, conics, opac):
+    margin = np.full((img_h, img_w), np.inf, F32)
+    args = [_c(gids_sorted, I32), _c(bins, I32), _c(xys, F32), _c(conics, F32), _c(opac, F32)]
+    lib().oracle_sum_min_margin(
+        ctypes.c_int(tb[0]), ctypes.c_int(tb[1]), ctypes.c_int(img_w), ctypes.c_int(img_h),
+        *[_p(a) for a in args], _p(margin))
+    return margin
+
+
+def render_sum(means2d, L, colors, opac, img_h, img_w):
+    """The whole sum-path forward of GaussianSplats_Represent.py:83-90 (minus
+    clamp/permute): project -> cumsum -> bin/sort -> sum-rasterize."""
+    tb = tile_bounds(img_h, img_w)
+    xys, depths, radii, conics, nth = project_2d_forward(means2d, L, img_h, img_w, tb)
+    m, cum = cumulative_intersects(nth)
+    if m < 1:
+        return dict(out=np.ones((img_h, img_w, 3), F32), m=0, xys=xys, radii=radii,
+                    conics=conics, nth=nth)
+    isect, gids, isect_sorted, gids_sorted, bins = bin_and_sort(xys, depths, radii, cum, tb, m)
+    out, Ts, idx = raster_sum_forward(tb, img_h, img_w, gids_sorted, bins, xys, conics, colors, opac)
+    return dict(out=out, final_Ts=Ts, final_idx=idx, m=m, cum=cum, xys=xys, depths=depths,
+                radii=radii, conics=conics, nth=nth, isect=isect, gids=gids,
+                isect_sorted=isect_sorted, gids_sorted=gids_sorted, bins=bins, tb=tb)
+
+
+def synthetic_frame(n: int, seed: int, rgb_w: float = 1.0, chol_scale: float = 1.0):
+    """Reference init distributions (GaussianSplats_Represent.py:28-38,57-70) on a
+    seeded numpy RNG: means = tanh(atanh(2(u-.5))) = 2u-1, L = rand + [.5,0,.5],
+    colors = rand * rgb_W, opacity = 1."""
+    rng = np.random.default_rng(seed)
+    u = rng.random((n, 2), dtype=np.float32)
+    means = np.tanh(np.arctanh(2.0 * (u - 0.5))).astype(F32)
+    chol = (rng.random((n, 3), dtype=np.float32) * chol_scale
+            + np.array([0.5, 0.0, 0.5], F32) * chol_scale).astype(F32)
+    colors = (rng.random((n, 3), dtype=np.float32) * np.float32(rgb_w)).astype(F32)
+    opac = np.ones((n, 1), F32)
+    return means, chol, colors, opac
