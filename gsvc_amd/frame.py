@@ -1,0 +1,218 @@
+"""Per-frame model: a restatement of GSVC's caller of the hot path.
+
+``GaussianVideoFrame`` mirrors ``GaussianVideo_frame``
+(reference GaussianSplats_Represent.py:11-221): the same parameters and init
+distributions (:28-38), activations (:57-70), forward (:83-90: project ->
+sum-rasterize -> clamp -> NCHW), ``train_iter`` (:191-207: L2 loss, PSNR via
+``.item()``, Adan step, zero_grad, StepLR), and the prune / densify controls
+(:98-172).  It is used by bench.py, the tests and the video driver; GSVC's own
+file also runs unchanged on top of the ``gsplat`` drop-in package.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .adan import Adan
+from .project_gaussians_2d import project_gaussians_2d
+from .rasterize_sum import rasterize_gaussians_sum
+
+
+def loss_fn(pred, target, loss_type="L2", lambda_value=0.7):
+    """utils.py:21-41 for the losses that need no pytorch_msssim (absent here;
+    the SSIM variants are parity-unpinned and not provided)."""
+    target = target.detach()
+    pred = pred.float()
+    target = target.float()
+    if loss_type == "L2":
+        return F.mse_loss(pred, target)
+    if loss_type == "L1":
+        return F.l1_loss(pred, target)
+    if loss_type == "Fusion3":
+        return lambda_value * F.mse_loss(pred, target) + (1 - lambda_value) * F.l1_loss(pred, target)
+    raise NotImplementedError(f"loss_type {loss_type!r} needs pytorch_msssim (not available)")
+
+
+class GaussianVideoFrame(nn.Module):
+    def __init__(self, loss_type="L2", **kwargs):
+        super().__init__()
+        self.loss_type = loss_type
+        self.init_num_points = kwargs["num_points"]
+        self.max_num_points = kwargs["max_num_points"]
+        self.densification_interval = kwargs["densification_interval"]
+        self.iterations = kwargs["iterations"]
+        self.H, self.W = kwargs["H"], kwargs["W"]
+        self.BLOCK_W, self.BLOCK_H = kwargs["BLOCK_W"], kwargs["BLOCK_H"]
+        self.tile_bounds = ((self.W + self.BLOCK_W - 1) // self.BLOCK_W,
+                            (self.H + self.BLOCK_H - 1) // self.BLOCK_H, 1)
+        self.device = kwargs["device"]
+        self.removal_rate = kwargs["removal_rate"]
+        n = self.init_num_points
+        self._xyz = nn.Parameter(torch.atanh(2 * (torch.rand(n, 2) - 0.5)))
+        self._cholesky = nn.Parameter(torch.rand(n, 3))
+        self.isdensity = kwargs["isdensity"]
+        self.isremoval = kwargs["isremoval"]
+        if self.isremoval:
+            self.rgb_W = nn.Parameter(0.01 * torch.ones(n, 1))
+        elif self.isdensity:
+            self.rgb_W = nn.Parameter(torch.ones(n, 1))
+        else:
+            self.register_buffer("rgb_W", torch.ones((n, 1)))
+        self._features_dc = nn.Parameter(torch.rand(n, 3))
+        self.last_size = (self.H, self.W)
+        self.quantize = kwargs.get("quantize", False)
+        self.register_buffer("background", torch.ones(3))
+        self.register_buffer("bound", torch.tensor([0.5, 0.5]).view(1, 2))
+        self.register_buffer("cholesky_bound", torch.tensor([0.5, 0, 0.5]).view(1, 3))
+        self.lr = kwargs["lr"]
+        self.opt_type = kwargs["opt_type"]
+        self.fused_adan = kwargs.get("fused_adan", False)
+        self.update_optimizer()
+        self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=20000, gamma=0.5)
+
+    @property
+    def get_xyz(self):
+        return torch.tanh(self._xyz)
+
+    @property
+    def get_features(self):
+        return self._features_dc * self.get_rgb_W
+
+    @property
+    def get_rgb_W(self):
+        return self.rgb_W
+
+    @property
+    def get_cholesky_elements(self):
+        return self._cholesky + self.cholesky_bound
+
+    def forward(self):
+        _opacity = torch.ones(self._xyz.shape[0], 1).to(self.device)
+        self.xys, depths, self.radii, conics, num_tiles_hit = project_gaussians_2d(
+            self.get_xyz, self.get_cholesky_elements, self.H, self.W, self.tile_bounds)
+        out_img = rasterize_gaussians_sum(self.xys, depths, self.radii, conics, num_tiles_hit,
+                                          self.get_features, _opacity, self.H, self.W, self.BLOCK_H,
+                                          self.BLOCK_W, background=self.background,
+                                          return_alpha=False)
+        out_img = torch.clamp(out_img, 0, 1)
+        out_img = out_img.view(-1, self.H, self.W, 3).permute(0, 3, 1, 2).contiguous()
+        return {"render": out_img}
+
+    def update_optimizer(self):
+        if self.opt_type == "adam":
+            self.optimizer = torch.optim.Adam(self.parameters(), lr=self.lr)
+        else:
+            self.optimizer = Adan(self.parameters(), lr=self.lr, fused=self.fused_adan)
+
+    def _keep(self, keep):
+        with torch.no_grad():
+            self._xyz = nn.Parameter(self._xyz[keep])
+            self._cholesky = nn.Parameter(self._cholesky[keep])
+            self._features_dc = nn.Parameter(self._features_dc[keep])
+            self.rgb_W = nn.Parameter(self.rgb_W[keep])
+
+    def _remove_lowest(self, sorted_indices, remove_count):
+        keep = torch.ones(self._xyz.shape[0], dtype=torch.bool, device=self._xyz.device)
+        keep[sorted_indices[:remove_count]] = False
+        self._keep(keep)
+
+    def _refresh_groups(self):
+        for param_group in self.optimizer.param_groups:
+            param_group["params"] = [p for p in self.parameters() if p.requires_grad]
+
+    def removal_control(self, iter):
+        """GaussianSplats_Represent.py:98-128 (I-frame pruning)."""
+        iter_threshold_remove = 4000
+        if iter > iter_threshold_remove:
+            return
+        rgb_weight = torch.norm(self.rgb_W, dim=1)
+        _, sorted_indices = torch.sort(rgb_weight)
+        removal_rate_per_step = self.removal_rate / int(iter_threshold_remove / self.densification_interval)
+        if iter < iter_threshold_remove:
+            self._remove_lowest(sorted_indices, int(removal_rate_per_step * self.max_num_points))
+            self._refresh_groups()
+        elif iter == iter_threshold_remove:
+            remove_count = self._xyz.shape[0] - int(self.max_num_points * (1 - self.removal_rate))
+            if remove_count > 0:
+                self._remove_lowest(sorted_indices, remove_count)
+            self.update_optimizer()
+
+    def adaptive_control(self, iter):
+        """GaussianSplats_Represent.py:130-172 (P-frame densify then prune)."""
+        iter_threshold_remove = 500
+        iter_threshold_add = 500
+        densification_num = int(self.max_num_points * self.removal_rate)
+        if iter > iter_threshold_add + iter_threshold_remove or iter < iter_threshold_add:
+            if iter == 1 and densification_num > 0:
+                dev = self._xyz.device
+                new_xyz = torch.atanh(2 * (torch.rand(densification_num, 2) - 0.5)).to(dev)
+                new_cholesky = torch.rand(densification_num, 3).to(dev)
+                new_features_dc = torch.rand(densification_num, 3).to(dev)
+                new_rgb_W = 0.01 * torch.ones(densification_num, 1).to(dev)
+                self._xyz = nn.Parameter(torch.cat((self._xyz, new_xyz), dim=0))
+                self._cholesky = nn.Parameter(torch.cat((self._cholesky, new_cholesky), dim=0))
+                self._features_dc = nn.Parameter(torch.cat((self._features_dc, new_features_dc), dim=0))
+                self.rgb_W = nn.Parameter(torch.cat((self.rgb_W, new_rgb_W), dim=0))
+                self._refresh_groups()
+            return
+        rgb_weight = torch.norm(self.rgb_W, dim=1)
+        _, sorted_indices = torch.sort(rgb_weight)
+        if iter < iter_threshold_add + iter_threshold_remove:
+            remove_count = int(densification_num / int(iter_threshold_remove / self.densification_interval))
+            self._remove_lowest(sorted_indices, remove_count)
+            self._refresh_groups()
+        elif iter == iter_threshold_add + iter_threshold_remove:
+            remove_count = self._xyz.shape[0] - int(self.max_num_points * (1 - self.removal_rate))
+            if remove_count > 0:
+                self._remove_lowest(sorted_indices, remove_count)
+            self.update_optimizer()
+
+    def train_iter(self, gt_image, iter):
+        render_pkg = self.forward()
+        image = render_pkg["render"]
+        loss = loss_fn(image.squeeze(0), gt_image.squeeze(0), self.loss_type, lambda_value=0)
+        loss.backward()
+        with torch.no_grad():
+            mse_loss = F.mse_loss(image, gt_image)
+            psnr = 10 * math.log10(1.0 / mse_loss.item())
+        if (iter == 1 or iter % self.densification_interval == 0) and self.isdensity:
+            self.adaptive_control(iter)
+        elif iter % self.densification_interval == 0 and self.isremoval:
+            self.removal_control(iter)
+        self.optimizer.step()
+        self.optimizer.zero_grad(set_to_none=True)
+        self.scheduler.step()
+        return loss, psnr
+
+
+def make_frame_model(H, W, num_points, device, seed=None, lr=1e-3, isremoval=False,
+                     isdensity=False, removal_rate=0.1, max_num_points=None,
+                     densification_interval=100, fused_adan=False):
+    """Construct like SimpleTrainer2d does (train_video_Represent.py:51-55)."""
+    if seed is not None:
+        torch.manual_seed(seed)
+    model = GaussianVideoFrame(
+        loss_type="L2", opt_type="adan", num_points=num_points,
+        max_num_points=max_num_points or num_points, densification_interval=densification_interval,
+        iterations=30000, H=H, W=W, BLOCK_H=16, BLOCK_W=16, device=device, lr=lr, quantize=False,
+        removal_rate=removal_rate, isdensity=isdensity, isremoval=isremoval,
+        fused_adan=fused_adan).to(device)
+    return model
+
+
+def synthetic_gt(H, W, seed, device):
+    """Seeded smooth procedural RGB frame in [0, 1]: a sum of 8
+    random sinusoids per channel."""
+    g = torch.Generator().manual_seed(int(seed))
+    yy, xx = torch.meshgrid(torch.linspace(0, 1, H), torch.linspace(0, 1, W), indexing="ij")
+    chans = []
+    for _ in range(3):
+        acc = torch.zeros(H, W)
+        for _ in range(8):
+            fx, fy, ph = (torch.rand(3, generator=g) * torch.tensor([12.0, 12.0, 6.28])).tolist()
+            acc += torch.sin(fx * xx + fy * yy + ph)
+        chans.append(0.5 + 0.5 * acc / 8)
+    return torch.stack(chans)[None].clamp(0, 1).to(device)

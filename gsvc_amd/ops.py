@@ -27,6 +27,38 @@ from . import _lib as L
 
 TILE = 16
 
+# Optional live timing of the composite kernels (bench.py): when a list is
+# installed here, each rasterizer launch is bracketed by HIP events recorded on
+# the stream the kernel is launched on (torch's current stream).
+_kernel_events = None
+
+
+def enable_kernel_timing(on: bool = True):
+    """Start (or stop) recording (name, start_event, end_event) per rasterizer launch."""
+    global _kernel_events
+    _kernel_events = [] if on else None
+    return _kernel_events
+
+
+def kernel_times_ms(name: str):
+    """Durations in ms of the recorded launches of ``name`` (synchronizes)."""
+    if not _kernel_events:
+        return []
+    torch.cuda.synchronize()
+    return [s.elapsed_time(e) for n, s, e in _kernel_events if n == name]
+
+
+def _timed_call(sym, *args):
+    if _kernel_events is None:
+        L.call(sym, *args)
+        return
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    L.call(sym, *args)
+    e.record()
+    _kernel_events.append((sym, s, e))
+
 
 def _dev(t: torch.Tensor, name: str) -> None:
     if not isinstance(t, torch.Tensor):
@@ -230,7 +262,7 @@ def _raster_fwd(sym, tile_bounds, block, img_size, gaussian_ids_sorted, tile_bin
     out = torch.empty((img_h, img_w, 3), dtype=torch.float32, device=dev)
     idx = torch.empty((img_h, img_w), dtype=torch.int32, device=dev)
     Ts = torch.empty((img_h, img_w), dtype=torch.float32, device=dev) if want_Ts else None
-    L.call(sym, tb[0], tb[1], tb[2], blk[0], blk[1], blk[2], img_w, img_h, img_d, L.ptr(gids),
+    _timed_call(sym, tb[0], tb[1], tb[2], blk[0], blk[1], blk[2], img_w, img_h, img_d, L.ptr(gids),
            L.ptr(bins), L.ptr(xys), L.ptr(conics), L.ptr(colors), L.ptr(opacities),
            L.ptr(background), L.ptr(out), L.ptr(Ts), L.ptr(idx), L.stream(dev))
     return out, Ts, idx
@@ -280,7 +312,7 @@ def _raster_bwd(sym, img_height, img_width, BLOCK_H, BLOCK_W, gaussian_ids_sorte
                if sym == "gsvc_rasterize_backward" else None)
     n = xys.shape[0]
     rec = torch.empty((n, 16), dtype=torch.float32, device=xys.device)
-    L.call(sym, h, w, int(BLOCK_H), int(BLOCK_W), n, L.ptr(gids), L.ptr(bins), L.ptr(xys),
+    _timed_call(sym, h, w, int(BLOCK_H), int(BLOCK_W), n, L.ptr(gids), L.ptr(bins), L.ptr(xys),
            L.ptr(conics), L.ptr(colors), L.ptr(opacities), L.ptr(background), L.ptr(Ts),
            L.ptr(final_idx), L.ptr(v_output), L.ptr(v_alpha), L.ptr(rec), L.stream(xys.device))
     return split_grad_records(rec)
