@@ -176,7 +176,7 @@ def main():
         torch.cuda.synchronize()
         barrier(world)
         elapsed = time.perf_counter() - t0
-        kt = ops.kernel_times_ms("gsvc_rasterize_sum_forward")
+        kt = ops.kernel_times_ms("gsvc_rasterize_sum_forward_auto")
         ops.enable_kernel_timing(False)
         del events
     elapsed = all_max(elapsed, world, device)

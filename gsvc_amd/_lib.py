@@ -28,6 +28,7 @@ _SZ = ctypes.c_size_t
 _SIGS = {
     "gsvc_abi_version": [],
     "gsvc_last_error": [],
+    "gsvc_debug_set": [_I, _I],
     "gsvc_project_gaussians_2d_forward": [_I, _P, _P, _U, _U, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P],
     "gsvc_project_gaussians_2d_backward": [_I, _P, _P, _U, _U, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "gsvc_compute_cov2d_bounds": [_I, _P, _P, _P, _P],
@@ -41,6 +42,8 @@ _SIGS = {
     "gsvc_bin_and_sort_tiles": [_I, _I, _P, _P, _P, _P, _I, _I, _P, _P, _I, _P, _P, _SZ, _P],
     "gsvc_rasterize_sum_forward": [_I, _I, _I, _I, _I, _I, _U, _U, _U, _P, _P, _P, _P, _P, _P, _P,
                                    _P, _P, _P, _P],
+    "gsvc_rasterize_sum_forward_auto": [_I, _I, _I, _I, _I, _I, _I, _U, _U, _U, _P, _P, _P, _P, _P,
+                                        _P, _P, _P, _P, _P, _P],
     "gsvc_rasterize_sum_backward": [_U, _U, _U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                     _P, _P],
     "gsvc_rasterize_forward": [_I, _I, _I, _I, _I, _I, _U, _U, _U, _P, _P, _P, _P, _P, _P, _P,

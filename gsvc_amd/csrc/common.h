@@ -21,6 +21,7 @@ constexpr float kAlphaMin = 1.0f / 255.0f;
 // Host-side error plumbing -------------------------------------------------
 int set_error(int code, const char *fmt, ...);
 int check_launch(const char *what);
+extern int g_knobs[8];  // gsvc_debug_set(); knob 0 = sum-forward variant
 
 // XCD-aware block -> work-item remap.  Blocks b and b+8 share an XCD (they are
 // dealt round-robin over the 8 XCDs), so give each XCD a contiguous range of

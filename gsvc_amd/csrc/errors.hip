@@ -22,8 +22,17 @@ int check_launch(const char *what) {
     return GSVC_OK;
 }
 
+int g_knobs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
 }  // namespace gsvc
 
 extern "C" int gsvc_abi_version(void) { return 1; }
+
+extern "C" int gsvc_debug_set(int key, int value) {
+    if (key < 0 || key >= 8) return -1;
+    const int old = gsvc::g_knobs[key];
+    gsvc::g_knobs[key] = value;
+    return old;
+}
 
 extern "C" const char *gsvc_last_error(void) { return gsvc::g_last_error; }

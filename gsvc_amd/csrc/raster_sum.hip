@@ -11,13 +11,23 @@
 // transmittance, no background; final_idx = last contributing sorted index,
 // 0 if none; final_Ts = 1.
 //
-// Forward layout: one wave64 per 16x16 tile, each lane owns 4
-// consecutive pixels of one row (16 rows x 4 quads).  The tile's entries are
-// gathered 64 at a time into LDS (one lane per entry) and broadcast from LDS to
-// the wave; the row terms of sigma (0.5c dy^2, b dy) are shared by the lane's 4
-// pixels.  Each lane stores its 4 pixels as three 16-byte stores of RGB plus
-// one 16-byte store of final_idx.  The kernel is bound by the 16 B/pixel of
-// output (HBM) plus ~15 VALU per (pixel, entry) pair.
+// Forward layout: a 128-thread workgroup (2 waves) per 16x16
+// tile, chosen per tile from its entry count n:
+//   * sparse tile (n <= threshold, default 8): wave 0 blends the whole tile,
+//     each lane owning 4 consecutive pixels of one row; entries are gathered
+//     64 at a time into LDS (lane = entry) and broadcast to the wave; the row
+//     terms of sigma are shared by the lane's 4 pixels; wave 1 exits;
+//   * dense tile: each wave owns one 8-row band, 2 pixels per lane; per chunk
+//     of 64 entries each lane gathers one entry and tests whether its
+//     alpha >= 1/255 ellipse can reach the band at all (a conservative bbox
+//     test); survivors are compacted (ballot + popcount) into LDS in sorted
+//     order and blended with packed f32 math.  About half of the
+//     (entry, band) pairs are culled at 50k splats; a culled pair contributes
+//     nothing in the reference either, so results are identical.
+// Output: RGB staged through LDS and written as whole 192-byte tile rows;
+// final_idx as 16- or 8-byte groups.  The kernel is bound by the 16 B/pixel of
+// output plus the VALU of the surviving (pixel, entry) pairs (see the
+// timestamp and ablation measurements in DESIGN.md §5).
 //
 // Backward layout: one 256-thread workgroup per tile, ENTRY-parallel: with
 // n entries (E = next pow2 >= n) thread t handles entry t % E against the
@@ -31,42 +41,99 @@
 namespace gsvc {
 
 constexpr int kChunk = 64;
+constexpr int kSlice = kTilePix * 3 / 4;  // float4s of LDS per wave (3 KB)
 
-__global__ __launch_bounds__(64) void raster_sum_fwd_kernel(
-    int tbx, int img_w, int img_h, int ntiles, bool vec_store,
-    const int *__restrict__ ids, const int2 *__restrict__ bins, const float2 *__restrict__ xys,
-    const float *__restrict__ conics, const float *__restrict__ colors,
-    const float *__restrict__ opac, float *__restrict__ out, int *__restrict__ final_idx,
-    float *__restrict__ final_Ts) {
-    __shared__ float4 s_geo[kChunk];  // x, y, 0.5a, b
-    __shared__ float4 s_col[kChunk];  // 0.5c, opacity, r, g
-    __shared__ float s_blu[kChunk];   // b
-    const int tile = xcd_remap(blockIdx.x, ntiles);
-    const int ty = tile / tbx, tx = tile - ty * tbx;
-    const int lane = threadIdx.x;
+// Forward kernel modes.  Production: the launcher picks kModeSparse (one wave
+// per tile) when the frame averages <= 5 entries per tile and kModeBanded
+// (two waves per tile) above, from the intersection count the caller already
+// holds (gsvc_rasterize_sum_forward_auto).  gsvc_debug_set(0, mode) forces a
+// mode for tools/kbench.py:
+//   1 sparse path only     2 banded path only
+//   3 per-tile choice (2 waves per tile) with timestamps (diagnostic)
+//   4 banded, no blending  5 banded, no stores   (ablations)
+//   6 per-tile choice (2 waves per tile; threshold gsvc_debug_set(3, t))
+// A per-tile choice inside one launch was measured slower than either pure
+// mode: a 128-thread workgroup whose second wave exits at once still halves
+// the dispatch rate of sparse tiles.
+enum { kModeAdaptive = 6, kModeSparse = 1, kModeBanded = 2, kModeStamp = 3, kModeNoBlend = 4,
+       kModeNoStore = 5 };
+constexpr int kDenseEntriesPerTile = 5;
+
+__device__ __forceinline__ void wave_lds_sync() {
+    // a wave owns its LDS slice and LDS ops of a wave complete in order: a
+    // drain of lgkmcnt is the only fence needed (no s_barrier)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Diagnostic only (kModeStamp): s_memrealtime (100 MHz) stamps per tile,
+// written to the final_Ts slot reinterpreted as int64[ntiles][4].
+__device__ __forceinline__ long long stamp() {
+    long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+// Can splat (x, y, conic a b c, opacity o) reach alpha >= 1/255 on any pixel
+// centre of [x0, x1] x [y0, y1]?  false only when provably not: alpha >= 1/255
+// needs sigma <= ln(255 o), i.e. the point inside the ellipse
+// d^T C d <= 2 ln(255 o), whose half-extents are sqrt(2 ln(255 o) c / det) and
+// sqrt(2 ln(255 o) a / det); margins (0.1 % + 0.01) dwarf fp32 rounding.
+__device__ __forceinline__ bool ellipse_hits_rect(float x, float y, float a, float b, float c,
+                                                  float o, float x0, float x1, float y0, float y1) {
+    if (!(o > 0.0f)) return !(o <= 0.0f);  // o <= 0: alpha <= 0 never valid; NaN: keep
+    const float det = a * c - b * b;
+    if (!(a > 0.0f) || !(det > 0.0f) || !(o < 3.0e38f) || !(fabsf(x) < 1e30f) || !(fabsf(y) < 1e30f))
+        return true;  // not positive definite / non-finite: no culling
+    const float lg = __logf(255.0f * o);
+    if (lg < -0.01f) return false;  // o < e^-0.01 / 255: alpha < 1/255 everywhere
+    const float S2 = 2.0f * (lg * 1.001f + 0.01f);
+    const float ex = sqrtf(S2 * c / det) * 1.001f + 0.01f;
+    const float ey = sqrtf(S2 * a / det) * 1.001f + 0.01f;
+    return (x + ex >= x0) && (x - ex <= x1) && (y + ey >= y0) && (y - ey <= y1);
+}
+
+struct SumFwdArgs {
+    int tbx, img_w, img_h, ntiles, sparse_max;
+    bool vec;  // W % 4 == 0 and 16-byte aligned outputs
+    const int *ids;
+    const int2 *bins;
+    const float2 *xys;
+    const float *conics, *colors, *opac;
+    float *out;
+    int *final_idx;
+    float *final_Ts;
+};
+
+// Sparse path: one wave blends the whole 16x16 tile, 4 pixels per lane.
+template <int kMode>
+__device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, int2 range, int n,
+                                               float4 *s_slice) {
+    float4 *s_geo = s_slice;                           // x, y, 0.5a, b
+    float4 *s_col = s_slice + kChunk;                  // 0.5c, opacity, r, g
+    float *s_blu = (float *)(s_slice + 2 * kChunk);    // b
+    const int lane = threadIdx.x & 63;
+    const int ty = tile / A.tbx, tx = tile - ty * A.tbx;
     const int pi = ty * kTile + (lane >> 2);
     const int pj = tx * kTile + ((lane & 3) << 2);
     const float py = (float)pi;
     const float px0 = (float)pj, px1 = (float)(pj + 1), px2 = (float)(pj + 2), px3 = (float)(pj + 3);
-    const int2 range = bins[tile];
-    int n = range.y - range.x;
-    n = n > kTilePix ? kTilePix : (n < 0 ? 0 : n);
-
     float r0 = 0.f, g0 = 0.f, b0 = 0.f, r1 = 0.f, g1 = 0.f, b1 = 0.f;
     float r2 = 0.f, g2 = 0.f, b2 = 0.f, r3 = 0.f, g3 = 0.f, b3 = 0.f;
     int l0 = 0, l1 = 0, l2 = 0, l3 = 0;
-
     for (int base = 0; base < n; base += kChunk) {
         const int cnt = min(kChunk, n - base);
         if (lane < cnt) {
-            const int g = ids[range.x + base + lane];
-            const float2 xy = xys[g];
-            const float a = conics[3 * g], b = conics[3 * g + 1], c = conics[3 * g + 2];
+            const int g = A.ids[range.x + base + lane];
+            const float2 xy = A.xys[g];
+            const float a = A.conics[3 * g], b = A.conics[3 * g + 1], c = A.conics[3 * g + 2];
             s_geo[lane] = make_float4(xy.x, xy.y, 0.5f * a, b);
-            s_col[lane] = make_float4(0.5f * c, opac[g], colors[3 * g], colors[3 * g + 1]);
-            s_blu[lane] = colors[3 * g + 2];
+            s_col[lane] = make_float4(0.5f * c, A.opac[g], A.colors[3 * g], A.colors[3 * g + 1]);
+            s_blu[lane] = A.colors[3 * g + 2];
         }
-        __syncthreads();
+        wave_lds_sync();
         const int k0 = range.x + base;
         for (int t = 0; t < cnt; ++t) {
             const float4 G = s_geo[t];
@@ -93,32 +160,197 @@ __global__ __launch_bounds__(64) void raster_sum_fwd_kernel(
             GSVC_SUM_PIXEL(px3, r3, g3, b3, l3)
 #undef GSVC_SUM_PIXEL
         }
-        __syncthreads();
+        wave_lds_sync();
     }
-
-    if (pi >= img_h) return;
-    const size_t p0 = (size_t)pi * (size_t)img_w + (size_t)pj;
-    if (vec_store && pj + 3 < img_w) {
-        float4 *o = reinterpret_cast<float4 *>(out + 3 * p0);
-        o[0] = make_float4(r0, g0, b0, r1);
-        o[1] = make_float4(g1, b1, r2, g2);
-        o[2] = make_float4(b2, r3, g3, b3);
-        *reinterpret_cast<int4 *>(final_idx + p0) = make_int4(l0, l1, l2, l3);
-        if (final_Ts) *reinterpret_cast<float4 *>(final_Ts + p0) = make_float4(1.f, 1.f, 1.f, 1.f);
+    if (A.vec && (tx + 1) * kTile <= A.img_w) {
+        // stage the tile's 3 KB of RGB (lane l owns floats 12l..12l+11, a
+        // conflict-free 48-byte stride), then write 16-byte chunk c = 64j + lane
+        // = row c / 12, column chunk c % 12: whole 192-byte rows per instruction
+        s_slice[3 * lane] = make_float4(r0, g0, b0, r1);
+        s_slice[3 * lane + 1] = make_float4(g1, b1, r2, g2);
+        s_slice[3 * lane + 2] = make_float4(b2, r3, g3, b3);
+        wave_lds_sync();
+        const size_t tile_base = ((size_t)(ty * kTile) * (size_t)A.img_w + (size_t)(tx * kTile)) * 3;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int c = j * 64 + lane;
+            const int row = c / 12, cc = c - row * 12;
+            if (ty * kTile + row < A.img_h)
+                *reinterpret_cast<float4 *>(A.out + tile_base + (size_t)row * A.img_w * 3 + cc * 4) =
+                    s_slice[c];
+        }
+        if (pi < A.img_h) {
+            const size_t p0 = (size_t)pi * (size_t)A.img_w + (size_t)pj;
+            *reinterpret_cast<int4 *>(A.final_idx + p0) = make_int4(l0, l1, l2, l3);
+            if (A.final_Ts && kMode != kModeStamp)
+                *reinterpret_cast<float4 *>(A.final_Ts + p0) = make_float4(1.f, 1.f, 1.f, 1.f);
+        }
         return;
     }
+    if (pi >= A.img_h) return;
     const float rr[4] = {r0, r1, r2, r3}, gg[4] = {g0, g1, g2, g3}, bb[4] = {b0, b1, b2, b3};
     const int ll[4] = {l0, l1, l2, l3};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        if (pj + q < img_w) {
-            const size_t p = p0 + q;
-            out[3 * p] = rr[q];
-            out[3 * p + 1] = gg[q];
-            out[3 * p + 2] = bb[q];
-            final_idx[p] = ll[q];
-            if (final_Ts) final_Ts[p] = 1.0f;
+        if (pj + q < A.img_w) {
+            const size_t p = (size_t)pi * (size_t)A.img_w + (size_t)(pj + q);
+            A.out[3 * p] = rr[q];
+            A.out[3 * p + 1] = gg[q];
+            A.out[3 * p + 2] = bb[q];
+            A.final_idx[p] = ll[q];
+            if (A.final_Ts && kMode != kModeStamp) A.final_Ts[p] = 1.0f;
         }
+    }
+}
+
+// Dense path: this wave blends one 8-row band, 2 pixels per lane.
+template <int kMode>
+__device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int band, int2 range,
+                                             int n, float4 *s_slice) {
+    float4 *s_geo = s_slice;                                      // x, y, 0.5a, b
+    float4 *s_col = s_slice + kChunk;                             // 0.5c, opacity, r, g
+    float *s_blu = reinterpret_cast<float *>(s_slice + 2 * kChunk);
+    int *s_k = reinterpret_cast<int *>(s_slice + 2 * kChunk + kChunk / 4);
+    const int lane = threadIdx.x & 63;
+    const int ty = tile / A.tbx, tx = tile - ty * A.tbx;
+    const int row0 = ty * kTile + band * 8;
+    const int pi = row0 + (lane >> 3);
+    const int pj = tx * kTile + ((lane & 7) << 1);
+    const float py = (float)pi;
+    const v2f pxv = {(float)pj, (float)(pj + 1)};
+    const float bx0 = (float)(tx * kTile), by0 = (float)row0;
+    if (kMode == kModeNoBlend) n = 0;
+    v2f ar = {0.f, 0.f}, ag = {0.f, 0.f}, ab = {0.f, 0.f};
+    int l0 = 0, l1 = 0;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int base = 0; base < n; base += kChunk) {
+        const int j = base + lane;
+        bool keep = false;
+        float4 geo = make_float4(0.f, 0.f, 0.f, 0.f), col = geo;
+        float blu = 0.f;
+        if (j < n) {
+            const int g = A.ids[range.x + j];
+            const float2 xy = A.xys[g];
+            const float a = A.conics[3 * g], b = A.conics[3 * g + 1], c = A.conics[3 * g + 2];
+            const float o = A.opac[g];
+            geo = make_float4(xy.x, xy.y, 0.5f * a, b);
+            col = make_float4(0.5f * c, o, A.colors[3 * g], A.colors[3 * g + 1]);
+            blu = A.colors[3 * g + 2];
+            keep = ellipse_hits_rect(xy.x, xy.y, a, b, c, o, bx0, bx0 + 15.0f, by0, by0 + 7.0f);
+        }
+        const unsigned long long m = __ballot(keep);
+        if (keep) {
+            const int pos = __popcll(m & lt);
+            s_geo[pos] = geo;
+            s_col[pos] = col;
+            s_blu[pos] = blu;
+            s_k[pos] = range.x + j;
+        }
+        const int cnt = __popcll(m);
+        wave_lds_sync();
+        for (int t = 0; t < cnt; ++t) {
+            const float4 G = s_geo[t];
+            const float4 C = s_col[t];
+            const float bl = s_blu[t];
+            const int k = s_k[t];
+            const float dy = G.y - py;
+            const float cq = (C.x * dy) * dy;
+            const float bdy = G.w * dy;
+            const v2f dx = G.x - pxv;
+            const v2f q = __builtin_elementwise_fma((v2f)G.z, dx, (v2f)bdy);
+            const v2f sg = __builtin_elementwise_fma(q, dx, (v2f)cq);
+            const v2f x = sg * kNegLog2e;
+            const v2f e = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+            const v2f al = C.y * e;
+            const float a0 = fminf(1.0f, al.x), a1 = fminf(1.0f, al.y);
+            const bool v0 = !(sg.x < 0.0f) && !(a0 < kAlphaMin);
+            const bool v1 = !(sg.y < 0.0f) && !(a1 < kAlphaMin);
+            // fmaf(c, 0, acc) == acc for finite c: a select on alpha keeps the
+            // oracle's op sequence for the valid pairs
+            const v2f wv = {v0 ? a0 : 0.0f, v1 ? a1 : 0.0f};
+            ar = __builtin_elementwise_fma((v2f)C.z, wv, ar);
+            ag = __builtin_elementwise_fma((v2f)C.w, wv, ag);
+            ab = __builtin_elementwise_fma((v2f)bl, wv, ab);
+            l0 = v0 ? k : l0;
+            l1 = v1 ? k : l1;
+        }
+        wave_lds_sync();
+    }
+    if (kMode == kModeNoStore) {
+        asm volatile("" ::"v"(ar.x), "v"(ar.y), "v"(ag.x), "v"(ag.y), "v"(ab.x), "v"(ab.y), "v"(l0),
+                     "v"(l1));
+        return;
+    }
+    if (A.vec && (tx + 1) * kTile <= A.img_w) {
+        // stage 8 rows x 16 px x 12 B = 1536 B (lane l owns floats 6l..6l+5),
+        // then 96 16-byte chunks as whole 192-byte rows; final_idx as pairs
+        float2 *so2 = reinterpret_cast<float2 *>(s_slice);
+        so2[3 * lane] = make_float2(ar.x, ag.x);
+        so2[3 * lane + 1] = make_float2(ab.x, ar.y);
+        so2[3 * lane + 2] = make_float2(ag.y, ab.y);
+        wave_lds_sync();
+        const size_t base_off = ((size_t)row0 * (size_t)A.img_w + (size_t)(tx * kTile)) * 3;
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            const int c = jj * 64 + lane;
+            if (c < 96) {
+                const int row = c / 12, cc = c - row * 12;
+                if (row0 + row < A.img_h)
+                    *reinterpret_cast<float4 *>(A.out + base_off + (size_t)row * A.img_w * 3 + cc * 4) =
+                        s_slice[c];
+            }
+        }
+        if (pi < A.img_h) {
+            const size_t p0 = (size_t)pi * (size_t)A.img_w + (size_t)pj;
+            *reinterpret_cast<int2 *>(A.final_idx + p0) = make_int2(l0, l1);
+            if (A.final_Ts && kMode != kModeStamp)
+                *reinterpret_cast<float2 *>(A.final_Ts + p0) = make_float2(1.f, 1.f);
+        }
+        return;
+    }
+    if (pi >= A.img_h) return;
+    const float rr[2] = {ar.x, ar.y}, gg[2] = {ag.x, ag.y}, bb[2] = {ab.x, ab.y};
+    const int ll[2] = {l0, l1};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        if (pj + q < A.img_w) {
+            const size_t p = (size_t)pi * (size_t)A.img_w + (size_t)(pj + q);
+            A.out[3 * p] = rr[q];
+            A.out[3 * p + 1] = gg[q];
+            A.out[3 * p + 2] = bb[q];
+            A.final_idx[p] = ll[q];
+            if (A.final_Ts && kMode != kModeStamp) A.final_Ts[p] = 1.0f;
+        }
+    }
+}
+
+// kModeSparse launches 64-thread workgroups (one wave per tile); every other
+// mode 128-thread workgroups (two waves per tile).
+template <int kMode>
+__global__ __launch_bounds__(kMode == kModeSparse ? 64 : 128, 8) void raster_sum_fwd_kernel(
+    SumFwdArgs A) {
+    __shared__ float4 s_buf[kMode == kModeSparse ? 1 : 2][kSlice];
+    const int w = (kMode == kModeSparse) ? 0 : (threadIdx.x >> 6);
+    const int tile = xcd_remap(blockIdx.x, A.ntiles);
+    long long t0 = 0;
+    if (kMode == kModeStamp) t0 = stamp();
+    const int2 range = A.bins[tile];
+    int n = range.y - range.x;
+    n = n > kTilePix ? kTilePix : (n < 0 ? 0 : n);
+    const int ty = tile / A.tbx;
+    const bool sparse = kMode == kModeSparse ||
+                        ((kMode == kModeAdaptive || kMode == kModeStamp) && n <= A.sparse_max);
+    if (sparse) {
+        if (w != 0) return;
+        sum_fwd_sparse<kMode>(A, tile, range, n, s_buf[0]);
+    } else {
+        if (ty * kTile + w * 8 >= A.img_h) return;  // band below the image
+        sum_fwd_band<kMode>(A, tile, w, range, n, s_buf[w]);
+    }
+    if (kMode == kModeStamp && (threadIdx.x & 63) == 0) {
+        long long *st = reinterpret_cast<long long *>(A.final_Ts) + 4 * (size_t)tile;
+        st[w == 0 ? 0 : 2] = t0;
+        st[w == 0 ? 1 : 3] = stamp();
     }
 }
 
@@ -266,6 +498,63 @@ static int check_tiles(const char *what, int bx, int by, int tbx, int tby, unsig
     return GSVC_OK;
 }
 
+extern "C" int gsvc_rasterize_sum_forward_auto(
+    int num_intersects, int tbx, int tby, int tbz, int block_x, int block_y, int block_z,
+    unsigned img_width, unsigned img_height, unsigned img_depth, const int *gaussian_ids_sorted,
+    const int *tile_bins, const float *xys, const float *conics, const float *colors,
+    const float *opacities, const float *background, float *out_img, float *final_Ts,
+    int *final_idx, void *stream) {
+    (void)tbz; (void)block_z; (void)img_depth; (void)background;
+    int rc = check_tiles("rasterize_sum_forward", block_x, block_y, tbx, tby, img_width, img_height);
+    if (rc) return rc;
+    const int ntiles = tbx * tby;
+    if (ntiles == 0) return GSVC_OK;
+    SumFwdArgs A;
+    A.tbx = tbx;
+    A.img_w = (int)img_width;
+    A.img_h = (int)img_height;
+    A.ntiles = ntiles;
+    A.sparse_max = g_knobs[3] > 0 ? g_knobs[3] : 8;
+    A.vec = (img_width % 4 == 0) && (((uintptr_t)out_img & 15) == 0) &&
+            (((uintptr_t)final_idx & 15) == 0) && (((uintptr_t)final_Ts & 15) == 0);
+    A.ids = gaussian_ids_sorted;
+    A.bins = (const int2 *)tile_bins;
+    A.xys = (const float2 *)xys;
+    A.conics = conics;
+    A.colors = colors;
+    A.opac = opacities;
+    A.out = out_img;
+    A.final_idx = final_idx;
+    A.final_Ts = final_Ts;
+    hipStream_t s = (hipStream_t)stream;
+    int mode = g_knobs[0];
+    if (mode == 0)
+        mode = (num_intersects > kDenseEntriesPerTile * ntiles) ? kModeBanded : kModeSparse;
+    switch (mode) {
+        case kModeSparse:
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeSparse>, dim3(ntiles), dim3(64), 0, s, A);
+            break;
+        case kModeBanded:
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeBanded>, dim3(ntiles), dim3(128), 0, s, A);
+            break;
+        case kModeStamp:
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeStamp>, dim3(ntiles), dim3(128), 0, s, A);
+            break;
+        case kModeNoBlend:
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeNoBlend>, dim3(ntiles), dim3(128), 0, s, A);
+            break;
+        case kModeNoStore:
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeNoStore>, dim3(ntiles), dim3(128), 0, s, A);
+            break;
+        case kModeAdaptive:
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeAdaptive>, dim3(ntiles), dim3(128), 0, s, A);
+            break;
+        default:
+            return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: unknown kernel mode %d", mode);
+    }
+    return check_launch("rasterize_sum_forward");
+}
+
 extern "C" int gsvc_rasterize_sum_forward(int tbx, int tby, int tbz, int block_x, int block_y,
                                           int block_z, unsigned img_width, unsigned img_height,
                                           unsigned img_depth, const int *gaussian_ids_sorted,
@@ -273,18 +562,11 @@ extern "C" int gsvc_rasterize_sum_forward(int tbx, int tby, int tbz, int block_x
                                           const float *colors, const float *opacities,
                                           const float *background, float *out_img, float *final_Ts,
                                           int *final_idx, void *stream) {
-    (void)tbz; (void)block_z; (void)img_depth; (void)background;
-    int rc = check_tiles("rasterize_sum_forward", block_x, block_y, tbx, tby, img_width, img_height);
-    if (rc) return rc;
-    const int ntiles = tbx * tby;
-    if (ntiles == 0) return GSVC_OK;
-    const bool vec = (img_width % 4 == 0) && (((uintptr_t)out_img & 15) == 0) &&
-                     (((uintptr_t)final_idx & 15) == 0) && (((uintptr_t)final_Ts & 15) == 0);
-    hipLaunchKernelGGL(raster_sum_fwd_kernel, dim3(ntiles), dim3(64), 0, (hipStream_t)stream, tbx,
-                       (int)img_width, (int)img_height, ntiles, vec, gaussian_ids_sorted,
-                       (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacities,
-                       out_img, final_idx, final_Ts);
-    return check_launch("rasterize_sum_forward");
+    // without the intersection count the sparse path is the safe default
+    return gsvc_rasterize_sum_forward_auto(0, tbx, tby, tbz, block_x, block_y, block_z, img_width,
+                                           img_height, img_depth, gaussian_ids_sorted, tile_bins,
+                                           xys, conics, colors, opacities, background, out_img,
+                                           final_Ts, final_idx, stream);
 }
 
 extern "C" int gsvc_rasterize_sum_backward(unsigned img_height, unsigned img_width, unsigned block_h,

@@ -245,7 +245,7 @@ def _bins_for(tile_bins: torch.Tensor, ntiles: int) -> torch.Tensor:
 
 
 def _raster_fwd(sym, tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys, conics,
-                colors, opacities, background, want_Ts):
+                colors, opacities, background, want_Ts, num_intersects=None):
     tb = _tb(tile_bounds)
     blk = _tb(block)
     img_w, img_h, img_d = (int(x) for x in img_size)
@@ -262,17 +262,22 @@ def _raster_fwd(sym, tile_bounds, block, img_size, gaussian_ids_sorted, tile_bin
     out = torch.empty((img_h, img_w, 3), dtype=torch.float32, device=dev)
     idx = torch.empty((img_h, img_w), dtype=torch.int32, device=dev)
     Ts = torch.empty((img_h, img_w), dtype=torch.float32, device=dev) if want_Ts else None
-    _timed_call(sym, tb[0], tb[1], tb[2], blk[0], blk[1], blk[2], img_w, img_h, img_d, L.ptr(gids),
-           L.ptr(bins), L.ptr(xys), L.ptr(conics), L.ptr(colors), L.ptr(opacities),
-           L.ptr(background), L.ptr(out), L.ptr(Ts), L.ptr(idx), L.stream(dev))
+    hint = () if num_intersects is None else (int(num_intersects),)
+    _timed_call(sym, *hint, tb[0], tb[1], tb[2], blk[0], blk[1], blk[2], img_w, img_h, img_d,
+                L.ptr(gids), L.ptr(bins), L.ptr(xys), L.ptr(conics), L.ptr(colors),
+                L.ptr(opacities), L.ptr(background), L.ptr(out), L.ptr(Ts), L.ptr(idx),
+                L.stream(dev))
     return out, Ts, idx
 
 
 def rasterize_sum_forward(tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys,
-                          conics, colors, opacities, background):
-    out, _, idx = _raster_fwd("gsvc_rasterize_sum_forward", tile_bounds, block, img_size,
-                              gaussian_ids_sorted, tile_bins, xys, conics, colors, opacities,
-                              background, want_Ts=False)
+                          conics, colors, opacities, background, num_intersects=None):
+    """``num_intersects`` (optional, beyond the reference signature) lets the
+    launcher pick the kernel for the frame's density (identical results)."""
+    sym = "gsvc_rasterize_sum_forward" if num_intersects is None else "gsvc_rasterize_sum_forward_auto"
+    out, _, idx = _raster_fwd(sym, tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins,
+                              xys, conics, colors, opacities, background, want_Ts=False,
+                              num_intersects=num_intersects)
     final_Ts = torch.ones((1, 1), dtype=torch.float32, device=out.device).expand(out.shape[0],
                                                                               out.shape[1])
     return out, final_Ts, idx

@@ -102,7 +102,7 @@ class _RasterizeGaussiansSum(Function):
         else:
             out_img, final_Ts, final_idx = _C.rasterize_sum_forward(
                 tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys, conics, colors,
-                opacity, background)
+                opacity, background, num_intersects=num_intersects)
 
         ctx.img_width = img_width
         ctx.img_height = img_height

@@ -47,6 +47,12 @@ enum gsvc_status {
 int gsvc_abi_version(void);
 const char *gsvc_last_error(void);
 
+/* Tuning / A-B knob for kernel variants (tools/kbench.py).  key 0 forces the
+ * sum-forward kernel mode (0 = automatic), key 3 the per-tile threshold of
+ * mode 6; returns the previous value.  Not part of the reference interface;
+ * results are identical for every value (modes 4/5 are ablations). */
+int gsvc_debug_set(int key, int value);
+
 /* ---------------------------------------------------------------------------
  * 2D projection.
  * Replaces _C.project_gaussians_2d_forward
@@ -144,6 +150,19 @@ int gsvc_bin_and_sort_tiles(
  * expanded constant).  background is accepted and unused, as in the reference. */
 int gsvc_rasterize_sum_forward(
     int tile_bounds_x, int tile_bounds_y, int tile_bounds_z,
+    int block_x, int block_y, int block_z,
+    unsigned img_width, unsigned img_height, unsigned img_depth,
+    const int *gaussian_ids_sorted, const int *tile_bins,
+    const float *xys, const float *conics, const float *colors,
+    const float *opacities, const float *background,
+    float *out_img, float *final_Ts, int *final_idx, void *stream);
+
+/* Same op with the frame's intersection count as a density hint: frames
+ * averaging more than 5 entries per tile use the banded two-waves-per-tile
+ * kernel with ellipse culling, sparser frames one wave per tile (the plain
+ * entry point uses the latter).  Results are identical either way. */
+int gsvc_rasterize_sum_forward_auto(
+    int num_intersects, int tile_bounds_x, int tile_bounds_y, int tile_bounds_z,
     int block_x, int block_y, int block_z,
     unsigned img_width, unsigned img_height, unsigned img_depth,
     const int *gaussian_ids_sorted, const int *tile_bins,
