@@ -13,7 +13,7 @@ collective (weak scaling); ranks only all-reduce their timings.
 
 Reported beside the primary value:
   roofline      composite kernel (rasterize_sum_forward): algorithmic bytes per
-                launch (36 N_vis + 4 M_eff + 8 T + 16 P) over its
+                launch (36 N_vis + 4 M_eff + 8 T + 12 P) over its
                 average duration from HIP events on its stream, vs 8 TB/s;
                 ``traffic`` = PMC HBM bytes per launch from profiles/ (rocprofv3).
   cpu_baseline  the CPU oracle (oracle/oracle.c, single thread) rendering the
@@ -79,7 +79,9 @@ def all_max(x, world, device):
 
 
 def composite_bytes(model):
-    """SURVEY §8d B_fwd = 36 N_vis + 4 M_eff + 8 T + 16 P for the last forward."""
+    """SURVEY §8d B_fwd = 36 N_vis + 4 M_eff + 8 T + 12 P for the render
+    (inference) forward: the [3,H,W] clamped image is written once and no
+    final_idx (the 16 P of the autograd forward counts its 4 B/px final_idx)."""
     from gsvc_amd import ops
     from gsvc_amd.utils import bin_and_sort_for_raster
     with torch.no_grad():
@@ -93,7 +95,7 @@ def composite_bytes(model):
         n_vis = int((nth > 0).sum())
     T = model.tile_bounds[0] * model.tile_bounds[1]
     P = H * W
-    return 36 * n_vis + 4 * m_eff + 8 * T + 16 * P, dict(N_vis=n_vis, M=m, M_eff=m_eff, T=T, P=P)
+    return 36 * n_vis + 4 * m_eff + 8 * T + 12 * P, dict(N_vis=n_vis, M=m, M_eff=m_eff, T=T, P=P)
 
 
 def load_traffic(n_splats):
@@ -176,7 +178,7 @@ def main():
         torch.cuda.synchronize()
         barrier(world)
         elapsed = time.perf_counter() - t0
-        kt = ops.kernel_times_ms("gsvc_rasterize_sum_forward_auto")
+        kt = ops.kernel_times_ms("gsvc_rasterize_sum_forward_ex")
         ops.enable_kernel_timing(False)
         del events
     elapsed = all_max(elapsed, world, device)

@@ -39,11 +39,13 @@ _SIGS = {
     "gsvc_sort_isect_pairs": [_I, _P, _P, _P, _P, _I, _I, _P, _SZ, _P],
     "gsvc_get_tile_bin_edges": [_I, _P, _P, _I, _P],
     "gsvc_bin_tiles_workspace_bytes": [_I, _I, _I],
+    "gsvc_bin_tiles_counted_workspace_bytes": [_I],
+    "gsvc_bin_tiles_counted": [_I, _P, _P, _I, _I, ctypes.c_longlong, _P, _P, _P, _P, _P, _SZ, _P],
     "gsvc_bin_and_sort_tiles": [_I, _I, _P, _P, _P, _P, _I, _I, _P, _P, _I, _P, _P, _SZ, _P],
     "gsvc_rasterize_sum_forward": [_I, _I, _I, _I, _I, _I, _U, _U, _U, _P, _P, _P, _P, _P, _P, _P,
                                    _P, _P, _P, _P],
-    "gsvc_rasterize_sum_forward_auto": [_I, _I, _I, _I, _I, _I, _I, _U, _U, _U, _P, _P, _P, _P, _P,
-                                        _P, _P, _P, _P, _P, _P],
+    "gsvc_rasterize_sum_forward_ex": [_I, _I, _I, _I, _I, _I, _U, _U, _U, _P, _P, _P, _P, _P, _P,
+                                      _P, _P, _I, _I, _P, _P, _P, _P],
     "gsvc_rasterize_sum_backward": [_U, _U, _U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                     _P, _P],
     "gsvc_rasterize_forward": [_I, _I, _I, _I, _I, _I, _U, _U, _U, _P, _P, _P, _P, _P, _P, _P,
@@ -56,6 +58,7 @@ _RESTYPE = {
     "gsvc_cumsum_workspace_bytes": _SZ,
     "gsvc_sort_pairs_workspace_bytes": _SZ,
     "gsvc_bin_tiles_workspace_bytes": _SZ,
+    "gsvc_bin_tiles_counted_workspace_bytes": _SZ,
 }
 
 ABI_VERSION = 1

@@ -372,6 +372,155 @@ __global__ __launch_bounds__(256) void expand_isect_kernel(int n, const unsigned
 }
 
 // ---------------------------------------------------------------------------
+// Sync-free tile-major binning.  The (tile, splat) list sorted
+// by (tile, splat id) is the transpose of the splat -> tiles incidence, so it
+// is built as a CSR transpose instead of a sort:
+//   count   per splat, one atomic increment per tile of its bbox;
+//   scan    one workgroup: tile_bins = [start, end) (0,0 when empty), the
+//           fill cursors, and M on the device (no host round trip);
+//   fill    per splat, slot = atomic cursor bump, ids[slot] = splat
+//           (order inside a tile depends on atomic timing);
+//   sort    per tile, the segment is put in splat-id order: shuffle ranks
+//           for <= 64 entries, an LDS bitmap over the id range otherwise.
+// Splat ids are unique inside a tile, so the result is exactly the stable
+// sort's order and deterministic.  Every size the host needs is a capacity
+// (the caller's bound on M), never M itself.
+__global__ __launch_bounds__(256) void tile_count_kernel(int n, const float2 *__restrict__ xys,
+                                                         const int *__restrict__ radii, int tbx,
+                                                         int tby, unsigned *__restrict__ counts) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int r = radii[i];
+    if (r <= 0) return;
+    unsigned x0, y0, x1, y1;
+    const float2 c = xys[i];
+    tile_bbox(c.x, c.y, (float)r, tbx, tby, x0, y0, x1, y1);
+    for (unsigned y = y0; y < y1; ++y)
+        for (unsigned x = x0; x < x1; ++x) atomicAdd(counts + y * (unsigned)tbx + x, 1u);
+}
+
+__global__ __launch_bounds__(1024) void tile_scan_kernel(int ntiles, const unsigned *__restrict__ counts,
+                                                         int2 *__restrict__ bins,
+                                                         unsigned *__restrict__ cursor,
+                                                         int *__restrict__ meta, long long capacity) {
+    __shared__ unsigned ws[16];
+    const int per = (ntiles + 1023) / 1024;
+    const int b = threadIdx.x * per;
+    const int e = min(b + per, ntiles);
+    unsigned s = 0u;
+    for (int i = b; i < e; ++i) s += counts[i];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned incl = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned u = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += u;
+    }
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    unsigned wo = 0u, tot = 0u;
+    for (int k = 0; k < 16; ++k) {
+        if (k < w) wo += ws[k];
+        tot += ws[k];
+    }
+    unsigned run = wo + incl - s;
+    for (int i = b; i < e; ++i) {
+        const unsigned c = counts[i];
+        bins[i] = c ? make_int2((int)run, (int)(run + c)) : make_int2(0, 0);
+        cursor[i] = run;
+        run += c;
+    }
+    if (threadIdx.x == 0) {
+        meta[0] = (int)tot;
+        meta[1] = (long long)tot > capacity ? 1 : 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void tile_fill_kernel(int n, const float2 *__restrict__ xys,
+                                                        const int *__restrict__ radii, int tbx, int tby,
+                                                        unsigned *__restrict__ cursor,
+                                                        int *__restrict__ ids, long long capacity) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int r = radii[i];
+    if (r <= 0) return;
+    unsigned x0, y0, x1, y1;
+    const float2 c = xys[i];
+    tile_bbox(c.x, c.y, (float)r, tbx, tby, x0, y0, x1, y1);
+    for (unsigned y = y0; y < y1; ++y)
+        for (unsigned x = x0; x < x1; ++x) {
+            const unsigned slot = atomicAdd(cursor + y * (unsigned)tbx + x, 1u);
+            if ((long long)slot < capacity) ids[slot] = i;
+        }
+}
+
+// One wave per tile; ``bm`` is ``bm_words`` words of dynamic LDS.
+__global__ __launch_bounds__(64) void tile_segsort_kernel(int ntiles, const int2 *__restrict__ bins,
+                                                          const int *__restrict__ ids_in,
+                                                          int *__restrict__ ids_out, int bm_words,
+                                                          long long capacity) {
+    extern __shared__ unsigned bm[];
+    const int tile = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int2 range = bins[tile];
+    const int n = range.y - range.x;
+    if (n <= 0 || (long long)range.y > capacity) return;
+    const int *in = ids_in + range.x;
+    int *out = ids_out + range.x;
+    if (n <= 64) {
+        const int v = lane < n ? in[lane] : 0x7fffffff;
+        int rank = 0;
+        for (int k = 0; k < n; ++k) rank += (__shfl(v, k, 64) < v) ? 1 : 0;
+        if (lane < n) out[rank] = v;
+        return;
+    }
+    int lo = 0x7fffffff, hi = -1;
+    for (int j = lane; j < n; j += 64) {
+        const int v = in[j];
+        lo = min(lo, v);
+        hi = max(hi, v);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = min(lo, __shfl_xor(lo, off, 64));
+        hi = max(hi, __shfl_xor(hi, off, 64));
+    }
+    int written = 0;
+    const long long span = 32ll * bm_words;
+    for (long long base = lo; base <= hi; base += span) {
+        const int words = (int)min((long long)bm_words, ((hi - base) >> 5) + 1);
+        for (int w = lane; w < words; w += 64) bm[w] = 0u;
+        __syncthreads();
+        for (int j = lane; j < n; j += 64) {
+            const long long d = (long long)in[j] - base;
+            if (d >= 0 && d < 32ll * words) atomicOr(bm + (d >> 5), 1u << (d & 31));
+        }
+        __syncthreads();
+        const int per = (words + 63) / 64;
+        const int w0 = min(lane * per, words), w1 = min(w0 + per, words);
+        int cnt = 0;
+        for (int w = w0; w < w1; ++w) cnt += __popc(bm[w]);
+        int incl = cnt;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int u = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += u;
+        }
+        int pos = written + incl - cnt;
+        for (int w = w0; w < w1; ++w) {
+            unsigned bits = bm[w];
+            while (bits) {
+                const int bit = __ffs(bits) - 1;
+                out[pos++] = (int)(base + 32 * w + bit);
+                bits &= bits - 1u;
+            }
+        }
+        written += __shfl(incl, 63, 64);
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Host-side drivers.
 struct SortPlan {
     int nblocks;
@@ -587,4 +736,41 @@ extern "C" int gsvc_bin_and_sort_tiles(int num_points, int num_intersects, const
         hipLaunchKernelGGL(expand_isect_kernel, dim3(ceil_div(m, 256)), dim3(256), 0, s, m, keysOut,
                            gaussian_ids_sorted, depths, (long long *)isect_ids_sorted);
     return check_launch("bin_and_sort_tiles");
+}
+
+// Sync-free tile-major binning (see tile_count_kernel).  Workspace: counts and
+// cursors, one u32 each per tile.
+extern "C" size_t gsvc_bin_tiles_counted_workspace_bytes(int num_tiles) {
+    return 2 * align_up(sizeof(unsigned) * (size_t)(num_tiles > 0 ? num_tiles : 1));
+}
+
+extern "C" int gsvc_bin_tiles_counted(int num_points, const float *xys, const int *radii, int tbx,
+                                      int tby, long long capacity, int *ids_scratch,
+                                      int *gaussian_ids_sorted, int *tile_bins, int *meta,
+                                      void *workspace, size_t workspace_bytes, void *stream) {
+    const int ntiles = tbx * tby;
+    if (num_points < 0 || tbx <= 0 || tby <= 0 || capacity < 0)
+        return set_error(GSVC_ERR_ARG, "bin_tiles_counted: bad sizes");
+    if (workspace_bytes < gsvc_bin_tiles_counted_workspace_bytes(ntiles))
+        return set_error(GSVC_ERR_WORKSPACE, "bin_tiles_counted: workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    unsigned *counts = (unsigned *)workspace;
+    unsigned *cursor = (unsigned *)((char *)workspace + align_up(sizeof(unsigned) * (size_t)ntiles));
+    if (hipMemsetAsync(counts, 0, sizeof(unsigned) * (size_t)ntiles, s) != hipSuccess)
+        return set_error(GSVC_ERR_HIP, "bin_tiles_counted: memset failed");
+    const int nb = ceil_div(num_points > 0 ? num_points : 1, 256);
+    if (num_points > 0)
+        hipLaunchKernelGGL(tile_count_kernel, dim3(nb), dim3(256), 0, s, num_points,
+                           (const float2 *)xys, radii, tbx, tby, counts);
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, ntiles, counts, (int2 *)tile_bins,
+                       cursor, meta, capacity);
+    if (num_points > 0) {
+        hipLaunchKernelGGL(tile_fill_kernel, dim3(nb), dim3(256), 0, s, num_points,
+                           (const float2 *)xys, radii, tbx, tby, cursor, ids_scratch, capacity);
+        const int bm_words = min(ceil_div(num_points, 32) + 1, 4096);
+        hipLaunchKernelGGL(tile_segsort_kernel, dim3(ntiles), dim3(64), sizeof(unsigned) * bm_words, s,
+                           ntiles, (const int2 *)tile_bins, ids_scratch, gaussian_ids_sorted, bm_words,
+                           capacity);
+    }
+    return check_launch("bin_tiles_counted");
 }

@@ -95,9 +95,18 @@ __device__ __forceinline__ bool ellipse_hits_rect(float x, float y, float a, flo
     return (x + ex >= x0) && (x - ex <= x1) && (y + ey >= y0) && (y - ey <= y1);
 }
 
+// Output layouts: kLayoutHWC is the reference's [H, W, 3] image (+ final_idx);
+// kLayoutCHWClamped writes torch.clamp(img, 0, 1) as planes [3, H, W], i.e. the
+// epilogue of GaussianSplats_Represent.py:88-89 (clamp, view, permute,
+// contiguous) fused into the store.
+enum { kLayoutHWC = 0, kLayoutCHWClamped = 1 };
+
 struct SumFwdArgs {
-    int tbx, img_w, img_h, ntiles, sparse_max;
-    bool vec;  // W % 4 == 0 and 16-byte aligned outputs
+    int tbx, img_w, img_h, ntiles, sparse_max, layout;
+    bool vec;      // HWC: W % 4 == 0 and 16-byte aligned outputs
+    bool vec_chw;  // CHW: W % 4 == 0, H*W % 4 == 0, 16-byte aligned
+    const int *m_dev;  // device num_intersects (NULL: > 0); 0 -> background
+    const float *bg;
     const int *ids;
     const int2 *bins;
     const float2 *xys;
@@ -105,12 +114,35 @@ struct SumFwdArgs {
     float *out;
     int *final_idx;
     float *final_Ts;
+    long long *stamps;  // kModeStamp only
 };
+
+__device__ __forceinline__ float clamp01(float x) {
+    // torch.clamp(x, 0, 1): NaN stays NaN
+    return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x);
+}
+
+// Scalar store of one pixel in either layout.
+__device__ __forceinline__ void store_pixel(const SumFwdArgs &A, size_t p, float r, float g, float b,
+                                            int l) {
+    if (A.layout == kLayoutCHWClamped) {
+        const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
+        A.out[p] = clamp01(r);
+        A.out[hw + p] = clamp01(g);
+        A.out[2 * hw + p] = clamp01(b);
+    } else {
+        A.out[3 * p] = r;
+        A.out[3 * p + 1] = g;
+        A.out[3 * p + 2] = b;
+    }
+    if (A.final_idx) A.final_idx[p] = l;
+    if (A.final_Ts) A.final_Ts[p] = 1.0f;
+}
 
 // Sparse path: one wave blends the whole 16x16 tile, 4 pixels per lane.
 template <int kMode>
 __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, int2 range, int n,
-                                               float4 *s_slice) {
+                                               float4 *s_slice, float3 init) {
     float4 *s_geo = s_slice;                           // x, y, 0.5a, b
     float4 *s_col = s_slice + kChunk;                  // 0.5c, opacity, r, g
     float *s_blu = (float *)(s_slice + 2 * kChunk);    // b
@@ -120,8 +152,8 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
     const int pj = tx * kTile + ((lane & 3) << 2);
     const float py = (float)pi;
     const float px0 = (float)pj, px1 = (float)(pj + 1), px2 = (float)(pj + 2), px3 = (float)(pj + 3);
-    float r0 = 0.f, g0 = 0.f, b0 = 0.f, r1 = 0.f, g1 = 0.f, b1 = 0.f;
-    float r2 = 0.f, g2 = 0.f, b2 = 0.f, r3 = 0.f, g3 = 0.f, b3 = 0.f;
+    float r0 = init.x, g0 = init.y, b0 = init.z, r1 = init.x, g1 = init.y, b1 = init.z;
+    float r2 = init.x, g2 = init.y, b2 = init.z, r3 = init.x, g3 = init.y, b3 = init.z;
     int l0 = 0, l1 = 0, l2 = 0, l3 = 0;
     for (int base = 0; base < n; base += kChunk) {
         const int cnt = min(kChunk, n - base);
@@ -162,7 +194,20 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         }
         wave_lds_sync();
     }
-    if (A.vec && (tx + 1) * kTile <= A.img_w) {
+    if (A.layout == kLayoutCHWClamped && A.vec_chw && (tx + 1) * kTile <= A.img_w) {
+        // 4 lanes write a 64-byte row segment of each plane
+        if (pi < A.img_h) {
+            const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
+            float *o = A.out + (size_t)pi * (size_t)A.img_w + (size_t)pj;
+            *reinterpret_cast<float4 *>(o) = make_float4(clamp01(r0), clamp01(r1), clamp01(r2), clamp01(r3));
+            *reinterpret_cast<float4 *>(o + hw) = make_float4(clamp01(g0), clamp01(g1), clamp01(g2), clamp01(g3));
+            *reinterpret_cast<float4 *>(o + 2 * hw) = make_float4(clamp01(b0), clamp01(b1), clamp01(b2), clamp01(b3));
+            if (A.final_idx)
+                *reinterpret_cast<int4 *>(A.final_idx + (o - A.out)) = make_int4(l0, l1, l2, l3);
+        }
+        return;
+    }
+    if (A.layout == kLayoutHWC && A.vec && (tx + 1) * kTile <= A.img_w) {
         // stage the tile's 3 KB of RGB (lane l owns floats 12l..12l+11, a
         // conflict-free 48-byte stride), then write 16-byte chunk c = 64j + lane
         // = row c / 12, column chunk c % 12: whole 192-byte rows per instruction
@@ -179,10 +224,10 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
                 *reinterpret_cast<float4 *>(A.out + tile_base + (size_t)row * A.img_w * 3 + cc * 4) =
                     s_slice[c];
         }
-        if (pi < A.img_h) {
+        if (pi < A.img_h && A.final_idx) {
             const size_t p0 = (size_t)pi * (size_t)A.img_w + (size_t)pj;
             *reinterpret_cast<int4 *>(A.final_idx + p0) = make_int4(l0, l1, l2, l3);
-            if (A.final_Ts && kMode != kModeStamp)
+            if (A.final_Ts)
                 *reinterpret_cast<float4 *>(A.final_Ts + p0) = make_float4(1.f, 1.f, 1.f, 1.f);
         }
         return;
@@ -191,22 +236,15 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
     const float rr[4] = {r0, r1, r2, r3}, gg[4] = {g0, g1, g2, g3}, bb[4] = {b0, b1, b2, b3};
     const int ll[4] = {l0, l1, l2, l3};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        if (pj + q < A.img_w) {
-            const size_t p = (size_t)pi * (size_t)A.img_w + (size_t)(pj + q);
-            A.out[3 * p] = rr[q];
-            A.out[3 * p + 1] = gg[q];
-            A.out[3 * p + 2] = bb[q];
-            A.final_idx[p] = ll[q];
-            if (A.final_Ts && kMode != kModeStamp) A.final_Ts[p] = 1.0f;
-        }
-    }
+    for (int q = 0; q < 4; ++q)
+        if (pj + q < A.img_w)
+            store_pixel(A, (size_t)pi * (size_t)A.img_w + (size_t)(pj + q), rr[q], gg[q], bb[q], ll[q]);
 }
 
 // Dense path: this wave blends one 8-row band, 2 pixels per lane.
 template <int kMode>
 __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int band, int2 range,
-                                             int n, float4 *s_slice) {
+                                             int n, float4 *s_slice, float3 init) {
     float4 *s_geo = s_slice;                                      // x, y, 0.5a, b
     float4 *s_col = s_slice + kChunk;                             // 0.5c, opacity, r, g
     float *s_blu = reinterpret_cast<float *>(s_slice + 2 * kChunk);
@@ -220,7 +258,7 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
     const v2f pxv = {(float)pj, (float)(pj + 1)};
     const float bx0 = (float)(tx * kTile), by0 = (float)row0;
     if (kMode == kModeNoBlend) n = 0;
-    v2f ar = {0.f, 0.f}, ag = {0.f, 0.f}, ab = {0.f, 0.f};
+    v2f ar = {init.x, init.x}, ag = {init.y, init.y}, ab = {init.z, init.z};
     int l0 = 0, l1 = 0;
     const unsigned long long lt = (1ull << lane) - 1ull;
     for (int base = 0; base < n; base += kChunk) {
@@ -281,7 +319,18 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
                      "v"(l1));
         return;
     }
-    if (A.vec && (tx + 1) * kTile <= A.img_w) {
+    if (A.layout == kLayoutCHWClamped && A.vec_chw && (tx + 1) * kTile <= A.img_w) {
+        if (pi < A.img_h) {
+            const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
+            float *o = A.out + (size_t)pi * (size_t)A.img_w + (size_t)pj;
+            *reinterpret_cast<float2 *>(o) = make_float2(clamp01(ar.x), clamp01(ar.y));
+            *reinterpret_cast<float2 *>(o + hw) = make_float2(clamp01(ag.x), clamp01(ag.y));
+            *reinterpret_cast<float2 *>(o + 2 * hw) = make_float2(clamp01(ab.x), clamp01(ab.y));
+            if (A.final_idx) *reinterpret_cast<int2 *>(A.final_idx + (o - A.out)) = make_int2(l0, l1);
+        }
+        return;
+    }
+    if (A.layout == kLayoutHWC && A.vec && (tx + 1) * kTile <= A.img_w) {
         // stage 8 rows x 16 px x 12 B = 1536 B (lane l owns floats 6l..6l+5),
         // then 96 16-byte chunks as whole 192-byte rows; final_idx as pairs
         float2 *so2 = reinterpret_cast<float2 *>(s_slice);
@@ -300,10 +349,10 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
                         s_slice[c];
             }
         }
-        if (pi < A.img_h) {
+        if (pi < A.img_h && A.final_idx) {
             const size_t p0 = (size_t)pi * (size_t)A.img_w + (size_t)pj;
             *reinterpret_cast<int2 *>(A.final_idx + p0) = make_int2(l0, l1);
-            if (A.final_Ts && kMode != kModeStamp)
+            if (A.final_Ts)
                 *reinterpret_cast<float2 *>(A.final_Ts + p0) = make_float2(1.f, 1.f);
         }
         return;
@@ -312,16 +361,9 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
     const float rr[2] = {ar.x, ar.y}, gg[2] = {ag.x, ag.y}, bb[2] = {ab.x, ab.y};
     const int ll[2] = {l0, l1};
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        if (pj + q < A.img_w) {
-            const size_t p = (size_t)pi * (size_t)A.img_w + (size_t)(pj + q);
-            A.out[3 * p] = rr[q];
-            A.out[3 * p + 1] = gg[q];
-            A.out[3 * p + 2] = bb[q];
-            A.final_idx[p] = ll[q];
-            if (A.final_Ts && kMode != kModeStamp) A.final_Ts[p] = 1.0f;
-        }
-    }
+    for (int q = 0; q < 2; ++q)
+        if (pj + q < A.img_w)
+            store_pixel(A, (size_t)pi * (size_t)A.img_w + (size_t)(pj + q), rr[q], gg[q], bb[q], ll[q]);
 }
 
 // kModeSparse launches 64-thread workgroups (one wave per tile); every other
@@ -337,18 +379,24 @@ __global__ __launch_bounds__(kMode == kModeSparse ? 64 : 128, 8) void raster_sum
     const int2 range = A.bins[tile];
     int n = range.y - range.x;
     n = n > kTilePix ? kTilePix : (n < 0 ? 0 : n);
+    // rasterize_sum.py:121-127: a frame without intersections is the background
+    float3 init = make_float3(0.f, 0.f, 0.f);
+    if (A.m_dev && *A.m_dev < 1) {
+        n = 0;
+        init = make_float3(A.bg[0], A.bg[1], A.bg[2]);
+    }
     const int ty = tile / A.tbx;
     const bool sparse = kMode == kModeSparse ||
                         ((kMode == kModeAdaptive || kMode == kModeStamp) && n <= A.sparse_max);
     if (sparse) {
         if (w != 0) return;
-        sum_fwd_sparse<kMode>(A, tile, range, n, s_buf[0]);
+        sum_fwd_sparse<kMode>(A, tile, range, n, s_buf[0], init);
     } else {
         if (ty * kTile + w * 8 >= A.img_h) return;  // band below the image
-        sum_fwd_band<kMode>(A, tile, w, range, n, s_buf[w]);
+        sum_fwd_band<kMode>(A, tile, w, range, n, s_buf[w], init);
     }
     if (kMode == kModeStamp && (threadIdx.x & 63) == 0) {
-        long long *st = reinterpret_cast<long long *>(A.final_Ts) + 4 * (size_t)tile;
+        long long *st = A.stamps + 4 * (size_t)tile;
         st[w == 0 ? 0 : 2] = t0;
         st[w == 0 ? 1 : 3] = stamp();
     }
@@ -498,15 +546,19 @@ static int check_tiles(const char *what, int bx, int by, int tbx, int tby, unsig
     return GSVC_OK;
 }
 
-extern "C" int gsvc_rasterize_sum_forward_auto(
-    int num_intersects, int tbx, int tby, int tbz, int block_x, int block_y, int block_z,
-    unsigned img_width, unsigned img_height, unsigned img_depth, const int *gaussian_ids_sorted,
-    const int *tile_bins, const float *xys, const float *conics, const float *colors,
-    const float *opacities, const float *background, float *out_img, float *final_Ts,
-    int *final_idx, void *stream) {
-    (void)tbz; (void)block_z; (void)img_depth; (void)background;
+extern "C" int gsvc_rasterize_sum_forward_ex(
+    int tbx, int tby, int tbz, int block_x, int block_y, int block_z, unsigned img_width,
+    unsigned img_height, unsigned img_depth, const int *gaussian_ids_sorted, const int *tile_bins,
+    const float *xys, const float *conics, const float *colors, const float *opacities,
+    const float *background, const int *num_intersects_dev, int density_hint, int out_layout,
+    float *out_img, float *final_Ts, int *final_idx, void *stream) {
+    (void)tbz; (void)block_z; (void)img_depth;
     int rc = check_tiles("rasterize_sum_forward", block_x, block_y, tbx, tby, img_width, img_height);
     if (rc) return rc;
+    if (out_layout != kLayoutHWC && out_layout != kLayoutCHWClamped)
+        return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: unknown output layout %d", out_layout);
+    if (num_intersects_dev && !background)
+        return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: background required with a device count");
     const int ntiles = tbx * tby;
     if (ntiles == 0) return GSVC_OK;
     SumFwdArgs A;
@@ -515,8 +567,12 @@ extern "C" int gsvc_rasterize_sum_forward_auto(
     A.img_h = (int)img_height;
     A.ntiles = ntiles;
     A.sparse_max = g_knobs[3] > 0 ? g_knobs[3] : 8;
+    A.layout = out_layout;
     A.vec = (img_width % 4 == 0) && (((uintptr_t)out_img & 15) == 0) &&
             (((uintptr_t)final_idx & 15) == 0) && (((uintptr_t)final_Ts & 15) == 0);
+    A.vec_chw = A.vec && (((size_t)img_width * img_height) % 4 == 0);
+    A.m_dev = num_intersects_dev;
+    A.bg = background;
     A.ids = gaussian_ids_sorted;
     A.bins = (const int2 *)tile_bins;
     A.xys = (const float2 *)xys;
@@ -526,10 +582,14 @@ extern "C" int gsvc_rasterize_sum_forward_auto(
     A.out = out_img;
     A.final_idx = final_idx;
     A.final_Ts = final_Ts;
+    A.stamps = nullptr;
     hipStream_t s = (hipStream_t)stream;
     int mode = g_knobs[0];
     if (mode == 0)
-        mode = (num_intersects > kDenseEntriesPerTile * ntiles) ? kModeBanded : kModeSparse;
+        mode = ((long long)density_hint > (long long)kDenseEntriesPerTile * ntiles) ? kModeBanded
+                                                                                     : kModeSparse;
+    if (mode == kModeStamp && out_layout != kLayoutHWC)
+        return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: stamp mode needs the HWC layout");
     switch (mode) {
         case kModeSparse:
             hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeSparse>, dim3(ntiles), dim3(64), 0, s, A);
@@ -538,6 +598,8 @@ extern "C" int gsvc_rasterize_sum_forward_auto(
             hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeBanded>, dim3(ntiles), dim3(128), 0, s, A);
             break;
         case kModeStamp:
+            A.final_Ts = nullptr;
+            A.stamps = reinterpret_cast<long long *>(final_Ts);
             hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeStamp>, dim3(ntiles), dim3(128), 0, s, A);
             break;
         case kModeNoBlend:
@@ -563,10 +625,10 @@ extern "C" int gsvc_rasterize_sum_forward(int tbx, int tby, int tbz, int block_x
                                           const float *background, float *out_img, float *final_Ts,
                                           int *final_idx, void *stream) {
     // without the intersection count the sparse path is the safe default
-    return gsvc_rasterize_sum_forward_auto(0, tbx, tby, tbz, block_x, block_y, block_z, img_width,
-                                           img_height, img_depth, gaussian_ids_sorted, tile_bins,
-                                           xys, conics, colors, opacities, background, out_img,
-                                           final_Ts, final_idx, stream);
+    return gsvc_rasterize_sum_forward_ex(tbx, tby, tbz, block_x, block_y, block_z, img_width,
+                                         img_height, img_depth, gaussian_ids_sorted, tile_bins, xys,
+                                         conics, colors, opacities, background, nullptr, 0, kLayoutHWC,
+                                         out_img, final_Ts, final_idx, stream);
 }
 
 extern "C" int gsvc_rasterize_sum_backward(unsigned img_height, unsigned img_width, unsigned block_h,

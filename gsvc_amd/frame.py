@@ -19,6 +19,7 @@ import torch.nn.functional as F
 from .adan import Adan
 from .project_gaussians_2d import project_gaussians_2d
 from .rasterize_sum import rasterize_gaussians_sum
+from .render import render_sum_frame
 
 
 def loss_fn(pred, target, loss_type="L2", lambda_value=0.7):
@@ -89,8 +90,24 @@ class GaussianVideoFrame(nn.Module):
     def get_cholesky_elements(self):
         return self._cholesky + self.cholesky_bound
 
+    def _ones_opacity(self):
+        n = self._xyz.shape[0]
+        o = getattr(self, "_opacity_ones", None)
+        if o is None or o.shape[0] != n or o.device != self._xyz.device:
+            o = torch.ones(n, 1, device=self._xyz.device)
+            self._opacity_ones = o
+        return o
+
     def forward(self):
-        _opacity = torch.ones(self._xyz.shape[0], 1).to(self.device)
+        if not torch.is_grad_enabled():
+            # inference: same image from the sync-free path with the clamp +
+            # NCHW epilogue fused into the rasterizer (gsvc_amd/render.py)
+            return {"render": render_sum_frame(self.get_xyz, self.get_cholesky_elements,
+                                               self.get_features, self._ones_opacity(), self.H,
+                                               self.W, self.tile_bounds, self.background,
+                                               self.BLOCK_H, self.BLOCK_W)}
+        # reference: torch.ones(N, 1).to(device) per call; same values
+        _opacity = self._ones_opacity()
         self.xys, depths, self.radii, conics, num_tiles_hit = project_gaussians_2d(
             self.get_xyz, self.get_cholesky_elements, self.H, self.W, self.tile_bounds)
         out_img = rasterize_gaussians_sum(self.xys, depths, self.radii, conics, num_tiles_hit,

@@ -113,6 +113,9 @@ def project_gaussians_2d_forward(num_points, means2d, L_elements, img_height, im
     L.call("gsvc_project_gaussians_2d_forward", n, L.ptr(means2d), L.ptr(L_elements),
            int(img_height), int(img_width), tb[0], tb[1], tb[2], float(clip_thresh),
            L.ptr(xys), L.ptr(depths), L.ptr(radii), L.ptr(conics), L.ptr(nth), L.stream(dev))
+    # the 2D projection writes depth 0 for every splat (foward2d.cu:67,122):
+    # tag it for utils.depths_known_zero (cleared by any in-place change)
+    depths._gsvc_zero_version = depths._version
     return xys, depths, radii, conics, nth
 
 
@@ -231,6 +234,28 @@ def bin_and_sort_tiles(num_points, num_intersects, xys, depths, radii, cum_tiles
     return gids, bins, isect
 
 
+def bin_tiles_counted(num_points, xys, radii, tile_bounds, capacity):
+    """Sync-free tile binning (gsvc_bin_tiles_counted): returns
+    (gaussian_ids_sorted [capacity], tile_bins [#tiles, 2], meta [2] = {M,
+    overflow}) with M only on the device.  Valid when every emitting splat has
+    the same depth bits (the order is (tile, splat id))."""
+    xys = _f32(xys, "xys")
+    radii = _i32(radii, "radii")
+    tb = _tb(tile_bounds)
+    n, cap = int(num_points), int(capacity)
+    ntiles = tb[0] * tb[1]
+    dev = xys.device
+    scratch = torch.empty((cap,), dtype=torch.int32, device=dev)
+    gids = torch.empty((cap,), dtype=torch.int32, device=dev)
+    bins = torch.empty((ntiles, 2), dtype=torch.int32, device=dev)
+    meta = torch.empty((2,), dtype=torch.int32, device=dev)
+    ws = torch.empty((L.size("gsvc_bin_tiles_counted_workspace_bytes", ntiles),), dtype=torch.uint8,
+                     device=dev)
+    L.call("gsvc_bin_tiles_counted", n, L.ptr(xys), L.ptr(radii), tb[0], tb[1], cap, L.ptr(scratch),
+           L.ptr(gids), L.ptr(bins), L.ptr(meta), L.ptr(ws), ws.numel(), L.stream(dev))
+    return gids, bins, meta
+
+
 # ---------------------------------------------------------------------------
 # Rasterizers (bindings.cu:332-469, 631-779)
 
@@ -244,8 +269,8 @@ def _bins_for(tile_bins: torch.Tensor, ntiles: int) -> torch.Tensor:
     return tile_bins
 
 
-def _raster_fwd(sym, tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys, conics,
-                colors, opacities, background, want_Ts, num_intersects=None):
+def _raster_inputs(tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys, conics,
+                   colors, opacities, background):
     tb = _tb(tile_bounds)
     blk = _tb(block)
     img_w, img_h, img_d = (int(x) for x in img_size)
@@ -258,12 +283,19 @@ def _raster_fwd(sym, tile_bounds, block, img_size, gaussian_ids_sorted, tile_bin
     if colors.dim() != 2 or colors.shape[1] != 3:
         raise RuntimeError("colors must have shape (N, 3)")
     bins = _bins_for(tile_bins, tb[0] * tb[1])
+    return tb, blk, (img_w, img_h, img_d), gids, bins, xys, conics, colors, opacities, background
+
+
+def _raster_fwd(sym, tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys, conics,
+                colors, opacities, background, want_Ts):
+    tb, blk, (img_w, img_h, img_d), gids, bins, xys, conics, colors, opacities, background = \
+        _raster_inputs(tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys, conics,
+                       colors, opacities, background)
     dev = xys.device
     out = torch.empty((img_h, img_w, 3), dtype=torch.float32, device=dev)
     idx = torch.empty((img_h, img_w), dtype=torch.int32, device=dev)
     Ts = torch.empty((img_h, img_w), dtype=torch.float32, device=dev) if want_Ts else None
-    hint = () if num_intersects is None else (int(num_intersects),)
-    _timed_call(sym, *hint, tb[0], tb[1], tb[2], blk[0], blk[1], blk[2], img_w, img_h, img_d,
+    _timed_call(sym, tb[0], tb[1], tb[2], blk[0], blk[1], blk[2], img_w, img_h, img_d,
                 L.ptr(gids), L.ptr(bins), L.ptr(xys), L.ptr(conics), L.ptr(colors),
                 L.ptr(opacities), L.ptr(background), L.ptr(out), L.ptr(Ts), L.ptr(idx),
                 L.stream(dev))
@@ -271,16 +303,45 @@ def _raster_fwd(sym, tile_bounds, block, img_size, gaussian_ids_sorted, tile_bin
 
 
 def rasterize_sum_forward(tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys,
-                          conics, colors, opacities, background, num_intersects=None):
-    """``num_intersects`` (optional, beyond the reference signature) lets the
-    launcher pick the kernel for the frame's density (identical results)."""
-    sym = "gsvc_rasterize_sum_forward" if num_intersects is None else "gsvc_rasterize_sum_forward_auto"
-    out, _, idx = _raster_fwd(sym, tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins,
-                              xys, conics, colors, opacities, background, want_Ts=False,
-                              num_intersects=num_intersects)
+                          conics, colors, opacities, background):
+    out, _, idx = _raster_fwd("gsvc_rasterize_sum_forward", tile_bounds, block, img_size,
+                              gaussian_ids_sorted, tile_bins, xys, conics, colors, opacities,
+                              background, want_Ts=False)
     final_Ts = torch.ones((1, 1), dtype=torch.float32, device=out.device).expand(out.shape[0],
                                                                               out.shape[1])
     return out, final_Ts, idx
+
+
+LAYOUT_HWC = 0
+LAYOUT_CHW_CLAMPED = 1
+
+
+def rasterize_sum_forward_ex(tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys,
+                             conics, colors, opacities, background, num_intersects_dev=None,
+                             density_hint=0, layout=LAYOUT_HWC, want_idx=True, out=None):
+    """Sum forward with the hot path's knobs (gsvc_rasterize_sum_forward_ex):
+    a device-side M (background when 0), a density hint for the kernel choice,
+    the fused clamp + [3,H,W] layout, and final_idx optional.  Returns
+    (out_img, final_idx | None); out_img is [H,W,3] or [3,H,W] (``out`` may
+    supply it)."""
+    tb, blk, (img_w, img_h, img_d), gids, bins, xys, conics, colors, opacities, background = \
+        _raster_inputs(tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys, conics,
+                       colors, opacities, background)
+    dev = xys.device
+    shape = (img_h, img_w, 3) if layout == LAYOUT_HWC else (3, img_h, img_w)
+    if out is None:
+        out = torch.empty(shape, dtype=torch.float32, device=dev)
+    elif out.numel() != img_h * img_w * 3 or not out.is_contiguous() or out.dtype != torch.float32:
+        raise RuntimeError("out must be a contiguous float32 tensor of H*W*3 elements")
+    idx = torch.empty((img_h, img_w), dtype=torch.int32, device=dev) if want_idx else None
+    m_dev = None
+    if num_intersects_dev is not None:
+        m_dev = _i32(num_intersects_dev, "num_intersects_dev")
+    _timed_call("gsvc_rasterize_sum_forward_ex", tb[0], tb[1], tb[2], blk[0], blk[1], blk[2], img_w,
+                img_h, img_d, L.ptr(gids), L.ptr(bins), L.ptr(xys), L.ptr(conics), L.ptr(colors),
+                L.ptr(opacities), L.ptr(background), L.ptr(m_dev), int(density_hint), int(layout),
+                L.ptr(out), None, L.ptr(idx), L.stream(dev))
+    return out, idx
 
 
 def rasterize_forward(tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys, conics,

@@ -14,7 +14,7 @@ from torch import Tensor
 from torch.autograd import Function
 
 from . import ops as _C
-from .utils import bin_and_sort_for_raster
+from .utils import bin_for_raster
 
 
 def rasterize_gaussians_sum(
@@ -89,10 +89,11 @@ class _RasterizeGaussiansSum(Function):
             # extension never exported (ext.cpp:6-23): AttributeError there too
             raise AttributeError("nd_rasterize_sum_forward: only 3-channel colors are supported")
 
-        num_intersects, gaussian_ids_sorted, tile_bins = bin_and_sort_for_raster(
-            num_points, xys, depths, radii, num_tiles_hit, tile_bounds)
+        binned = bin_for_raster(num_points, xys, depths, radii, num_tiles_hit, tile_bounds)
+        num_intersects = binned.num_intersects
+        gaussian_ids_sorted, tile_bins = binned.gaussian_ids_sorted, binned.tile_bins
 
-        if num_intersects < 1:
+        if num_intersects is not None and num_intersects < 1:
             out_img = (torch.ones(img_height, img_width, colors.shape[-1], device=xys.device)
                        * background)
             gaussian_ids_sorted = torch.zeros(0, 1, device=xys.device)
@@ -100,9 +101,13 @@ class _RasterizeGaussiansSum(Function):
             final_Ts = torch.zeros(img_height, img_width, device=xys.device)
             final_idx = torch.zeros(img_height, img_width, device=xys.device)
         else:
-            out_img, final_Ts, final_idx = _C.rasterize_sum_forward(
+            # with M on the device (sync-free binning) the kernel itself takes
+            # the M < 1 branch: background out, final_idx 0
+            out_img, final_idx = _C.rasterize_sum_forward_ex(
                 tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys, conics, colors,
-                opacity, background, num_intersects=num_intersects)
+                opacity, background, num_intersects_dev=binned.m_dev,
+                density_hint=binned.density_hint)
+            final_Ts = None  # identically 1 (0 when M < 1): built only for return_alpha
 
         ctx.img_width = img_width
         ctx.img_height = img_height
@@ -110,9 +115,15 @@ class _RasterizeGaussiansSum(Function):
         ctx.BLOCK_W = BLOCK_W
         ctx.num_intersects = num_intersects
         ctx.save_for_backward(gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
-                              background, final_Ts, final_idx)
+                              background, final_idx)
 
         if return_alpha:
+            if final_Ts is None:
+                if binned.m_dev is not None:
+                    ts = (binned.m_dev > 0).to(torch.float32).view(1, 1)
+                else:
+                    ts = torch.ones((1, 1), dtype=torch.float32, device=xys.device)
+                final_Ts = ts.expand(img_height, img_width)
             out_alpha = 1 - final_Ts
             return out_img, out_alpha
         return out_img
@@ -126,10 +137,10 @@ class _RasterizeGaussiansSum(Function):
         if v_out_alpha is None:
             v_out_alpha = torch.zeros_like(v_out_img[..., 0])
 
-        (gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background, final_Ts,
+        (gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
          final_idx) = ctx.saved_tensors
 
-        if num_intersects < 1:
+        if num_intersects is not None and num_intersects < 1:
             v_xy = torch.zeros_like(xys)
             v_conic = torch.zeros_like(conics)
             v_colors = torch.zeros_like(colors)
@@ -137,7 +148,7 @@ class _RasterizeGaussiansSum(Function):
         else:
             v_xy, v_conic, v_colors, v_opacity = _C.rasterize_sum_backward(
                 img_height, img_width, ctx.BLOCK_H, ctx.BLOCK_W, gaussian_ids_sorted, tile_bins,
-                xys, conics, colors, opacity, background, final_Ts, final_idx, v_out_img,
+                xys, conics, colors, opacity, background, None, final_idx, v_out_img,
                 v_out_alpha)
             v_opacity = v_opacity.reshape(opacity.shape) if opacity.dim() != 2 else v_opacity
 

@@ -6,12 +6,77 @@ of torch.cumsum / torch.sort / torch.gather.
 """
 from __future__ import annotations
 
-from typing import Tuple
+import os
+from typing import NamedTuple, Optional, Tuple
 
 import torch
 from torch import Tensor
 
 from . import ops as _C
+
+# Upper bound, in entries, on the intersection buffers the sync-free binning
+# may allocate (its capacity is num_points * num_tiles, which cannot
+# overflow).  Above it the rasterizers read M on the host first.
+BIN_CAPACITY_BUDGET = int(os.environ.get("GSVC_BIN_CAPACITY_BUDGET", str(1 << 30)))
+
+
+def mark_zero_depths(depths: Tensor) -> Tensor:
+    """Record that ``depths`` is identically zero (project_gaussians_2d's
+    output): the rasterizers may then order entries by (tile, splat id)
+    without reading the depth bits back.  Any in-place change clears it."""
+    depths._gsvc_zero_version = depths._version
+    return depths
+
+
+def depths_known_zero(depths: Optional[Tensor]) -> bool:
+    return depths is None or getattr(depths, "_gsvc_zero_version", None) == depths._version
+
+
+class _LazyCount:
+    """Last intersection count seen on a device, refreshed every ``period``
+    calls through a non-blocking copy to pinned memory (no host sync).  Used
+    only to pick a kernel variant, so a stale value is harmless."""
+
+    def __init__(self, period=16):
+        self.period = period
+        self.value = 0
+        self.calls = 0
+        self.buf = None
+        self.event = None
+
+    def update(self, m_dev: Tensor) -> int:
+        if self.event is not None and self.event.query():
+            self.value = int(self.buf[0])
+            self.event = None
+        if self.event is None and self.calls % self.period == 0:
+            if self.buf is None:
+                self.buf = torch.empty((1,), dtype=torch.int32, pin_memory=True)
+            self.buf.copy_(m_dev[:1], non_blocking=True)
+            self.event = torch.cuda.Event()
+            self.event.record()
+        self.calls += 1
+        return self.value
+
+
+_lazy_counts = {}
+
+
+def _density_hint(m_dev: Tensor) -> int:
+    key = m_dev.device.index
+    if key not in _lazy_counts:
+        _lazy_counts[key] = _LazyCount()
+    return _lazy_counts[key].update(m_dev)
+
+
+class TileBinning(NamedTuple):
+    """Binned intersections for a rasterizer.  ``num_intersects`` is the host
+    int when it was read (sized path), else None and ``m_dev`` holds M on the
+    device; ``density_hint`` estimates M for the kernel choice."""
+    num_intersects: Optional[int]
+    m_dev: Optional[Tensor]
+    gaussian_ids_sorted: Optional[Tensor]
+    tile_bins: Optional[Tensor]
+    density_hint: int
 
 
 def map_gaussian_to_intersects(num_points: int, num_intersects: int, xys: Tensor, depths: Tensor,
@@ -81,3 +146,25 @@ def bin_and_sort_for_raster(num_points: int, xys: Tensor, depths: Tensor, radii:
         return m, gids, bins
     _, _, _, gids, bins = bin_and_sort_gaussians(num_points, m, xys, depths, radii, cum, tile_bounds)
     return m, gids, bins
+
+
+def bin_for_raster(num_points: int, xys: Tensor, depths: Optional[Tensor], radii: Tensor,
+                   num_tiles_hit: Tensor, tile_bounds: Tuple[int, int, int]) -> TileBinning:
+    """Binning front of the rasterizers (utils.py:99-167 as the reference's
+    rasterize_sum.py:110-118 uses it).
+
+    When the depths are known to be zero (project_gaussians_2d's output) the
+    (tile, splat id) order IS the reference's sorted order, and the sync-free
+    CSR binning runs with capacity num_points * tiles (no host round trip);
+    otherwise -- or when that capacity exceeds BIN_CAPACITY_BUDGET -- M is read
+    on the host and the sorted path of ``bin_and_sort_for_raster`` runs.
+    """
+    ntiles = int(tile_bounds[0]) * int(tile_bounds[1])
+    cap = int(num_points) * ntiles
+    if depths_known_zero(depths) and cap <= BIN_CAPACITY_BUDGET:
+        gids, bins, meta = _C.bin_tiles_counted(num_points, xys, radii, tile_bounds, cap)
+        m_dev = meta[:1]
+        return TileBinning(None, m_dev, gids, bins, _density_hint(m_dev))
+    m, gids, bins = bin_and_sort_for_raster(num_points, xys, depths, radii, num_tiles_hit,
+                                            tile_bounds)
+    return TileBinning(m, None, gids, bins, m)

@@ -140,6 +140,21 @@ int gsvc_bin_and_sort_tiles(
     int64_t *isect_ids_sorted, void *workspace, size_t workspace_bytes,
     void *stream);
 
+/* Sync-free tile binning used by the rasterizer ops (the hot path of
+ * utils.py:99-167 + bindings.cu:274-330 without reading num_intersects on the
+ * host): builds gaussian_ids_sorted in the stable (tile, splat id) order of
+ * the reference's sorted pairs and tile_bins[tbx*tby] ([start,end), (0,0)
+ * when empty), every size staying on the device.  meta[0] <- M,
+ * meta[1] <- 1 if M > capacity (outputs then incomplete).  ids_scratch and
+ * gaussian_ids_sorted hold >= capacity ints; capacity = num_points * tiles
+ * can never overflow.  Results are deterministic. */
+size_t gsvc_bin_tiles_counted_workspace_bytes(int num_tiles);
+int gsvc_bin_tiles_counted(int num_points, const float *xys, const int *radii,
+                           int tile_bounds_x, int tile_bounds_y, long long capacity,
+                           int *ids_scratch, int *gaussian_ids_sorted, int *tile_bins,
+                           int *meta, void *workspace, size_t workspace_bytes,
+                           void *stream);
+
 /* ---------------------------------------------------------------------------
  * Sum rasterizer (the GSVC renderer, rasterize_sum.py).
  * Replaces _C.rasterize_sum_forward (bindings.cu:400-469 -> forward.cu:512-627):
@@ -157,17 +172,26 @@ int gsvc_rasterize_sum_forward(
     const float *opacities, const float *background,
     float *out_img, float *final_Ts, int *final_idx, void *stream);
 
-/* Same op with the frame's intersection count as a density hint: frames
- * averaging more than 5 entries per tile use the banded two-waves-per-tile
- * kernel with ellipse culling, sparser frames one wave per tile (the plain
- * entry point uses the latter).  Results are identical either way. */
-int gsvc_rasterize_sum_forward_auto(
-    int num_intersects, int tile_bounds_x, int tile_bounds_y, int tile_bounds_z,
+/* The same op with the knobs of the sync-free hot path (results identical to
+ * gsvc_rasterize_sum_forward for the same inputs):
+ *   num_intersects_dev  device int M (NULL: M > 0 assumed); when M < 1 every
+ *                       pixel gets background, the reference's M < 1 branch
+ *                       (rasterize_sum.py:121-127), final_idx 0;
+ *   density_hint        an estimate of M (any value is correct; > 5 entries
+ *                       per tile selects the banded two-waves-per-tile
+ *                       kernel, otherwise one wave per tile);
+ *   out_layout          0: out_img [H,W,3] as the reference;
+ *                       1: out_img [3,H,W] = torch.clamp(img, 0, 1) permuted,
+ *                       the caller epilogue of GaussianSplats_Represent.py:88-89;
+ *   final_idx, final_Ts may be NULL (not written). */
+int gsvc_rasterize_sum_forward_ex(
+    int tile_bounds_x, int tile_bounds_y, int tile_bounds_z,
     int block_x, int block_y, int block_z,
     unsigned img_width, unsigned img_height, unsigned img_depth,
     const int *gaussian_ids_sorted, const int *tile_bins,
     const float *xys, const float *conics, const float *colors,
     const float *opacities, const float *background,
+    const int *num_intersects_dev, int density_hint, int out_layout,
     float *out_img, float *final_Ts, int *final_idx, void *stream);
 
 /* Replaces _C.rasterize_sum_backward (bindings.cu:706-779 -> backward.cu:696-862).

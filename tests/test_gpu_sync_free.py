@@ -1,0 +1,216 @@
+"""GPU parity of the sync-free hot path:
+
+* gsvc_bin_tiles_counted (count -> scan -> fill -> per-tile segment sort) must
+  give exactly the reference's sorted order -- gaussian_ids_sorted and
+  tile_bins bit-exact against the oracle's stable sort and the golden
+  fixtures -- including long segments (LDS-bitmap path), the 64/65 boundary
+  between the two segment sorts, and an id span wider than one bitmap window;
+* the rasterizer ops on that path (device-side M, background when M = 0,
+  return_alpha) match the sized path and the fixtures;
+* the render path (fused clamp + NCHW store, no final_idx) is bit-identical to
+  GSVC's forward composed from the ops, in both kernel modes.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_names, load_golden
+
+pytestmark = pytest.mark.gpu
+
+SUM_CASES = golden_names("sum_")
+
+
+def T(a, dev="cuda"):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def N(t):
+    return t.detach().cpu().numpy()
+
+
+def _tb(H, W):
+    return ((W + 15) // 16, (H + 15) // 16, 1)
+
+
+def _counted(n, xys, radii, tb):
+    from gsvc_amd import ops
+    cap = n * tb[0] * tb[1]
+    gids, bins, meta = ops.bin_tiles_counted(n, xys, radii, tb, cap)
+    m, ovf = (int(x) for x in meta.tolist())
+    assert ovf == 0
+    return m, gids[:m], bins
+
+
+@pytest.mark.parametrize("name", SUM_CASES)
+def test_counted_binning_golden(cuda, name):
+    from gsvc_amd import ops
+    z = load_golden(name)
+    H, W = int(z["H"]), int(z["W"])
+    tb = _tb(H, W)
+    n = len(z["xys"])
+    m, gids, bins = _counted(n, T(z["xys"]), T(z["radii"]), tb)
+    assert m == int(z["num_intersects"])
+    ref_bins = np.zeros((tb[0] * tb[1], 2), np.int32)
+    if m > 0:
+        np.testing.assert_array_equal(N(gids), z["gaussian_ids_sorted"])
+        ref_bins = z["tile_bins"][: tb[0] * tb[1]]
+    np.testing.assert_array_equal(N(bins), ref_bins)
+    # deterministic despite the atomic fill
+    m2, gids2, bins2 = _counted(n, T(z["xys"]), T(z["radii"]), tb)
+    assert torch.equal(gids, gids2) and torch.equal(bins, bins2)
+    del ops
+
+
+@pytest.mark.parametrize("n,chol", [(10000, 1.0), (50000, 1.0), (20000, 8.0)])
+def test_counted_binning_1080p(cuda, oracle, n, chol):
+    """Full size, and large splats (chol x8: hundreds of entries per tile,
+    LDS-bitmap segment sort)."""
+    from gsvc_amd import ops
+    H, W = 1080, 1920
+    tb = _tb(H, W)
+    means, L, colors, opac = oracle.synthetic_frame(n, seed=n + 3, chol_scale=chol)
+    ref = oracle.render_sum(means, L, colors, opac, H, W)
+    xys, depths, radii, conics, nth = ops.project_gaussians_2d_forward(n, T(means), T(L), H, W, tb,
+                                                                      0.01)
+    m, gids, bins = _counted(n, xys, radii, tb)
+    assert m == ref["m"]
+    np.testing.assert_array_equal(N(gids), ref["gids_sorted"])
+    np.testing.assert_array_equal(N(bins), ref["bins"][: tb[0] * tb[1]])
+    counts = ref["bins"][:, 1] - ref["bins"][:, 0]
+    if chol > 1:
+        assert counts.max() > 64  # the bitmap path ran
+
+
+def _clustered_frame(n, ids_on_tile, H=64, W=64):
+    """Every splat far off-screen (no tiles) except ``ids_on_tile``, which all
+    cover tile (1, 1) and its neighbours."""
+    means = np.full((n, 2), 5.0, np.float32)
+    L = np.tile(np.array([[1.0, 0.0, 1.0]], np.float32), (n, 1))
+    rng = np.random.default_rng(0)
+    sel = np.asarray(ids_on_tile)
+    # pixel ~ (24, 24) +- 4: means2d in [-1, 1] maps to [0, W]
+    means[sel, 0] = (24 + rng.uniform(-4, 4, len(sel))) / (W / 2) - 1
+    means[sel, 1] = (24 + rng.uniform(-4, 4, len(sel))) / (H / 2) - 1
+    L[sel] = np.array([3.0, 0.5, 2.0], np.float32)
+    colors = rng.uniform(0, 1, (n, 3)).astype(np.float32)
+    opac = np.ones((n, 1), np.float32)
+    return means, L, colors, opac, H, W
+
+
+@pytest.mark.parametrize("count", [63, 64, 65, 130])
+def test_segment_sort_boundaries(cuda, oracle, count):
+    from gsvc_amd import ops
+    n = 4000
+    ids = np.random.default_rng(count).choice(n, count, replace=False)
+    means, L, colors, opac, H, W = _clustered_frame(n, ids)
+    ref = oracle.render_sum(means, L, colors, opac, H, W)
+    tb = _tb(H, W)
+    xys, depths, radii, conics, nth = ops.project_gaussians_2d_forward(n, T(means), T(L), H, W, tb,
+                                                                      0.01)
+    m, gids, bins = _counted(n, xys, radii, tb)
+    assert m == ref["m"]
+    np.testing.assert_array_equal(N(gids), ref["gids_sorted"])
+    np.testing.assert_array_equal(N(bins), ref["bins"][: tb[0] * tb[1]])
+    assert (ref["bins"][:, 1] - ref["bins"][:, 0]).max() == count
+
+
+def test_segment_sort_multi_window(cuda, oracle):
+    """Splat ids spanning more than one 4096-word LDS bitmap (131072 ids)."""
+    from gsvc_amd import ops
+    n = 150000
+    ids = np.unique(np.concatenate([np.linspace(0, n - 1, 150).astype(np.int64),
+                                    [131071, 131072, 131073]]))
+    means, L, colors, opac, H, W = _clustered_frame(n, ids)
+    ref = oracle.render_sum(means, L, colors, opac, H, W)
+    tb = _tb(H, W)
+    xys, depths, radii, conics, nth = ops.project_gaussians_2d_forward(n, T(means), T(L), H, W, tb,
+                                                                      0.01)
+    m, gids, bins = _counted(n, xys, radii, tb)
+    np.testing.assert_array_equal(N(gids), ref["gids_sorted"])
+    np.testing.assert_array_equal(N(bins), ref["bins"][: tb[0] * tb[1]])
+
+
+def test_sized_fallback_same_as_sync_free(cuda):
+    """Untagged depths (not known to be zero) take the host-sized sorted path;
+    both paths give the same image and gradients."""
+    from gsplat.project_gaussians_2d import project_gaussians_2d
+    from gsplat.rasterize_sum import rasterize_gaussians_sum
+    z = load_golden("sum_64x96_n300")
+    H, W = int(z["H"]), int(z["W"])
+    outs, grads = [], []
+    for tagged in (True, False):
+        m = T(z["means2d"]).requires_grad_(True)
+        xys, depths, radii, conics, nth = project_gaussians_2d(m, T(z["L"]), H, W, _tb(H, W))
+        if not tagged:
+            depths = depths.clone()
+        out = rasterize_gaussians_sum(xys, depths, radii, conics, nth, T(z["colors"]),
+                                      T(z["opacity"]), H, W)
+        (out * T(z["v_out"])).sum().backward()
+        outs.append(out.detach())
+        grads.append(m.grad)
+    assert torch.equal(outs[0], outs[1])
+    # the backward accumulates per-tile records with float atomics: the
+    # summation order (not the set of terms) varies between runs
+    torch.testing.assert_close(grads[0], grads[1], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(N(outs[0]), z["out_img"], rtol=1e-6, atol=1e-5)
+
+
+def _op_path_frame(means, L, colors, opac, H, W, bg):
+    from gsplat.project_gaussians_2d import project_gaussians_2d
+    from gsplat.rasterize_sum import rasterize_gaussians_sum
+    xys, depths, radii, conics, nth = project_gaussians_2d(means, L, H, W, _tb(H, W))
+    out = rasterize_gaussians_sum(xys, depths, radii, conics, nth, colors, opac, H, W,
+                                  background=bg)
+    out = torch.clamp(out, 0, 1)
+    return out.view(-1, H, W, 3).permute(0, 3, 1, 2).contiguous()
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("case", ["sum_37x53_n120", "sum_stress_48x48_n700", "1080p_10k",
+                                  "1080p_50k"])
+def test_render_frame_matches_op_path(cuda, oracle, mode, case):
+    from gsvc_amd import _lib
+    from gsvc_amd.render import render_sum_frame
+    if case.startswith("sum_"):
+        z = load_golden(case)
+        H, W = int(z["H"]), int(z["W"])
+        means, L, colors, opac = z["means2d"], z["L"], z["colors"], z["opacity"]
+    else:
+        H, W = 1080, 1920
+        n = 10000 if case.endswith("10k") else 50000
+        means, L, colors, opac = oracle.synthetic_frame(n, seed=n + 1, rgb_w=2.0)
+    bg = torch.ones(3, device="cuda")
+    lib = _lib.load()
+    prev = lib.gsvc_debug_set(0, mode)
+    try:
+        fast = render_sum_frame(T(means), T(L), T(colors), T(opac), H, W, _tb(H, W), bg)
+    finally:
+        lib.gsvc_debug_set(0, prev)
+    with torch.no_grad():
+        ref = _op_path_frame(T(means), T(L), T(colors), T(opac), H, W, bg)
+    assert fast.shape == (1, 3, H, W) and fast.is_contiguous()
+    assert torch.equal(fast, ref)
+
+
+def test_render_frame_empty_is_background(cuda):
+    from gsvc_amd.render import render_sum_frame
+    z = load_golden("sum_empty_32x32_n10")
+    bg = torch.tensor([0.25, 1.5, -0.5], device="cuda")
+    fast = render_sum_frame(T(z["means2d"]), T(z["L"]), T(z["colors"]), T(z["opacity"]), 32, 32,
+                            _tb(32, 32), bg)
+    with torch.no_grad():
+        ref = _op_path_frame(T(z["means2d"]), T(z["L"]), T(z["colors"]), T(z["opacity"]), 32, 32,
+                             bg)
+    assert torch.equal(fast, ref)
+    np.testing.assert_array_equal(N(fast)[0, :, 0, 0], [0.25, 1.0, 0.0])
+
+
+def test_frame_model_forward_no_grad_matches_autograd(cuda):
+    from gsvc_amd.frame import make_frame_model
+    model = make_frame_model(72, 120, 500, cuda, seed=3)
+    with torch.no_grad():
+        fast = model()["render"]
+    slow = model()["render"]
+    assert slow.requires_grad
+    assert torch.equal(fast, slow.detach())

@@ -46,11 +46,11 @@ def setup(n, seed, chol_scale=1.0):
                 bg=torch.ones(3, device=dev), shape=shape, dev=dev)
 
 
-def fwd_args(s, out, idx):
+def fwd_args(s, out, idx, layout=0):
     tb = s["tb"]
-    return (s["shape"]["M"], tb[0], tb[1], 1, 16, 16, 1, W, H, 1, L.ptr(s["gids"]), L.ptr(s["bins"]), L.ptr(s["xys"]),
-            L.ptr(s["conics"]), L.ptr(s["colors"]), L.ptr(s["opac"]), L.ptr(s["bg"]), L.ptr(out),
-            None, L.ptr(idx), L.stream(s["dev"]))
+    return (tb[0], tb[1], 1, 16, 16, 1, W, H, 1, L.ptr(s["gids"]), L.ptr(s["bins"]), L.ptr(s["xys"]),
+            L.ptr(s["conics"]), L.ptr(s["colors"]), L.ptr(s["opac"]), L.ptr(s["bg"]), None,
+            s["shape"]["M"], layout, L.ptr(out), None, L.ptr(idx), L.stream(s["dev"]))
 
 
 def bwd_args(s, idx, v_out, rec):
@@ -105,7 +105,7 @@ def main():
             lib.gsvc_debug_set(3, v - 1000 if v >= 1000 else 0)
             out = torch.empty((H, W, 3), device=s["dev"])
             idx = torch.empty((H, W), dtype=torch.int32, device=s["dev"])
-            us = time_graph(lambda: L.call("gsvc_rasterize_sum_forward_auto", *fwd_args(s, out, idx)),
+            us = time_graph(lambda: L.call("gsvc_rasterize_sum_forward_ex", *fwd_args(s, out, idx)),
                             args.iters)
             if ref_out is None:
                 ref_out, ref_idx = out.clone(), idx.clone()
@@ -123,9 +123,9 @@ def main():
             idx = torch.empty((H, W), dtype=torch.int32, device=s["dev"])
             st = torch.zeros((s["shape"]["T"], 4), dtype=torch.int64, device=s["dev"])
             a = list(fwd_args(s, out, idx))
-            a[18] = L.ptr(st)
+            a[20] = L.ptr(st)
             for _ in range(3):
-                L.call("gsvc_rasterize_sum_forward_auto", *a)
+                L.call("gsvc_rasterize_sum_forward_ex", *a)
             torch.cuda.synchronize()
             t = st.cpu().numpy().astype(np.float64)
             t0 = t[:, 0].min()
@@ -142,7 +142,7 @@ def main():
             lib.gsvc_debug_set(0, 0)
             out = torch.empty((H, W, 3), device=s["dev"])
             idx = torch.empty((H, W), dtype=torch.int32, device=s["dev"])
-            L.call("gsvc_rasterize_sum_forward_auto", *fwd_args(s, out, idx))
+            L.call("gsvc_rasterize_sum_forward_ex", *fwd_args(s, out, idx))
             v_out = torch.randn((H, W, 3), device=s["dev"])
             rec_t = torch.empty((n, 16), device=s["dev"])
             us = time_graph(lambda: L.call("gsvc_rasterize_sum_backward",
