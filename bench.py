@@ -169,7 +169,9 @@ def main():
         for _ in range(args.warmup):
             model()
         torch.cuda.synchronize()
-        events = ops.enable_kernel_timing(True)
+        # HIP events around every 8th composite launch of the timed region,
+        # recorded by the library on the kernel's own stream
+        ops.composite_timing(True, max_launches=args.steps, every=8)
         barrier(world)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -178,9 +180,8 @@ def main():
         torch.cuda.synchronize()
         barrier(world)
         elapsed = time.perf_counter() - t0
-        kt = ops.kernel_times_ms("gsvc_rasterize_sum_forward_ex")
-        ops.enable_kernel_timing(False)
-        del events
+        kt = ops.composite_times_ms(args.steps)
+        ops.composite_timing(False)
     elapsed = all_max(elapsed, world, device)
     value = world * args.steps / elapsed
 

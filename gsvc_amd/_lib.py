@@ -29,6 +29,8 @@ _SIGS = {
     "gsvc_abi_version": [],
     "gsvc_last_error": [],
     "gsvc_debug_set": [_I, _I],
+    "gsvc_timing_enable": [_I, _I],
+    "gsvc_timing_collect": [_P, _I, _P],
     "gsvc_project_gaussians_2d_forward": [_I, _P, _P, _U, _U, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P],
     "gsvc_project_gaussians_2d_backward": [_I, _P, _P, _U, _U, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "gsvc_compute_cov2d_bounds": [_I, _P, _P, _P, _P],
@@ -46,6 +48,10 @@ _SIGS = {
                                    _P, _P, _P, _P],
     "gsvc_rasterize_sum_forward_ex": [_I, _I, _I, _I, _I, _I, _U, _U, _U, _P, _P, _P, _P, _P, _P,
                                       _P, _P, _I, _I, _P, _P, _P, _P],
+    "gsvc_render_frame_workspace_bytes": [_I, _U, _U, ctypes.c_longlong],
+    "gsvc_render_frame_zeroed_bytes": [_U, _U],
+    "gsvc_render_frame_sum": [_I, _P, _I, _P, _P, _P, _P, _P, _P, _U, _U, ctypes.c_longlong, _I, _P,
+                              _P, _SZ, _P, _P],
     "gsvc_rasterize_sum_backward": [_U, _U, _U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                     _P, _P],
     "gsvc_rasterize_forward": [_I, _I, _I, _I, _I, _I, _U, _U, _U, _P, _P, _P, _P, _P, _P, _P,
@@ -59,6 +65,8 @@ _RESTYPE = {
     "gsvc_sort_pairs_workspace_bytes": _SZ,
     "gsvc_bin_tiles_workspace_bytes": _SZ,
     "gsvc_bin_tiles_counted_workspace_bytes": _SZ,
+    "gsvc_render_frame_workspace_bytes": _SZ,
+    "gsvc_render_frame_zeroed_bytes": _SZ,
 }
 
 ABI_VERSION = 1

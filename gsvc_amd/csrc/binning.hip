@@ -17,7 +17,7 @@
 // the data path).  The general signed-int64 sort (used by the drop-in
 // bin_and_sort_gaussians when depth bits differ) runs the same kernels on all
 // 8 digits.
-#include "common.h"
+#include "binning.h"
 
 namespace gsvc {
 
@@ -392,47 +392,68 @@ __global__ __launch_bounds__(256) void tile_count_kernel(int n, const float2 *__
     if (i >= n) return;
     const int r = radii[i];
     if (r <= 0) return;
-    unsigned x0, y0, x1, y1;
     const float2 c = xys[i];
-    tile_bbox(c.x, c.y, (float)r, tbx, tby, x0, y0, x1, y1);
-    for (unsigned y = y0; y < y1; ++y)
-        for (unsigned x = x0; x < x1; ++x) atomicAdd(counts + y * (unsigned)tbx + x, 1u);
+    count_splat_tiles(c.x, c.y, r, tbx, tby, counts);
 }
 
-__global__ __launch_bounds__(1024) void tile_scan_kernel(int ntiles, const unsigned *__restrict__ counts,
+// One workgroup; tiles in chunks of 8192: every thread issues its 8 loads
+// (one per 1024-tile round, coalesced) up front, scans them per wave with
+// shuffles, and one LDS exchange of the 8 x 16 wave totals gives every
+// offset.  With zero_counts the counters are cleared for the next call (the
+// thread that read a counter clears it).
+constexpr int kTileScanRounds = 8;
+__global__ __launch_bounds__(1024) void tile_scan_kernel(int ntiles, unsigned *__restrict__ counts,
                                                          int2 *__restrict__ bins,
                                                          unsigned *__restrict__ cursor,
-                                                         int *__restrict__ meta, long long capacity) {
-    __shared__ unsigned ws[16];
-    const int per = (ntiles + 1023) / 1024;
-    const int b = threadIdx.x * per;
-    const int e = min(b + per, ntiles);
-    unsigned s = 0u;
-    for (int i = b; i < e; ++i) s += counts[i];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    unsigned incl = s;
+                                                         int *__restrict__ meta, long long capacity,
+                                                         int zero_counts) {
+    __shared__ unsigned s_tot[kTileScanRounds][16];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    unsigned carry = 0u;
+    for (int c0 = 0; c0 < ntiles; c0 += 1024 * kTileScanRounds) {
+        unsigned v[kTileScanRounds], incl[kTileScanRounds];
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const unsigned u = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += u;
+        for (int r = 0; r < kTileScanRounds; ++r) {
+            const int i = c0 + r * 1024 + tid;
+            v[r] = i < ntiles ? counts[i] : 0u;
+        }
+#pragma unroll
+        for (int r = 0; r < kTileScanRounds; ++r) {
+            unsigned x = v[r];
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const unsigned u = __shfl_up(x, off, 64);
+                if (lane >= off) x += u;
+            }
+            incl[r] = x;
+            if (lane == 63) s_tot[r][w] = x;
+        }
+        __syncthreads();
+        unsigned base = carry;
+#pragma unroll
+        for (int r = 0; r < kTileScanRounds; ++r) {
+            unsigned wo = 0u, rt = 0u;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const unsigned t = s_tot[r][k];
+                wo += (k < w) ? t : 0u;
+                rt += t;
+            }
+            const int i = c0 + r * 1024 + tid;
+            if (i < ntiles) {
+                const unsigned start = base + wo + incl[r] - v[r];
+                bins[i] = v[r] ? make_int2((int)start, (int)(start + v[r])) : make_int2(0, 0);
+                cursor[i] = start;
+                if (zero_counts) counts[i] = 0u;
+            }
+            base += rt;
+        }
+        carry = base;
+        __syncthreads();
     }
-    if (lane == 63) ws[w] = incl;
-    __syncthreads();
-    unsigned wo = 0u, tot = 0u;
-    for (int k = 0; k < 16; ++k) {
-        if (k < w) wo += ws[k];
-        tot += ws[k];
-    }
-    unsigned run = wo + incl - s;
-    for (int i = b; i < e; ++i) {
-        const unsigned c = counts[i];
-        bins[i] = c ? make_int2((int)run, (int)(run + c)) : make_int2(0, 0);
-        cursor[i] = run;
-        run += c;
-    }
-    if (threadIdx.x == 0) {
-        meta[0] = (int)tot;
-        meta[1] = (long long)tot > capacity ? 1 : 0;
+    if (tid == 0) {
+        meta[0] = (int)carry;
+        meta[1] = (long long)carry > capacity ? 1 : 0;
     }
 }
 
@@ -585,6 +606,23 @@ static int bits_for(int count) {
     int b = 0;
     while ((1ll << b) < (long long)count) ++b;
     return b;
+}
+
+int tile_bins_from_counts(int num_points, const float2 *xys, const int *radii, int tbx, int tby,
+                          long long capacity, unsigned *counts, unsigned *cursor, int *ids_scratch,
+                          int *ids_sorted, int2 *bins, int *meta, bool zero_counts,
+                          hipStream_t s) {
+    const int ntiles = tbx * tby;
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, ntiles, counts, bins, cursor, meta,
+                       capacity, zero_counts ? 1 : 0);
+    if (num_points > 0) {
+        hipLaunchKernelGGL(tile_fill_kernel, dim3(ceil_div(num_points, 256)), dim3(256), 0, s,
+                           num_points, xys, radii, tbx, tby, cursor, ids_scratch, capacity);
+        const int bm_words = min(ceil_div(num_points, 32) + 1, 4096);
+        hipLaunchKernelGGL(tile_segsort_kernel, dim3(ntiles), dim3(64), sizeof(unsigned) * bm_words, s,
+                           ntiles, (const int2 *)bins, ids_scratch, ids_sorted, bm_words, capacity);
+    }
+    return check_launch("tile binning");
 }
 
 }  // namespace gsvc
@@ -758,19 +796,10 @@ extern "C" int gsvc_bin_tiles_counted(int num_points, const float *xys, const in
     unsigned *cursor = (unsigned *)((char *)workspace + align_up(sizeof(unsigned) * (size_t)ntiles));
     if (hipMemsetAsync(counts, 0, sizeof(unsigned) * (size_t)ntiles, s) != hipSuccess)
         return set_error(GSVC_ERR_HIP, "bin_tiles_counted: memset failed");
-    const int nb = ceil_div(num_points > 0 ? num_points : 1, 256);
     if (num_points > 0)
-        hipLaunchKernelGGL(tile_count_kernel, dim3(nb), dim3(256), 0, s, num_points,
-                           (const float2 *)xys, radii, tbx, tby, counts);
-    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, ntiles, counts, (int2 *)tile_bins,
-                       cursor, meta, capacity);
-    if (num_points > 0) {
-        hipLaunchKernelGGL(tile_fill_kernel, dim3(nb), dim3(256), 0, s, num_points,
-                           (const float2 *)xys, radii, tbx, tby, cursor, ids_scratch, capacity);
-        const int bm_words = min(ceil_div(num_points, 32) + 1, 4096);
-        hipLaunchKernelGGL(tile_segsort_kernel, dim3(ntiles), dim3(64), sizeof(unsigned) * bm_words, s,
-                           ntiles, (const int2 *)tile_bins, ids_scratch, gaussian_ids_sorted, bm_words,
-                           capacity);
-    }
-    return check_launch("bin_tiles_counted");
+        hipLaunchKernelGGL(tile_count_kernel, dim3(ceil_div(num_points, 256)), dim3(256), 0, s,
+                           num_points, (const float2 *)xys, radii, tbx, tby, counts);
+    return tile_bins_from_counts(num_points, (const float2 *)xys, radii, tbx, tby, capacity, counts,
+                                 cursor, ids_scratch, gaussian_ids_sorted, (int2 *)tile_bins, meta,
+                                 false, s);
 }

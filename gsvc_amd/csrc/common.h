@@ -22,6 +22,8 @@ constexpr float kAlphaMin = 1.0f / 255.0f;
 int set_error(int code, const char *fmt, ...);
 int check_launch(const char *what);
 extern int g_knobs[8];  // gsvc_debug_set(); knob 0 = sum-forward variant
+int timing_begin(hipStream_t s);  // timing.hip: -1 when not recording
+void timing_end(hipStream_t s, int slot);
 
 // XCD-aware block -> work-item remap.  Blocks b and b+8 share an XCD (they are
 // dealt round-robin over the 8 XCDs), so give each XCD a contiguous range of

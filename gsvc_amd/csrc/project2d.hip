@@ -8,26 +8,9 @@
 // 92N backward).  Unlike the reference binding, which zero-fills
 // five outputs with torch::zeros before the launch, the kernel writes every
 // output element itself, so a call is exactly one kernel.
-#include "common.h"
+#include "project2d.h"
 
 namespace gsvc {
-
-// helpers.cuh:45-68 compute_cov2d_bounds
-__device__ __forceinline__ bool cov2d_bounds(float cxx, float cxy, float cyy,
-                                             float &c0, float &c1, float &c2, float &radius) {
-    const float det = cxx * cyy - cxy * cxy;
-    if (det == 0.0f) return false;
-    const float inv_det = 1.0f / det;
-    c0 = cyy * inv_det;
-    c1 = -cxy * inv_det;
-    c2 = cxx * inv_det;
-    const float b = 0.5f * (cxx + cyy);
-    const float disc = fmaxf(0.1f, b * b - det);
-    const float v1 = b + sqrtf(disc);
-    const float v2 = b - sqrtf(disc);
-    radius = ceilf(3.0f * sqrtf(fmaxf(v1, v2)));
-    return true;
-}
 
 __global__ __launch_bounds__(256) void project2d_fwd_kernel(
     int n, const float2 *__restrict__ means2d, const float *__restrict__ L,
@@ -37,25 +20,10 @@ __global__ __launch_bounds__(256) void project2d_fwd_kernel(
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float2 m = means2d[i];
-    const float l11 = L[3 * i], l21 = L[3 * i + 1], l22 = L[3 * i + 2];
-    const float cx = fmaf(hw, m.x, hw);
-    const float cy = fmaf(hh, m.y, hh);
-    const float cxx = l11 * l11;
-    const float cxy = l11 * l21;
-    const float cyy = l21 * l21 + l22 * l22;
-    float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, radius = 0.0f;
-    float2 xy = make_float2(0.0f, 0.0f);
-    int rad = 0, hit = 0;
-    if (cov2d_bounds(cxx, cxy, cyy, c0, c1, c2, radius)) {
-        xy = make_float2(cx, cy);
-        rad = cvt_i32(radius);
-        unsigned x0, y0, x1, y1;
-        tile_bbox(cx, cy, radius, tbx, tby, x0, y0, x1, y1);
-        const int area = (int)((x1 - x0) * (y1 - y0));
-        hit = area > 0 ? area : 0;
-    } else {
-        c0 = c1 = c2 = 0.0f;
-    }
+    const SplatProj P = project_splat(m.x, m.y, L[3 * i], L[3 * i + 1], L[3 * i + 2], hw, hh, tbx, tby);
+    const float2 xy = P.xy;
+    const float c0 = P.c0, c1 = P.c1, c2 = P.c2;
+    const int rad = P.rad, hit = P.hit;
     xys[i] = xy;
     depths[i] = 0.0f;
     radii[i] = rad;

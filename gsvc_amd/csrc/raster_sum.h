@@ -1,0 +1,39 @@
+// Sum rasterizer launch interface shared by raster_sum.hip and frame.hip.
+#pragma once
+
+#include "common.h"
+
+namespace gsvc {
+
+// Output layouts: kLayoutHWC is the reference's [H, W, 3] image (+ final_idx);
+// kLayoutCHWClamped writes torch.clamp(img, 0, 1) as planes [3, H, W], i.e. the
+// epilogue of GaussianSplats_Represent.py:88-89 (clamp, view, permute,
+// contiguous) fused into the store.
+enum { kLayoutHWC = 0, kLayoutCHWClamped = 1 };
+
+struct SumFwdArgs {
+    int tbx, img_w, img_h, ntiles, sparse_max, layout;
+    bool vec;      // HWC: W % 4 == 0 and 16-byte aligned outputs
+    bool vec_chw;  // CHW: W % 4 == 0, H*W % 4 == 0, 16-byte aligned
+    const int *m_dev;  // device num_intersects (NULL: > 0); 0 -> background
+    const float *bg;
+    const int *ids;
+    const int2 *bins;
+    const float2 *xys;
+    const float *conics, *colors, *opac;
+    // frame path: per-splat records {x, y, a/2, b}, {c/2, opacity, r, g},
+    // {b, -, -, -} replace the four arrays above (same values)
+    const float4 *rec;
+    float *out;
+    int *final_idx;
+    float *final_Ts;
+    long long *stamps;  // kModeStamp only
+};
+
+// sum_fwd_args_init zeroes every field (rec, stamps, m_dev NULL; HWC layout);
+// callers set the rest.  sum_forward_launch launches the kernel variant for
+// ``density_hint`` (or the gsvc_debug_set(0) override).
+void sum_fwd_args_init(SumFwdArgs &A);
+int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s);
+
+}  // namespace gsvc

@@ -36,7 +36,7 @@
 // per entry (shuffles + LDS), then one 64-byte-aligned 9-float record per
 // (splat, tile) is added with 9 lanes of one atomic instruction (one memory
 // request per entry instead of the reference's 9 per warp).
-#include "common.h"
+#include "raster_sum.h"
 
 namespace gsvc {
 
@@ -95,31 +95,25 @@ __device__ __forceinline__ bool ellipse_hits_rect(float x, float y, float a, flo
     return (x + ex >= x0) && (x - ex <= x1) && (y + ey >= y0) && (y - ey <= y1);
 }
 
-// Output layouts: kLayoutHWC is the reference's [H, W, 3] image (+ final_idx);
-// kLayoutCHWClamped writes torch.clamp(img, 0, 1) as planes [3, H, W], i.e. the
-// epilogue of GaussianSplats_Represent.py:88-89 (clamp, view, permute,
-// contiguous) fused into the store.
-enum { kLayoutHWC = 0, kLayoutCHWClamped = 1 };
-
-struct SumFwdArgs {
-    int tbx, img_w, img_h, ntiles, sparse_max, layout;
-    bool vec;      // HWC: W % 4 == 0 and 16-byte aligned outputs
-    bool vec_chw;  // CHW: W % 4 == 0, H*W % 4 == 0, 16-byte aligned
-    const int *m_dev;  // device num_intersects (NULL: > 0); 0 -> background
-    const float *bg;
-    const int *ids;
-    const int2 *bins;
-    const float2 *xys;
-    const float *conics, *colors, *opac;
-    float *out;
-    int *final_idx;
-    float *final_Ts;
-    long long *stamps;  // kModeStamp only
-};
-
 __device__ __forceinline__ float clamp01(float x) {
     // torch.clamp(x, 0, 1): NaN stays NaN
     return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x);
+}
+
+// Gather splat g: geo = {x, y, a/2, b}, col = {c/2, opacity, r, g}, blu = b.
+__device__ __forceinline__ void load_splat(const SumFwdArgs &A, int g, float4 &geo, float4 &col,
+                                           float &blu) {
+    if (A.rec) {
+        geo = A.rec[3 * g];
+        col = A.rec[3 * g + 1];
+        blu = A.rec[3 * g + 2].x;
+        return;
+    }
+    const float2 xy = A.xys[g];
+    const float a = A.conics[3 * g], b = A.conics[3 * g + 1], c = A.conics[3 * g + 2];
+    geo = make_float4(xy.x, xy.y, 0.5f * a, b);
+    col = make_float4(0.5f * c, A.opac[g], A.colors[3 * g], A.colors[3 * g + 1]);
+    blu = A.colors[3 * g + 2];
 }
 
 // Scalar store of one pixel in either layout.
@@ -158,12 +152,12 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
     for (int base = 0; base < n; base += kChunk) {
         const int cnt = min(kChunk, n - base);
         if (lane < cnt) {
-            const int g = A.ids[range.x + base + lane];
-            const float2 xy = A.xys[g];
-            const float a = A.conics[3 * g], b = A.conics[3 * g + 1], c = A.conics[3 * g + 2];
-            s_geo[lane] = make_float4(xy.x, xy.y, 0.5f * a, b);
-            s_col[lane] = make_float4(0.5f * c, A.opac[g], A.colors[3 * g], A.colors[3 * g + 1]);
-            s_blu[lane] = A.colors[3 * g + 2];
+            float4 geo, col;
+            float blu;
+            load_splat(A, A.ids[range.x + base + lane], geo, col, blu);
+            s_geo[lane] = geo;
+            s_col[lane] = col;
+            s_blu[lane] = blu;
         }
         wave_lds_sync();
         const int k0 = range.x + base;
@@ -267,14 +261,10 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
         float4 geo = make_float4(0.f, 0.f, 0.f, 0.f), col = geo;
         float blu = 0.f;
         if (j < n) {
-            const int g = A.ids[range.x + j];
-            const float2 xy = A.xys[g];
-            const float a = A.conics[3 * g], b = A.conics[3 * g + 1], c = A.conics[3 * g + 2];
-            const float o = A.opac[g];
-            geo = make_float4(xy.x, xy.y, 0.5f * a, b);
-            col = make_float4(0.5f * c, o, A.colors[3 * g], A.colors[3 * g + 1]);
-            blu = A.colors[3 * g + 2];
-            keep = ellipse_hits_rect(xy.x, xy.y, a, b, c, o, bx0, bx0 + 15.0f, by0, by0 + 7.0f);
+            load_splat(A, A.ids[range.x + j], geo, col, blu);
+            // 2 * (a/2) == a except for subnormal a, where culling is off anyway
+            keep = ellipse_hits_rect(geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, bx0,
+                                     bx0 + 15.0f, by0, by0 + 7.0f);
         }
         const unsigned long long m = __ballot(keep);
         if (keep) {
@@ -533,10 +523,6 @@ __global__ __launch_bounds__(256) void raster_sum_bwd_kernel(
     }
 }
 
-}  // namespace gsvc
-
-using namespace gsvc;
-
 static int check_tiles(const char *what, int bx, int by, int tbx, int tby, unsigned w, unsigned h) {
     if (bx != kTile || by != kTile)
         return set_error(GSVC_ERR_ARG, "%s: only 16x16 tiles are supported (got %dx%d)", what, bx, by);
@@ -545,6 +531,56 @@ static int check_tiles(const char *what, int bx, int by, int tbx, int tby, unsig
                          tby, w, h);
     return GSVC_OK;
 }
+
+void sum_fwd_args_init(SumFwdArgs &A) {
+    A = SumFwdArgs{};
+    A.sparse_max = g_knobs[3] > 0 ? g_knobs[3] : 8;
+    A.layout = kLayoutHWC;
+}
+
+int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
+    A.vec = (A.img_w % 4 == 0) && (((uintptr_t)A.out & 15) == 0) &&
+            (((uintptr_t)A.final_idx & 15) == 0) && (((uintptr_t)A.final_Ts & 15) == 0);
+    A.vec_chw = A.vec && (((size_t)A.img_w * (size_t)A.img_h) % 4 == 0);
+    const int ntiles = A.ntiles;
+    int mode = g_knobs[0];
+    if (mode == 0)
+        mode = ((long long)density_hint > (long long)kDenseEntriesPerTile * ntiles) ? kModeBanded
+                                                                                     : kModeSparse;
+    if (mode == kModeStamp && A.layout != kLayoutHWC)
+        return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: stamp mode needs the HWC layout");
+    const int tslot = timing_begin(s);
+    switch (mode) {
+        case kModeSparse:
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeSparse>, dim3(ntiles), dim3(64), 0, s, A);
+            break;
+        case kModeBanded:
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeBanded>, dim3(ntiles), dim3(128), 0, s, A);
+            break;
+        case kModeStamp:
+            A.stamps = reinterpret_cast<long long *>(A.final_Ts);
+            A.final_Ts = nullptr;
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeStamp>, dim3(ntiles), dim3(128), 0, s, A);
+            break;
+        case kModeNoBlend:
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeNoBlend>, dim3(ntiles), dim3(128), 0, s, A);
+            break;
+        case kModeNoStore:
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeNoStore>, dim3(ntiles), dim3(128), 0, s, A);
+            break;
+        case kModeAdaptive:
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeAdaptive>, dim3(ntiles), dim3(128), 0, s, A);
+            break;
+        default:
+            return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: unknown kernel mode %d", mode);
+    }
+    timing_end(s, tslot);
+    return check_launch("rasterize_sum_forward");
+}
+
+}  // namespace gsvc
+
+using namespace gsvc;
 
 extern "C" int gsvc_rasterize_sum_forward_ex(
     int tbx, int tby, int tbz, int block_x, int block_y, int block_z, unsigned img_width,
@@ -562,15 +598,12 @@ extern "C" int gsvc_rasterize_sum_forward_ex(
     const int ntiles = tbx * tby;
     if (ntiles == 0) return GSVC_OK;
     SumFwdArgs A;
+    sum_fwd_args_init(A);
     A.tbx = tbx;
     A.img_w = (int)img_width;
     A.img_h = (int)img_height;
     A.ntiles = ntiles;
-    A.sparse_max = g_knobs[3] > 0 ? g_knobs[3] : 8;
     A.layout = out_layout;
-    A.vec = (img_width % 4 == 0) && (((uintptr_t)out_img & 15) == 0) &&
-            (((uintptr_t)final_idx & 15) == 0) && (((uintptr_t)final_Ts & 15) == 0);
-    A.vec_chw = A.vec && (((size_t)img_width * img_height) % 4 == 0);
     A.m_dev = num_intersects_dev;
     A.bg = background;
     A.ids = gaussian_ids_sorted;
@@ -582,39 +615,7 @@ extern "C" int gsvc_rasterize_sum_forward_ex(
     A.out = out_img;
     A.final_idx = final_idx;
     A.final_Ts = final_Ts;
-    A.stamps = nullptr;
-    hipStream_t s = (hipStream_t)stream;
-    int mode = g_knobs[0];
-    if (mode == 0)
-        mode = ((long long)density_hint > (long long)kDenseEntriesPerTile * ntiles) ? kModeBanded
-                                                                                     : kModeSparse;
-    if (mode == kModeStamp && out_layout != kLayoutHWC)
-        return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: stamp mode needs the HWC layout");
-    switch (mode) {
-        case kModeSparse:
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeSparse>, dim3(ntiles), dim3(64), 0, s, A);
-            break;
-        case kModeBanded:
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeBanded>, dim3(ntiles), dim3(128), 0, s, A);
-            break;
-        case kModeStamp:
-            A.final_Ts = nullptr;
-            A.stamps = reinterpret_cast<long long *>(final_Ts);
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeStamp>, dim3(ntiles), dim3(128), 0, s, A);
-            break;
-        case kModeNoBlend:
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeNoBlend>, dim3(ntiles), dim3(128), 0, s, A);
-            break;
-        case kModeNoStore:
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeNoStore>, dim3(ntiles), dim3(128), 0, s, A);
-            break;
-        case kModeAdaptive:
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeAdaptive>, dim3(ntiles), dim3(128), 0, s, A);
-            break;
-        default:
-            return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: unknown kernel mode %d", mode);
-    }
-    return check_launch("rasterize_sum_forward");
+    return sum_forward_launch(A, density_hint, (hipStream_t)stream);
 }
 
 extern "C" int gsvc_rasterize_sum_forward(int tbx, int tby, int tbz, int block_x, int block_y,

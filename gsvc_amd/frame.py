@@ -19,7 +19,7 @@ import torch.nn.functional as F
 from .adan import Adan
 from .project_gaussians_2d import project_gaussians_2d
 from .rasterize_sum import rasterize_gaussians_sum
-from .render import render_sum_frame
+from .render import render_frame_sum
 
 
 def loss_fn(pred, target, loss_type="L2", lambda_value=0.7):
@@ -99,13 +99,14 @@ class GaussianVideoFrame(nn.Module):
         return o
 
     def forward(self):
-        if not torch.is_grad_enabled():
+        if not torch.is_grad_enabled() and self.BLOCK_H == 16 and self.BLOCK_W == 16:
             # inference: same image from the sync-free path with the clamp +
             # NCHW epilogue fused into the rasterizer (gsvc_amd/render.py)
-            return {"render": render_sum_frame(self.get_xyz, self.get_cholesky_elements,
-                                               self.get_features, self._ones_opacity(), self.H,
-                                               self.W, self.tile_bounds, self.background,
-                                               self.BLOCK_H, self.BLOCK_W)}
+            # (activations fused into the frame kernel: tanh, + bound, * rgb_W)
+            return {"render": render_frame_sum(self._xyz, self._cholesky, self._features_dc,
+                                               self.H, self.W, self.background, xyz_tanh=True,
+                                               cholesky_bound=self.cholesky_bound,
+                                               rgb_w=self.rgb_W)}
         # reference: torch.ones(N, 1).to(device) per call; same values
         _opacity = self._ones_opacity()
         self.xys, depths, self.radii, conics, num_tiles_hit = project_gaussians_2d(

@@ -33,11 +33,33 @@ TILE = 16
 _kernel_events = None
 
 
-def enable_kernel_timing(on: bool = True):
-    """Start (or stop) recording (name, start_event, end_event) per rasterizer launch."""
-    global _kernel_events
+_timing_every = 1
+_timing_calls = 0
+
+
+def enable_kernel_timing(on: bool = True, every: int = 1):
+    """Start (or stop) recording (name, start_event, end_event) around the
+    rasterizer launches -- every ``every``-th call, so that the event records
+    do not slow the loop being measured."""
+    global _kernel_events, _timing_every, _timing_calls
     _kernel_events = [] if on else None
+    _timing_every = max(1, int(every))
+    _timing_calls = 0
     return _kernel_events
+
+
+def composite_timing(on: bool, max_launches: int = 4096, every: int = 1):
+    """C-side HIP-event timing of the sum-forward kernel launches (every
+    entry point, including the fused frame render); see gsvc_timing_enable."""
+    L.call("gsvc_timing_enable", int(max_launches) if on else 0, int(every))
+
+
+def composite_times_ms(max_launches: int = 4096):
+    import ctypes
+    buf = (ctypes.c_float * max_launches)()
+    cnt = ctypes.c_int(0)
+    L.call("gsvc_timing_collect", ctypes.addressof(buf), max_launches, ctypes.addressof(cnt))
+    return list(buf[: cnt.value])
 
 
 def kernel_times_ms(name: str):
@@ -49,7 +71,12 @@ def kernel_times_ms(name: str):
 
 
 def _timed_call(sym, *args):
+    global _timing_calls
     if _kernel_events is None:
+        L.call(sym, *args)
+        return
+    _timing_calls += 1
+    if (_timing_calls - 1) % _timing_every:
         L.call(sym, *args)
         return
     s = torch.cuda.Event(enable_timing=True)

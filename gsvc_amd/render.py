@@ -1,18 +1,24 @@
 """Forward-only frame render: the inference side of GSVC's hot path.
 
-``render_sum_frame`` computes exactly what GSVC's frame forward
-(GaussianSplats_Represent.py:83-90) returns --
+``render_frame_sum`` computes exactly what GSVC's frame forward
+(GaussianSplats_Represent.py:57-90) returns --
 
+    means2d = tanh(_xyz); L = _cholesky + cholesky_bound; colors = _features_dc * rgb_W
     xys, depths, radii, conics, nth = project_gaussians_2d(means2d, L, H, W, tb)
-    img = rasterize_gaussians_sum(xys, depths, radii, conics, nth, colors, opacity, H, W)
+    img = rasterize_gaussians_sum(xys, depths, radii, conics, nth, colors, ones, H, W)
     img = torch.clamp(img, 0, 1).view(-1, H, W, 3).permute(0, 3, 1, 2).contiguous()
 
--- as four device steps with no host synchronisation: the projection kernel,
-the sync-free tile binning (binning.hip, tile_count/scan/fill/segsort), and
-the sum rasterizer writing clamp(img) straight into the [1, 3, H, W] planes
-(the clamp + permute + contiguous epilogue fused into its store, final_idx not
-written since no backward follows).  Results are bit-identical to the
-autograd path (tests/test_gpu_parity.py::test_render_frame_matches_op_path).
+-- in ONE C call (gsvc_render_frame_sum, csrc/frame.hip) with no host
+synchronisation: a fused activation + projection + tile-count kernel, the
+sync-free tile binning (scan / fill / per-tile segment sort), and the sum
+rasterizer writing clamp(img) straight into the [1, 3, H, W] planes (final_idx
+is not written: no backward follows).  The workspace (intermediates and the
+intersection buffers, capacity N * tiles) is cached per device and stream and
+reused across frames.  Results are bit-identical to the autograd path
+(tests/test_gpu_sync_free.py).
+
+``render_sum_frame`` is the same for already-activated inputs (means2d, L,
+colors, opacity), the signature of the two reference ops it replaces.
 """
 from __future__ import annotations
 
@@ -21,15 +27,106 @@ from typing import Optional, Tuple
 import torch
 from torch import Tensor
 
+from . import _lib as L
 from . import ops as _C
-from .utils import bin_for_raster
+from .utils import BIN_CAPACITY_BUDGET, _LazyCount, bin_for_raster
+
+
+class _FrameWorkspace:
+    def __init__(self):
+        self.buf = None
+        self.hw = None
+        self.dirty = True
+        self.meta = None
+        self.hint = _LazyCount()
+
+
+_workspaces = {}
+
+
+def _workspace(dev: torch.device, n: int, H: int, W: int, cap: int) -> _FrameWorkspace:
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    fw = _workspaces.get(key)
+    if fw is None:
+        fw = _workspaces[key] = _FrameWorkspace()
+        fw.meta = torch.zeros((2,), dtype=torch.int32, device=dev)
+    need = L.size("gsvc_render_frame_workspace_bytes", n, H, W, cap)
+    if fw.buf is None or fw.buf.numel() < need:
+        fw.buf = torch.empty((need,), dtype=torch.uint8, device=dev)
+        fw.dirty = True
+    if fw.dirty or fw.hw != (H, W):
+        # the per-tile counters start at zero; every call leaves them zero
+        fw.buf[: L.size("gsvc_render_frame_zeroed_bytes", H, W)].zero_()
+        fw.hw = (H, W)
+        fw.dirty = False
+    return fw
+
+
+def _f32c(t: Optional[Tensor], name: str) -> Optional[Tensor]:
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be a CUDA tensor")
+    return t.detach().to(torch.float32).contiguous()
+
+
+def render_frame_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, img_height: int,
+                     img_width: int, background: Tensor, xyz_tanh: bool = True,
+                     cholesky_bound: Optional[Tensor] = None, rgb_w: Optional[Tensor] = None,
+                     opacity: Optional[Tensor] = None) -> Tensor:
+    """One frame of GSVC's model to a clamped [1, 3, H, W] image (no autograd).
+
+    xyz [N,2] (tanh applied when ``xyz_tanh``), cholesky [N,3] (+ bound [3]),
+    features [N,3] (* rgb_w [N,1]), opacity [N,1] or None for ones.
+    """
+    H, W = int(img_height), int(img_width)
+    n = xyz.shape[0]
+    dev = xyz.device
+    ntiles = ((W + 15) // 16) * ((H + 15) // 16)
+    cap = n * ntiles
+    if cap > BIN_CAPACITY_BUDGET:
+        # intersection buffers too large to reserve: sized (host-synchronised) path
+        with torch.no_grad():
+            means2d = torch.tanh(xyz) if xyz_tanh else xyz
+            Lc = cholesky + cholesky_bound if cholesky_bound is not None else cholesky
+            colors = features * rgb_w if rgb_w is not None else features
+            opac = opacity if opacity is not None else torch.ones(n, 1, device=dev)
+            return _render_sum_frame_ops(means2d, Lc, colors, opac, H, W,
+                                         ((W + 15) // 16, (H + 15) // 16, 1), background)
+    xyz_c = _f32c(xyz, "xyz")
+    chol_c = _f32c(cholesky, "cholesky")
+    feat_c = _f32c(features, "features")
+    bound_c = _f32c(cholesky_bound, "cholesky_bound")
+    rgbw_c = _f32c(rgb_w, "rgb_w")
+    opac_c = _f32c(opacity, "opacity")
+    bg_c = _f32c(background, "background")
+    if xyz_c.shape != (n, 2) or chol_c.shape != (n, 3) or feat_c.shape != (n, 3):
+        raise ValueError("xyz [N,2], cholesky [N,3] and features [N,3] expected")
+    if bg_c.numel() != 3 or (bound_c is not None and bound_c.numel() != 3):
+        raise ValueError("background and cholesky_bound need 3 elements")
+    for t, nm in ((rgbw_c, "rgb_w"), (opac_c, "opacity")):
+        if t is not None and t.numel() != n:
+            raise ValueError(f"{nm} needs N elements")
+    fw = _workspace(dev, n, H, W, cap)
+    out = torch.empty((1, 3, H, W), dtype=torch.float32, device=dev)
+    hint = fw.hint.value
+    try:
+        L.call("gsvc_render_frame_sum", n, L.ptr(xyz_c), 1 if xyz_tanh else 0, L.ptr(chol_c),
+               L.ptr(bound_c), L.ptr(feat_c), L.ptr(rgbw_c), L.ptr(opac_c), L.ptr(bg_c), H, W, cap,
+               hint, L.ptr(fw.meta), L.ptr(fw.buf), fw.buf.numel(), L.ptr(out), L.stream(dev))
+    except Exception:
+        fw.dirty = True
+        raise
+    fw.hint.update(fw.meta)
+    return out
 
 
 def render_sum_frame(means2d: Tensor, L_elements: Tensor, colors: Tensor, opacity: Tensor,
                      img_height: int, img_width: int, tile_bounds: Tuple[int, int, int],
                      background: Optional[Tensor] = None, BLOCK_H: int = 16, BLOCK_W: int = 16,
-                     clip_thresh: float = 0.01, out: Optional[Tensor] = None) -> Tensor:
-    """Render one frame to a clamped [1, 3, H, W] float32 image (no autograd)."""
+                     clip_thresh: float = 0.01) -> Tensor:
+    """project_gaussians_2d + rasterize_gaussians_sum + clamp + NCHW for
+    activated inputs, as one frame render (no autograd)."""
     if BLOCK_H != 16 or BLOCK_W != 16:
         raise ValueError("only 16x16 tiles are supported (reference config.h:1-2)")
     if colors.dtype == torch.uint8:
@@ -40,7 +137,13 @@ def render_sum_frame(means2d: Tensor, L_elements: Tensor, colors: Tensor, opacit
         raise AttributeError("nd_rasterize_sum_forward: only 3-channel colors are supported")
     if background is None:
         background = torch.ones(3, dtype=torch.float32, device=colors.device)
-    H, W = int(img_height), int(img_width)
+    return render_frame_sum(means2d, L_elements, colors, img_height, img_width, background,
+                            xyz_tanh=False, opacity=opacity)
+
+
+def _render_sum_frame_ops(means2d, L_elements, colors, opacity, H, W, tile_bounds, background,
+                          clip_thresh=0.01):
+    """The same render composed from the ops (used above the capacity budget)."""
     n = means2d.shape[-2]
     with torch.no_grad():
         xys, depths, radii, conics, nth = _C.project_gaussians_2d_forward(
@@ -48,14 +151,10 @@ def render_sum_frame(means2d: Tensor, L_elements: Tensor, colors: Tensor, opacit
         binned = bin_for_raster(n, xys, depths, radii, nth, tile_bounds)
         if binned.num_intersects is not None and binned.num_intersects < 1:
             img = torch.clamp(background.view(3, 1, 1).expand(3, H, W), 0, 1)
-            if out is None:
-                return img.reshape(1, 3, H, W).contiguous()
-            out.view(3, H, W).copy_(img)
-            return out.view(1, 3, H, W)
+            return img.reshape(1, 3, H, W).contiguous()
         img, _ = _C.rasterize_sum_forward_ex(
-            tile_bounds, (BLOCK_W, BLOCK_H, 1), (W, H, 1), binned.gaussian_ids_sorted,
-            binned.tile_bins, xys, conics, colors.contiguous(), opacity.contiguous(),
-            background.contiguous(), num_intersects_dev=binned.m_dev,
-            density_hint=binned.density_hint, layout=_C.LAYOUT_CHW_CLAMPED, want_idx=False,
-            out=out)
+            tile_bounds, (16, 16, 1), (W, H, 1), binned.gaussian_ids_sorted, binned.tile_bins, xys,
+            conics, colors.contiguous(), opacity.contiguous(), background.contiguous(),
+            num_intersects_dev=binned.m_dev, density_hint=binned.density_hint,
+            layout=_C.LAYOUT_CHW_CLAMPED, want_idx=False)
     return img.view(1, 3, H, W)

@@ -47,6 +47,14 @@ enum gsvc_status {
 int gsvc_abi_version(void);
 const char *gsvc_last_error(void);
 
+/* Launch timing of the sum-forward composite kernel (every rasterizer entry
+ * point above): after gsvc_timing_enable(max, every), every every-th launch
+ * is bracketed by HIP events recorded on its stream (up to max launches);
+ * gsvc_timing_collect waits for them and writes the durations in ms.
+ * gsvc_timing_enable(0, 0) stops and frees.  Not part of the reference. */
+int gsvc_timing_enable(int max_launches, int every);
+int gsvc_timing_collect(float *ms, int max_out, int *count);
+
 /* Tuning / A-B knob for kernel variants (tools/kbench.py).  key 0 forces the
  * sum-forward kernel mode (0 = automatic), key 3 the per-tile threshold of
  * mode 6; returns the previous value.  Not part of the reference interface;
@@ -193,6 +201,31 @@ int gsvc_rasterize_sum_forward_ex(
     const float *opacities, const float *background,
     const int *num_intersects_dev, int density_hint, int out_layout,
     float *out_img, float *final_Ts, int *final_idx, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Whole-frame render of GSVC's per-frame model (GaussianSplats_Represent.py:
+ * 57-90) in one call, no host synchronisation: out[3,H,W] =
+ * clamp(rasterize_gaussians_sum(project_gaussians_2d(means2d, L)), 0, 1)
+ * permuted to planes, with
+ *   means2d = xyz_tanh ? tanh(xyz) : xyz            xyz [N,2]
+ *   L       = cholesky + cholesky_bound (if given)   cholesky [N,3], bound [3]
+ *   colors  = features * rgb_w (if given)            features [N,3], rgb_w [N]
+ *   opacity = opacity (if given) else 1              [N]
+ * Results are bit-identical to the op path.  meta (device int[2]) <- {M,
+ * M > capacity}; capacity = N * tiles never overflows.  The workspace
+ * (gsvc_render_frame_workspace_bytes) must have its first
+ * gsvc_render_frame_zeroed_bytes zero before the first call; every call
+ * leaves them zero.  density_hint as in gsvc_rasterize_sum_forward_ex. */
+size_t gsvc_render_frame_workspace_bytes(int num_points, unsigned img_height,
+                                         unsigned img_width, long long capacity);
+size_t gsvc_render_frame_zeroed_bytes(unsigned img_height, unsigned img_width);
+int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_tanh,
+                          const float *cholesky, const float *cholesky_bound,
+                          const float *features, const float *rgb_w,
+                          const float *opacity, const float *background,
+                          unsigned img_height, unsigned img_width, long long capacity,
+                          int density_hint, int *meta, void *workspace,
+                          size_t workspace_bytes, float *out, void *stream);
 
 /* Replaces _C.rasterize_sum_backward (bindings.cu:706-779 -> backward.cu:696-862).
  * Gradients are written into one 64-byte record per splat,

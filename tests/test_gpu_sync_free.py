@@ -206,11 +206,56 @@ def test_render_frame_empty_is_background(cuda):
     np.testing.assert_array_equal(N(fast)[0, :, 0, 0], [0.25, 1.0, 0.0])
 
 
-def test_frame_model_forward_no_grad_matches_autograd(cuda):
-    from gsvc_amd.frame import make_frame_model
-    model = make_frame_model(72, 120, 500, cuda, seed=3)
+@pytest.mark.parametrize("H,W,n", [(72, 120, 500), (1080, 1920, 10000), (1080, 1920, 50000)])
+def test_frame_model_forward_no_grad_matches_autograd(cuda, H, W, n):
+    """The fused frame entry (tanh, + bound, * rgb_W in its kernel) against
+    GaussianVideoFrame's op-by-op autograd forward, after some training so
+    rgb_W and the Cholesky factors are not at their init values."""
+    from gsvc_amd.frame import make_frame_model, synthetic_gt
+    model = make_frame_model(H, W, n, cuda, seed=3, isdensity=True)
+    gt = synthetic_gt(H, W, 5, cuda)
+    for it in range(1, 4):
+        model.train_iter(gt, it)
     with torch.no_grad():
         fast = model()["render"]
+        again = model()["render"]  # workspace reuse (counters left at zero)
     slow = model()["render"]
     assert slow.requires_grad
     assert torch.equal(fast, slow.detach())
+    assert torch.equal(again, fast)
+
+
+def test_frame_workspace_reuse_across_sizes(cuda):
+    from gsvc_amd.frame import make_frame_model
+    a = make_frame_model(72, 120, 300, cuda, seed=4)
+    b = make_frame_model(40, 56, 200, cuda, seed=5)
+    with torch.no_grad():
+        ra = a()["render"]
+        rb = b()["render"]
+        ra2 = a()["render"]
+        rb2 = b()["render"]
+    assert torch.equal(ra, ra2) and torch.equal(rb, rb2)
+    assert torch.equal(rb, b()["render"].detach())
+
+
+def test_tanh_matches_torch(cuda):
+    """The frame kernel's tanhf against torch.tanh, bit for bit, over a
+    sweep of magnitudes (the activation of _xyz)."""
+    from gsvc_amd.render import render_frame_sum
+    x = torch.cat([torch.linspace(-12, 12, 20001), torch.randn(20000) * 3,
+                   torch.tensor([0.0, -0.0, 1e-30, -1e-30, 1e-8, 20.0, -20.0])]).cuda()
+    n = x.numel() // 2
+    xyz = x[: 2 * n].view(n, 2)
+    # render a 16x16 frame: means2d only matter through xys; compare xys via
+    # the op path instead -- tanh is checked on the projected centres
+    from gsvc_amd import ops
+    ref = ops.project_gaussians_2d_forward(n, torch.tanh(xyz), torch.ones(n, 3, device="cuda"),
+                                           16, 16, (1, 1, 1), 0.01)[0]
+    out = render_frame_sum(xyz, torch.ones(n, 3, device="cuda"), torch.zeros(n, 3, device="cuda"),
+                           16, 16, torch.zeros(3, device="cuda"))
+    assert out.shape == (1, 3, 16, 16)
+    from gsvc_amd.render import _workspaces
+    fw = _workspaces[(0, torch.cuda.current_stream().cuda_stream)]
+    off = 3 * 256  # counts, cursor, bins slots (each 256-byte aligned)
+    xys = fw.buf[off: off + 8 * n].view(torch.float32).view(n, 2)
+    assert torch.equal(xys, ref)
