@@ -48,10 +48,10 @@ _SIGS = {
                                    _P, _P, _P, _P],
     "gsvc_rasterize_sum_forward_ex": [_I, _I, _I, _I, _I, _I, _U, _U, _U, _P, _P, _P, _P, _P, _P,
                                       _P, _P, _I, _I, _P, _P, _P, _P],
-    "gsvc_render_frame_workspace_bytes": [_I, _U, _U, ctypes.c_longlong],
+    "gsvc_render_frame_workspace_bytes": [_I, _U, _U],
     "gsvc_render_frame_zeroed_bytes": [_U, _U],
-    "gsvc_render_frame_sum": [_I, _P, _I, _P, _P, _P, _P, _P, _P, _U, _U, ctypes.c_longlong, _I, _P,
-                              _P, _SZ, _P, _P],
+    "gsvc_render_frame_sum": [_I, _P, _I, _P, _P, _P, _P, _P, _P, _U, _U, _I, _I, _P, _P, _SZ, _P,
+                              _P],
     "gsvc_rasterize_sum_backward": [_U, _U, _U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                     _P, _P],
     "gsvc_rasterize_forward": [_I, _I, _I, _I, _I, _I, _U, _U, _U, _P, _P, _P, _P, _P, _P, _P,

@@ -8,11 +8,76 @@ namespace gsvc {
 // Given per-tile entry counts (counts[tbx*tby], already accumulated on the
 // stream), launches scan -> fill -> per-tile segment sort: tile_bins,
 // ids_sorted in (tile, splat id) order, meta = {M, M > capacity}.  With
-// zero_counts the scan clears counts for the next call.
+// zero_counts the scan clears counts for the next call.  counts NULL skips the
+// scan (the producer ran scan_tile_counts itself); ids_sorted NULL skips the
+// segment sort (ids_scratch then holds each tile's ids in fill order).
 int tile_bins_from_counts(int num_points, const float2 *xys, const int *radii, int tbx, int tby,
                           long long capacity, unsigned *counts, unsigned *cursor, int *ids_scratch,
                           int *ids_sorted, int2 *bins, int *meta, bool zero_counts,
                           hipStream_t s);
+
+// Exclusive scan of the per-tile counts by one workgroup of kThreads threads:
+// tiles in chunks of kR * kThreads, every thread issuing its kR loads (one per
+// round, coalesced) up front -- one memory round trip per chunk -- wave scans by shuffles, one LDS exchange of the
+// wave totals per chunk.  Writes tile_bins ((0,0) when empty), the fill
+// cursors and meta = {M, M > capacity}; with zero_counts the reading thread
+// clears each counter for the next call.
+template <int kThreads, int kR = 8>
+__device__ __forceinline__ void scan_tile_counts(int ntiles, unsigned *__restrict__ counts,
+                                                 int2 *__restrict__ bins,
+                                                 unsigned *__restrict__ cursor,
+                                                 int *__restrict__ meta, long long capacity,
+                                                 bool zero_counts) {
+    constexpr int kW = kThreads / 64;
+    __shared__ unsigned s_tot[kR][kW];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    unsigned carry = 0u;
+    for (int c0 = 0; c0 < ntiles; c0 += kThreads * kR) {
+        unsigned v[kR], incl[kR];
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+            const int i = c0 + r * kThreads + tid;
+            v[r] = i < ntiles ? counts[i] : 0u;
+        }
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+            unsigned x = v[r];
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const unsigned u = __shfl_up(x, off, 64);
+                if (lane >= off) x += u;
+            }
+            incl[r] = x;
+            if (lane == 63) s_tot[r][w] = x;
+        }
+        __syncthreads();
+        unsigned base = carry;
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+            unsigned wo = 0u, rt = 0u;
+#pragma unroll
+            for (int k = 0; k < kW; ++k) {
+                const unsigned t = s_tot[r][k];
+                wo += (k < w) ? t : 0u;
+                rt += t;
+            }
+            const int i = c0 + r * kThreads + tid;
+            if (i < ntiles) {
+                const unsigned start = base + wo + incl[r] - v[r];
+                bins[i] = v[r] ? make_int2((int)start, (int)(start + v[r])) : make_int2(0, 0);
+                cursor[i] = start;
+                if (zero_counts) counts[i] = 0u;
+            }
+            base += rt;
+        }
+        carry = base;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        meta[0] = (int)carry;
+        meta[1] = (long long)carry > capacity ? 1 : 0;
+    }
+}
 
 // Per-tile entry counting of one splat's bbox (tile_count_kernel's body).
 __device__ __forceinline__ void count_splat_tiles(float cx, float cy, int r, int tbx, int tby,

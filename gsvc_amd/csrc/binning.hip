@@ -396,67 +396,16 @@ __global__ __launch_bounds__(256) void tile_count_kernel(int n, const float2 *__
     count_splat_tiles(c.x, c.y, r, tbx, tby, counts);
 }
 
-// One workgroup; tiles in chunks of 8192: every thread issues its 8 loads
-// (one per 1024-tile round, coalesced) up front, scans them per wave with
-// shuffles, and one LDS exchange of the 8 x 16 wave totals gives every
-// offset.  With zero_counts the counters are cleared for the next call (the
-// thread that read a counter clears it).
-constexpr int kTileScanRounds = 8;
 __global__ __launch_bounds__(1024) void tile_scan_kernel(int ntiles, unsigned *__restrict__ counts,
                                                          int2 *__restrict__ bins,
                                                          unsigned *__restrict__ cursor,
                                                          int *__restrict__ meta, long long capacity,
                                                          int zero_counts) {
-    __shared__ unsigned s_tot[kTileScanRounds][16];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    unsigned carry = 0u;
-    for (int c0 = 0; c0 < ntiles; c0 += 1024 * kTileScanRounds) {
-        unsigned v[kTileScanRounds], incl[kTileScanRounds];
-#pragma unroll
-        for (int r = 0; r < kTileScanRounds; ++r) {
-            const int i = c0 + r * 1024 + tid;
-            v[r] = i < ntiles ? counts[i] : 0u;
-        }
-#pragma unroll
-        for (int r = 0; r < kTileScanRounds; ++r) {
-            unsigned x = v[r];
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const unsigned u = __shfl_up(x, off, 64);
-                if (lane >= off) x += u;
-            }
-            incl[r] = x;
-            if (lane == 63) s_tot[r][w] = x;
-        }
-        __syncthreads();
-        unsigned base = carry;
-#pragma unroll
-        for (int r = 0; r < kTileScanRounds; ++r) {
-            unsigned wo = 0u, rt = 0u;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const unsigned t = s_tot[r][k];
-                wo += (k < w) ? t : 0u;
-                rt += t;
-            }
-            const int i = c0 + r * 1024 + tid;
-            if (i < ntiles) {
-                const unsigned start = base + wo + incl[r] - v[r];
-                bins[i] = v[r] ? make_int2((int)start, (int)(start + v[r])) : make_int2(0, 0);
-                cursor[i] = start;
-                if (zero_counts) counts[i] = 0u;
-            }
-            base += rt;
-        }
-        carry = base;
-        __syncthreads();
-    }
-    if (tid == 0) {
-        meta[0] = (int)carry;
-        meta[1] = (long long)carry > capacity ? 1 : 0;
-    }
+    scan_tile_counts<1024>(ntiles, counts, bins, cursor, meta, capacity, zero_counts != 0);
 }
 
+// The cursor atomics of a splat are issued in batches of 8 before any of
+// their results is waited for (one round trip per batch, not per tile).
 __global__ __launch_bounds__(256) void tile_fill_kernel(int n, const float2 *__restrict__ xys,
                                                         const int *__restrict__ radii, int tbx, int tby,
                                                         unsigned *__restrict__ cursor,
@@ -468,11 +417,25 @@ __global__ __launch_bounds__(256) void tile_fill_kernel(int n, const float2 *__r
     unsigned x0, y0, x1, y1;
     const float2 c = xys[i];
     tile_bbox(c.x, c.y, (float)r, tbx, tby, x0, y0, x1, y1);
+    constexpr int kBatch = 8;
+    unsigned tl[kBatch];
+    int cnt = 0;
+    auto flush = [&]() {
+        unsigned sl[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k)
+            if (k < cnt) sl[k] = atomicAdd(cursor + tl[k], 1u);
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k)
+            if (k < cnt && (long long)sl[k] < capacity) ids[sl[k]] = i;
+        cnt = 0;
+    };
     for (unsigned y = y0; y < y1; ++y)
         for (unsigned x = x0; x < x1; ++x) {
-            const unsigned slot = atomicAdd(cursor + y * (unsigned)tbx + x, 1u);
-            if ((long long)slot < capacity) ids[slot] = i;
+            tl[cnt < kBatch ? cnt : 0] = y * (unsigned)tbx + x;
+            if (++cnt == kBatch) flush();
         }
+    if (cnt) flush();
 }
 
 // One wave per tile; ``bm`` is ``bm_words`` words of dynamic LDS.
@@ -613,11 +576,14 @@ int tile_bins_from_counts(int num_points, const float2 *xys, const int *radii, i
                           int *ids_sorted, int2 *bins, int *meta, bool zero_counts,
                           hipStream_t s) {
     const int ntiles = tbx * tby;
-    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, ntiles, counts, bins, cursor, meta,
-                       capacity, zero_counts ? 1 : 0);
+    if (counts)  // NULL: the producer already scanned (bins, cursor, meta written)
+        hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, ntiles, counts, bins, cursor,
+                           meta, capacity, zero_counts ? 1 : 0);
     if (num_points > 0) {
         hipLaunchKernelGGL(tile_fill_kernel, dim3(ceil_div(num_points, 256)), dim3(256), 0, s,
                            num_points, xys, radii, tbx, tby, cursor, ids_scratch, capacity);
+    }
+    if (num_points > 0 && ids_sorted) {  // NULL: the consumer sorts each tile itself
         const int bm_words = min(ceil_div(num_points, 32) + 1, 4096);
         hipLaunchKernelGGL(tile_segsort_kernel, dim3(ntiles), dim3(64), sizeof(unsigned) * bm_words, s,
                            ntiles, (const int2 *)bins, ids_scratch, ids_sorted, bm_words, capacity);

@@ -1,4 +1,4 @@
-// Whole-frame render of GSVC's per-frame model, one C call (gfx950).
+// Whole-frame render of GSVC's per-frame model, one C call, two kernels (gfx950).
 //
 // Reference: GaussianSplats_Represent.py:57-90 (parameter activations and
 // forward), i.e. for each frame
@@ -7,71 +7,122 @@
 //     project_gaussians_2d -> rasterize_gaussians_sum -> clamp -> NCHW
 // (foward2d.cu:12-69, utils.py:99-167, forward.cu:512-627).
 //
-// Launches:
+// The rasterizer reads only the first <= 256 entries of each tile in splat-id
+// order (forward.cu:569-571,613), so the frame path needs no global sort and
+// no scan:
 //   frame_project_kernel  activations + projection (project2d.h, the op's own
-//                         op sequence) + per-tile entry counts (atomics), and
-//                         a 48-byte record per splat for the rasterizer;
-//   tile_scan/fill/segsort (binning.hip) -- the scan clears the counters
-//                         for the next frame, so no memset is needed;
-//   raster_sum_fwd_kernel (raster_sum.hip) in the clamped [3,H,W] layout,
-//                         reading the records (no final_idx: no backward).
-// Nothing is read back to the host, and the workspace is reused across
-// frames.
-#include "binning.h"
+//                         op sequence) + a 48-byte record per splat; each
+//                         visible splat appends its id to a fixed 256-slot
+//                         slab per tile it touches (slot = atomic count;
+//                         ids past 256 are dropped) and the block-reduced
+//                         tile count goes into this frame's M;
+//   raster_sum_fwd_kernel sorts each tile's slab in LDS -- or, for a tile
+//                         with more than 256 entries, rebuilds its first 256
+//                         ids by scanning every splat's bbox in id order --
+//                         blends, writes the clamped [3,H,W] planes, and
+//                         clears the tile's count for the next frame.
+// M lives in two device slots used on alternate frames (frame_index & 1): the
+// projection clears the other slot, which the previous frame has finished
+// with.  Nothing is read back to the host.
 #include "project2d.h"
 #include "raster_sum.h"
 
 namespace gsvc {
 
-__global__ __launch_bounds__(256) void frame_project_kernel(
+// Append splat i to the slab of every tile of its bbox; the slot atomics are
+// issued in batches of 8 before their results are waited for.
+__device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, int tby, int i,
+                                           unsigned *__restrict__ counts, int *__restrict__ slab) {
+    unsigned x0, y0, x1, y1;
+    tile_bbox(cx, cy, (float)r, tbx, tby, x0, y0, x1, y1);
+    constexpr int kBatch = 8;
+    unsigned tl[kBatch];
+    int cnt = 0, hits = 0;
+    auto flush = [&]() {
+        unsigned sl[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k)
+            if (k < cnt) sl[k] = atomicAdd(counts + tl[k], 1u);
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k)
+            if (k < cnt && sl[k] < (unsigned)kTilePix) slab[(size_t)tl[k] * kTilePix + sl[k]] = i;
+        hits += cnt;
+        cnt = 0;
+    };
+    for (unsigned y = y0; y < y1; ++y)
+        for (unsigned x = x0; x < x1; ++x) {
+            tl[cnt < kBatch ? cnt : 0] = y * (unsigned)tbx + x;
+            if (++cnt == kBatch) flush();
+        }
+    if (cnt) flush();
+    return hits;
+}
+
+constexpr int kProjThreads = 256;
+__global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
     int n, const float *__restrict__ xyz, int xyz_tanh, const float *__restrict__ chol,
     const float *__restrict__ chol_bound, const float *__restrict__ feat,
     const float *__restrict__ rgb_w, const float *__restrict__ opac, float hw, float hh, int tbx,
     int tby, float2 *__restrict__ xys, int *__restrict__ radii, float4 *__restrict__ rec,
-    unsigned *__restrict__ counts) {
+    unsigned *__restrict__ counts, int *__restrict__ slab, int *__restrict__ m_acc,
+    int *__restrict__ m_clear) {
+    __shared__ int s_hits[kProjThreads / 64];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    float mx = xyz[2 * i], my = xyz[2 * i + 1];
-    if (xyz_tanh) {  // get_xyz (GaussianSplats_Represent.py:57-59)
-        mx = tanhf(mx);
-        my = tanhf(my);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *m_clear = 0;  // the next frame's slot
+    int hits = 0;
+    if (i < n) {
+        float mx = xyz[2 * i], my = xyz[2 * i + 1];
+        if (xyz_tanh) {  // get_xyz (GaussianSplats_Represent.py:57-59)
+            mx = tanhf(mx);
+            my = tanhf(my);
+        }
+        float l11 = chol[3 * i], l21 = chol[3 * i + 1], l22 = chol[3 * i + 2];
+        if (chol_bound) {  // get_cholesky_elements (:69-70)
+            l11 = l11 + chol_bound[0];
+            l21 = l21 + chol_bound[1];
+            l22 = l22 + chol_bound[2];
+        }
+        float r = feat[3 * i], g = feat[3 * i + 1], b = feat[3 * i + 2];
+        if (rgb_w) {  // get_features (:61-63)
+            const float w = rgb_w[i];
+            r = r * w;
+            g = g * w;
+            b = b * w;
+        }
+        const float o = opac ? opac[i] : 1.0f;
+        const SplatProj P = project_splat(mx, my, l11, l21, l22, hw, hh, tbx, tby);
+        xys[i] = P.xy;
+        radii[i] = P.rad;
+        rec[3 * i] = make_float4(P.xy.x, P.xy.y, 0.5f * P.c0, P.c1);
+        rec[3 * i + 1] = make_float4(0.5f * P.c2, o, r, g);
+        rec[3 * i + 2] = make_float4(b, 0.0f, 0.0f, 0.0f);
+        if (P.rad > 0) hits = slab_insert(P.xy.x, P.xy.y, P.rad, tbx, tby, i, counts, slab);
     }
-    float l11 = chol[3 * i], l21 = chol[3 * i + 1], l22 = chol[3 * i + 2];
-    if (chol_bound) {  // get_cholesky_elements (:69-70)
-        l11 = l11 + chol_bound[0];
-        l21 = l21 + chol_bound[1];
-        l22 = l22 + chol_bound[2];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) hits += __shfl_xor(hits, off, 64);
+    if ((threadIdx.x & 63) == 0) s_hits[threadIdx.x >> 6] = hits;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+#pragma unroll
+        for (int k = 0; k < kProjThreads / 64; ++k) t += s_hits[k];
+        if (t) atomicAdd(m_acc, t);
     }
-    float r = feat[3 * i], g = feat[3 * i + 1], b = feat[3 * i + 2];
-    if (rgb_w) {  // get_features (:61-63)
-        const float w = rgb_w[i];
-        r = r * w;
-        g = g * w;
-        b = b * w;
-    }
-    const float o = opac ? opac[i] : 1.0f;
-    const SplatProj P = project_splat(mx, my, l11, l21, l22, hw, hh, tbx, tby);
-    xys[i] = P.xy;
-    radii[i] = P.rad;
-    rec[3 * i] = make_float4(P.xy.x, P.xy.y, 0.5f * P.c0, P.c1);
-    rec[3 * i + 1] = make_float4(0.5f * P.c2, o, r, g);
-    rec[3 * i + 2] = make_float4(b, 0.0f, 0.0f, 0.0f);
-    if (P.rad > 0) count_splat_tiles(P.xy.x, P.xy.y, P.rad, tbx, tby, counts);
 }
 
 static inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct FrameWs {
-    unsigned *counts, *cursor;
-    int2 *bins;
+    unsigned *counts;
+    int *m_slots;
+    int *slab;
     float2 *xys;
     int *radii;
     float4 *rec;
-    int *ids_scratch, *ids_sorted;
-    size_t bytes;
+    size_t zeroed, bytes;
 };
 
-static FrameWs frame_ws(char *base, int n, int ntiles, long long capacity) {
+static FrameWs frame_ws(char *base, int n, int ntiles) {
     FrameWs w;
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -80,17 +131,21 @@ static FrameWs frame_ws(char *base, int n, int ntiles, long long capacity) {
         return p;
     };
     const size_t nn = (size_t)(n > 0 ? n : 1), nt = (size_t)(ntiles > 0 ? ntiles : 1);
-    const size_t cap = (size_t)(capacity > 0 ? capacity : 1);
-    w.counts = (unsigned *)take(sizeof(unsigned) * nt);  // first: zeroed by the caller once
-    w.cursor = (unsigned *)take(sizeof(unsigned) * nt);
-    w.bins = (int2 *)take(sizeof(int2) * nt);
+    // first: counts[T] and the two M slots, zeroed by the caller once; every
+    // call leaves them zero (the rasterizer clears each tile's count)
+    w.counts = (unsigned *)take(sizeof(unsigned) * nt + 2 * sizeof(int));
+    w.m_slots = (int *)(w.counts + nt);
+    w.zeroed = sizeof(unsigned) * nt + 2 * sizeof(int);
+    w.slab = (int *)take(sizeof(int) * kTilePix * nt);
     w.xys = (float2 *)take(sizeof(float2) * nn);
     w.radii = (int *)take(sizeof(int) * nn);
     w.rec = (float4 *)take(sizeof(float4) * 3 * nn);
-    w.ids_scratch = (int *)take(sizeof(int) * cap);
-    w.ids_sorted = (int *)take(sizeof(int) * cap);
     w.bytes = off;
     return w;
+}
+
+static int tiles_of(unsigned h, unsigned w) {
+    return ceil_div((int)w, kTile) * ceil_div((int)h, kTile);
 }
 
 }  // namespace gsvc
@@ -98,41 +153,42 @@ static FrameWs frame_ws(char *base, int n, int ntiles, long long capacity) {
 using namespace gsvc;
 
 extern "C" size_t gsvc_render_frame_workspace_bytes(int num_points, unsigned img_height,
-                                                    unsigned img_width, long long capacity) {
-    const int ntiles = ceil_div((int)img_width, kTile) * ceil_div((int)img_height, kTile);
-    return frame_ws(nullptr, num_points, ntiles, capacity).bytes;
+                                                    unsigned img_width) {
+    return frame_ws(nullptr, num_points, tiles_of(img_height, img_width)).bytes;
 }
 
 extern "C" size_t gsvc_render_frame_zeroed_bytes(unsigned img_height, unsigned img_width) {
-    const int ntiles = ceil_div((int)img_width, kTile) * ceil_div((int)img_height, kTile);
-    return sizeof(unsigned) * (size_t)ntiles;
+    return frame_ws(nullptr, 1, tiles_of(img_height, img_width)).zeroed;
 }
 
 extern "C" int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_tanh,
                                      const float *cholesky, const float *cholesky_bound,
                                      const float *features, const float *rgb_w,
                                      const float *opacity, const float *background,
-                                     unsigned img_height, unsigned img_width, long long capacity,
+                                     unsigned img_height, unsigned img_width, int frame_index,
                                      int density_hint, int *meta, void *workspace,
                                      size_t workspace_bytes, float *out, void *stream) {
-    if (num_points < 0 || capacity < 0 || img_height == 0 || img_width == 0)
+    if (num_points < 0 || img_height == 0 || img_width == 0)
         return set_error(GSVC_ERR_ARG, "render_frame_sum: bad sizes");
     if (!xyz || !cholesky || !features || !background || !meta || !out)
         return set_error(GSVC_ERR_ARG, "render_frame_sum: missing input");
     const int tbx = ceil_div((int)img_width, kTile), tby = ceil_div((int)img_height, kTile);
     const int ntiles = tbx * tby;
-    const FrameWs w = frame_ws((char *)workspace, num_points, ntiles, capacity);
+    const FrameWs w = frame_ws((char *)workspace, num_points, ntiles);
     if (!workspace || workspace_bytes < w.bytes)
         return set_error(GSVC_ERR_WORKSPACE, "render_frame_sum: workspace too small (%zu < %zu)",
                          workspace_bytes, w.bytes);
     hipStream_t s = (hipStream_t)stream;
     const float hw = 0.5f * (float)img_width, hh = 0.5f * (float)img_height;
+    int *m_acc = w.m_slots + (frame_index & 1), *m_clear = w.m_slots + ((frame_index + 1) & 1);
     if (num_points > 0)
-        hipLaunchKernelGGL(frame_project_kernel, dim3(ceil_div(num_points, 256)), dim3(256), 0, s,
-                           num_points, xyz, xyz_tanh, cholesky, cholesky_bound, features, rgb_w,
-                           opacity, hw, hh, tbx, tby, w.xys, w.radii, w.rec, w.counts);
-    int rc = tile_bins_from_counts(num_points, w.xys, w.radii, tbx, tby, capacity, w.counts, w.cursor,
-                                   w.ids_scratch, w.ids_sorted, w.bins, meta, true, s);
+        hipLaunchKernelGGL(frame_project_kernel, dim3(ceil_div(num_points, kProjThreads)),
+                           dim3(kProjThreads), 0, s, num_points, xyz, xyz_tanh, cholesky,
+                           cholesky_bound, features, rgb_w, opacity, hw, hh, tbx, tby, w.xys, w.radii,
+                           w.rec, w.counts, w.slab, m_acc, m_clear);
+    else if (hipMemsetAsync(m_acc, 0, sizeof(int), s) != hipSuccess)
+        return set_error(GSVC_ERR_HIP, "render_frame_sum: memset failed");
+    int rc = check_launch("render_frame_sum: projection");
     if (rc) return rc;
     SumFwdArgs A;
     sum_fwd_args_init(A);
@@ -141,10 +197,15 @@ extern "C" int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_t
     A.img_h = (int)img_height;
     A.ntiles = ntiles;
     A.layout = kLayoutCHWClamped;
-    A.m_dev = meta;
+    A.m_dev = m_acc;
+    A.meta_out = meta;
     A.bg = background;
-    A.ids = w.ids_sorted;
-    A.bins = w.bins;
+    A.sort_ids = true;
+    A.slab = w.slab;
+    A.slab_counts = w.counts;
+    A.cull_xys = w.xys;
+    A.cull_radii = w.radii;
+    A.num_points = num_points;
     A.rec = w.rec;
     A.out = out;
     return sum_forward_launch(A, density_hint, s);

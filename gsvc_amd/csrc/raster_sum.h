@@ -24,6 +24,16 @@ struct SumFwdArgs {
     // frame path: per-splat records {x, y, a/2, b}, {c/2, opacity, r, g},
     // {b, -, -, -} replace the four arrays above (same values)
     const float4 *rec;
+    bool sort_ids;  // ids of a tile arrive unsorted; the kernel sorts them in LDS
+    // frame path: per-tile 256-slot slabs with their counts (cleared here for
+    // the next frame); tiles with more than 256 entries are rebuilt from the
+    // splats' bboxes (cull_xys, cull_radii, num_points)
+    const int *slab;
+    unsigned *slab_counts;
+    const float2 *cull_xys;
+    const int *cull_radii;
+    int num_points;
+    int *meta_out;  // frame path: meta[0] <- M (from m_dev), meta[1] <- 0
     float *out;
     int *final_idx;
     float *final_Ts;

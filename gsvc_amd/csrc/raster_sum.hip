@@ -133,10 +133,111 @@ __device__ __forceinline__ void store_pixel(const SumFwdArgs &A, size_t p, float
     if (A.final_Ts) A.final_Ts[p] = 1.0f;
 }
 
+// The tile's splat ids in ascending order -- the first min(n_all, 256) of
+// them -- into s_ids (LDS): the segment sort of binning.hip done by the wave
+// that blends the tile, when the ids arrive in fill order (frame path).  At
+// most 64 entries: ranks by broadcast compares; more: an LDS bitmap over the
+// id range in windows of 16384 ids, emitted in order until 256 are found.
+// ``bm`` is 512 words of this wave's LDS (free until blending starts).  Ids
+// are unique within a tile, so this is the stable sort's order.
+constexpr int kSortWords = 512;
+__device__ int wave_sorted_tile_ids(const int *__restrict__ ids, int n_all, int *s_ids,
+                                    unsigned *bm) {
+    const int lane = threadIdx.x & 63;
+    if (n_all <= 0) return 0;
+    if (n_all <= 64) {
+        const int v = lane < n_all ? ids[lane] : 0x7fffffff;
+        int rank = 0;
+        for (int k = 0; k < n_all; ++k) rank += (__shfl(v, k, 64) < v) ? 1 : 0;
+        if (lane < n_all) s_ids[rank] = v;
+        wave_lds_sync();
+        return n_all;
+    }
+    int lo = 0x7fffffff, hi = -1;
+    for (int j = lane; j < n_all; j += 64) {
+        const int v = ids[j];
+        lo = min(lo, v);
+        hi = max(hi, v);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = min(lo, __shfl_xor(lo, off, 64));
+        hi = max(hi, __shfl_xor(hi, off, 64));
+    }
+    int written = 0;
+    for (long long base = lo; base <= hi && written < kTilePix; base += 32 * kSortWords) {
+        for (int w = lane; w < kSortWords; w += 64) bm[w] = 0u;
+        wave_lds_sync();
+        for (int j = lane; j < n_all; j += 64) {
+            const long long d = (long long)ids[j] - base;
+            if (d >= 0 && d < 32 * kSortWords) atomicOr(bm + (d >> 5), 1u << (d & 31));
+        }
+        wave_lds_sync();
+        constexpr int kPer = kSortWords / 64;  // words per lane, in order
+        unsigned wv[kPer];
+        int cnt = 0;
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            wv[q] = bm[kPer * lane + q];
+            cnt += __popc(wv[q]);
+        }
+        int incl = cnt;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int u = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += u;
+        }
+        int pos = written + incl - cnt;
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            unsigned bits = wv[q];
+            while (bits && pos < kTilePix) {
+                s_ids[pos++] = (int)(base + 32 * (kPer * lane + q) + (__ffs(bits) - 1));
+                bits &= bits - 1u;
+            }
+        }
+        written += __shfl(incl, 63, 64);
+        wave_lds_sync();
+    }
+    return min(written, kTilePix);
+}
+
+// A tile with more than 256 entries on the frame path (its slab kept an
+// arbitrary 256): its first 256 ids are rebuilt by testing every splat's tile
+// bbox (the binning's own tile_bbox of xys and radii) in id order, 64 at a
+// time, compacting the hits by ballot -- sorted by construction.
+__device__ int wave_brute_tile_ids(const SumFwdArgs &A, int tile, int *s_ids) {
+    const int lane = threadIdx.x & 63;
+    const unsigned ty = (unsigned)(tile / A.tbx), tx = (unsigned)(tile - (int)ty * A.tbx);
+    const int tby = (A.img_h + kTile - 1) / kTile;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int written = 0;
+    for (int base = 0; base < A.num_points && written < kTilePix; base += 64) {
+        const int j = base + lane;
+        bool hit = false;
+        if (j < A.num_points) {
+            const int r = A.cull_radii[j];
+            if (r > 0) {
+                const float2 c = A.cull_xys[j];
+                unsigned x0, y0, x1, y1;
+                tile_bbox(c.x, c.y, (float)r, A.tbx, tby, x0, y0, x1, y1);
+                hit = tx >= x0 && tx < x1 && ty >= y0 && ty < y1;
+            }
+        }
+        const unsigned long long m = __ballot(hit);
+        const int pos = written + __popcll(m & lt);
+        if (hit && pos < kTilePix) s_ids[pos] = j;
+        written += __popcll(m);
+    }
+    wave_lds_sync();
+    return min(written, kTilePix);
+}
+
 // Sparse path: one wave blends the whole 16x16 tile, 4 pixels per lane.
 template <int kMode>
 __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, int2 range, int n,
-                                               float4 *s_slice, float3 init) {
+                                               float4 *s_slice, float3 init, bool ids_in_lds,
+                                               const int *s_ids) {
     float4 *s_geo = s_slice;                           // x, y, 0.5a, b
     float4 *s_col = s_slice + kChunk;                  // 0.5c, opacity, r, g
     float *s_blu = (float *)(s_slice + 2 * kChunk);    // b
@@ -154,7 +255,8 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         if (lane < cnt) {
             float4 geo, col;
             float blu;
-            load_splat(A, A.ids[range.x + base + lane], geo, col, blu);
+            const int j = base + lane;
+            load_splat(A, ids_in_lds ? s_ids[j] : A.ids[range.x + j], geo, col, blu);
             s_geo[lane] = geo;
             s_col[lane] = col;
             s_blu[lane] = blu;
@@ -238,7 +340,8 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
 // Dense path: this wave blends one 8-row band, 2 pixels per lane.
 template <int kMode>
 __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int band, int2 range,
-                                             int n, float4 *s_slice, float3 init) {
+                                             int n, float4 *s_slice, float3 init, bool ids_in_lds,
+                                             const int *s_ids) {
     float4 *s_geo = s_slice;                                      // x, y, 0.5a, b
     float4 *s_col = s_slice + kChunk;                             // 0.5c, opacity, r, g
     float *s_blu = reinterpret_cast<float *>(s_slice + 2 * kChunk);
@@ -261,7 +364,7 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
         float4 geo = make_float4(0.f, 0.f, 0.f, 0.f), col = geo;
         float blu = 0.f;
         if (j < n) {
-            load_splat(A, A.ids[range.x + j], geo, col, blu);
+            load_splat(A, ids_in_lds ? s_ids[j] : A.ids[range.x + j], geo, col, blu);
             // 2 * (a/2) == a except for subnormal a, where culling is off anyway
             keep = ellipse_hits_rect(geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, bx0,
                                      bx0 + 15.0f, by0, by0 + 7.0f);
@@ -362,17 +465,39 @@ template <int kMode>
 __global__ __launch_bounds__(kMode == kModeSparse ? 64 : 128, 8) void raster_sum_fwd_kernel(
     SumFwdArgs A) {
     __shared__ float4 s_buf[kMode == kModeSparse ? 1 : 2][kSlice];
+    __shared__ int s_ids[kMode == kModeSparse ? 1 : 2][kTilePix];
     const int w = (kMode == kModeSparse) ? 0 : (threadIdx.x >> 6);
     const int tile = xcd_remap(blockIdx.x, A.ntiles);
     long long t0 = 0;
     if (kMode == kModeStamp) t0 = stamp();
-    const int2 range = A.bins[tile];
-    int n = range.y - range.x;
-    n = n > kTilePix ? kTilePix : (n < 0 ? 0 : n);
+    int2 range;
+    const int *seg;  // the tile's ids (unsorted when A.sort_ids)
+    int n_all;
+    if (A.slab) {
+        __shared__ int s_cnt;
+        if (threadIdx.x == 0) {
+            s_cnt = (int)A.slab_counts[tile];
+            A.slab_counts[tile] = 0u;  // for the next frame
+            if (tile == 0) {
+                A.meta_out[0] = *A.m_dev;
+                A.meta_out[1] = 0;
+            }
+        }
+        __syncthreads();
+        n_all = s_cnt;
+        range = make_int2(0, n_all);
+        seg = A.slab + (size_t)tile * kTilePix;
+    } else {
+        range = A.bins[tile];
+        n_all = range.y - range.x;
+        n_all = n_all < 0 ? 0 : n_all;
+        seg = A.ids + range.x;
+    }
+    int n = n_all > kTilePix ? kTilePix : n_all;
     // rasterize_sum.py:121-127: a frame without intersections is the background
     float3 init = make_float3(0.f, 0.f, 0.f);
     if (A.m_dev && *A.m_dev < 1) {
-        n = 0;
+        n = n_all = 0;
         init = make_float3(A.bg[0], A.bg[1], A.bg[2]);
     }
     const int ty = tile / A.tbx;
@@ -380,10 +505,18 @@ __global__ __launch_bounds__(kMode == kModeSparse ? 64 : 128, 8) void raster_sum
                         ((kMode == kModeAdaptive || kMode == kModeStamp) && n <= A.sparse_max);
     if (sparse) {
         if (w != 0) return;
-        sum_fwd_sparse<kMode>(A, tile, range, n, s_buf[0], init);
+        if (A.sort_ids)
+            n = (A.slab && n_all > kTilePix)
+                    ? wave_brute_tile_ids(A, tile, s_ids[0])
+                    : wave_sorted_tile_ids(seg, n_all, s_ids[0], reinterpret_cast<unsigned *>(s_buf[0]));
+        sum_fwd_sparse<kMode>(A, tile, range, n, s_buf[0], init, A.sort_ids, s_ids[0]);
     } else {
         if (ty * kTile + w * 8 >= A.img_h) return;  // band below the image
-        sum_fwd_band<kMode>(A, tile, w, range, n, s_buf[w], init);
+        if (A.sort_ids)
+            n = (A.slab && n_all > kTilePix)
+                    ? wave_brute_tile_ids(A, tile, s_ids[w])
+                    : wave_sorted_tile_ids(seg, n_all, s_ids[w], reinterpret_cast<unsigned *>(s_buf[w]));
+        sum_fwd_band<kMode>(A, tile, w, range, n, s_buf[w], init, A.sort_ids, s_ids[w]);
     }
     if (kMode == kModeStamp && (threadIdx.x & 63) == 0) {
         long long *st = A.stamps + 4 * (size_t)tile;

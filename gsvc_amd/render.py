@@ -8,14 +8,13 @@
     img = rasterize_gaussians_sum(xys, depths, radii, conics, nth, colors, ones, H, W)
     img = torch.clamp(img, 0, 1).view(-1, H, W, 3).permute(0, 3, 1, 2).contiguous()
 
--- in ONE C call (gsvc_render_frame_sum, csrc/frame.hip) with no host
-synchronisation: a fused activation + projection + tile-count kernel, the
-sync-free tile binning (scan / fill / per-tile segment sort), and the sum
-rasterizer writing clamp(img) straight into the [1, 3, H, W] planes (final_idx
-is not written: no backward follows).  The workspace (intermediates and the
-intersection buffers, capacity N * tiles) is cached per device and stream and
-reused across frames.  Results are bit-identical to the autograd path
-(tests/test_gpu_sync_free.py).
+-- in ONE C call (gsvc_render_frame_sum, csrc/frame.hip), two kernels, no host
+synchronisation: activations + projection + per-tile 256-slot slabs of splat
+ids, then the sum rasterizer sorting each tile's slab in LDS and writing
+clamp(img) straight into the [1, 3, H, W] planes (final_idx is not written: no
+backward follows).  The workspace (slabs, per-splat records; ~1 KB per tile +
+64 B per splat) is cached per device and stream and reused across frames.
+Results are bit-identical to the autograd path (tests/test_gpu_sync_free.py).
 
 ``render_sum_frame`` is the same for already-activated inputs (means2d, L,
 colors, opacity), the signature of the two reference ops it replaces.
@@ -28,8 +27,7 @@ import torch
 from torch import Tensor
 
 from . import _lib as L
-from . import ops as _C
-from .utils import BIN_CAPACITY_BUDGET, _LazyCount, bin_for_raster
+from .utils import _LazyCount
 
 
 class _FrameWorkspace:
@@ -38,25 +36,27 @@ class _FrameWorkspace:
         self.hw = None
         self.dirty = True
         self.meta = None
+        self.frame = 0
         self.hint = _LazyCount()
 
 
 _workspaces = {}
 
 
-def _workspace(dev: torch.device, n: int, H: int, W: int, cap: int) -> _FrameWorkspace:
+def _workspace(dev: torch.device, n: int, H: int, W: int) -> _FrameWorkspace:
     key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
     fw = _workspaces.get(key)
     if fw is None:
         fw = _workspaces[key] = _FrameWorkspace()
         fw.meta = torch.zeros((2,), dtype=torch.int32, device=dev)
-    need = L.size("gsvc_render_frame_workspace_bytes", n, H, W, cap)
+    need = L.size("gsvc_render_frame_workspace_bytes", n, H, W)
     if fw.buf is None or fw.buf.numel() < need:
         fw.buf = torch.empty((need,), dtype=torch.uint8, device=dev)
         fw.dirty = True
     if fw.dirty or fw.hw != (H, W):
         # the per-tile counters start at zero; every call leaves them zero
         fw.buf[: L.size("gsvc_render_frame_zeroed_bytes", H, W)].zero_()
+        fw.frame = 0
         fw.hw = (H, W)
         fw.dirty = False
     return fw
@@ -82,17 +82,6 @@ def render_frame_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, img_height
     H, W = int(img_height), int(img_width)
     n = xyz.shape[0]
     dev = xyz.device
-    ntiles = ((W + 15) // 16) * ((H + 15) // 16)
-    cap = n * ntiles
-    if cap > BIN_CAPACITY_BUDGET:
-        # intersection buffers too large to reserve: sized (host-synchronised) path
-        with torch.no_grad():
-            means2d = torch.tanh(xyz) if xyz_tanh else xyz
-            Lc = cholesky + cholesky_bound if cholesky_bound is not None else cholesky
-            colors = features * rgb_w if rgb_w is not None else features
-            opac = opacity if opacity is not None else torch.ones(n, 1, device=dev)
-            return _render_sum_frame_ops(means2d, Lc, colors, opac, H, W,
-                                         ((W + 15) // 16, (H + 15) // 16, 1), background)
     xyz_c = _f32c(xyz, "xyz")
     chol_c = _f32c(cholesky, "cholesky")
     feat_c = _f32c(features, "features")
@@ -107,16 +96,18 @@ def render_frame_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, img_height
     for t, nm in ((rgbw_c, "rgb_w"), (opac_c, "opacity")):
         if t is not None and t.numel() != n:
             raise ValueError(f"{nm} needs N elements")
-    fw = _workspace(dev, n, H, W, cap)
+    fw = _workspace(dev, n, H, W)
     out = torch.empty((1, 3, H, W), dtype=torch.float32, device=dev)
     hint = fw.hint.value
     try:
         L.call("gsvc_render_frame_sum", n, L.ptr(xyz_c), 1 if xyz_tanh else 0, L.ptr(chol_c),
-               L.ptr(bound_c), L.ptr(feat_c), L.ptr(rgbw_c), L.ptr(opac_c), L.ptr(bg_c), H, W, cap,
-               hint, L.ptr(fw.meta), L.ptr(fw.buf), fw.buf.numel(), L.ptr(out), L.stream(dev))
+               L.ptr(bound_c), L.ptr(feat_c), L.ptr(rgbw_c), L.ptr(opac_c), L.ptr(bg_c), H, W,
+               fw.frame, hint, L.ptr(fw.meta), L.ptr(fw.buf), fw.buf.numel(), L.ptr(out),
+               L.stream(dev))
     except Exception:
         fw.dirty = True
         raise
+    fw.frame += 1
     fw.hint.update(fw.meta)
     return out
 
@@ -139,22 +130,3 @@ def render_sum_frame(means2d: Tensor, L_elements: Tensor, colors: Tensor, opacit
         background = torch.ones(3, dtype=torch.float32, device=colors.device)
     return render_frame_sum(means2d, L_elements, colors, img_height, img_width, background,
                             xyz_tanh=False, opacity=opacity)
-
-
-def _render_sum_frame_ops(means2d, L_elements, colors, opacity, H, W, tile_bounds, background,
-                          clip_thresh=0.01):
-    """The same render composed from the ops (used above the capacity budget)."""
-    n = means2d.shape[-2]
-    with torch.no_grad():
-        xys, depths, radii, conics, nth = _C.project_gaussians_2d_forward(
-            n, means2d.contiguous(), L_elements.contiguous(), H, W, tile_bounds, clip_thresh)
-        binned = bin_for_raster(n, xys, depths, radii, nth, tile_bounds)
-        if binned.num_intersects is not None and binned.num_intersects < 1:
-            img = torch.clamp(background.view(3, 1, 1).expand(3, H, W), 0, 1)
-            return img.reshape(1, 3, H, W).contiguous()
-        img, _ = _C.rasterize_sum_forward_ex(
-            tile_bounds, (16, 16, 1), (W, H, 1), binned.gaussian_ids_sorted, binned.tile_bins, xys,
-            conics, colors.contiguous(), opacity.contiguous(), background.contiguous(),
-            num_intersects_dev=binned.m_dev, density_hint=binned.density_hint,
-            layout=_C.LAYOUT_CHW_CLAMPED, want_idx=False)
-    return img.view(1, 3, H, W)

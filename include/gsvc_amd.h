@@ -204,26 +204,27 @@ int gsvc_rasterize_sum_forward_ex(
 
 /* ---------------------------------------------------------------------------
  * Whole-frame render of GSVC's per-frame model (GaussianSplats_Represent.py:
- * 57-90) in one call, no host synchronisation: out[3,H,W] =
+ * 57-90) in one call (two kernels), no host synchronisation: out[3,H,W] =
  * clamp(rasterize_gaussians_sum(project_gaussians_2d(means2d, L)), 0, 1)
  * permuted to planes, with
  *   means2d = xyz_tanh ? tanh(xyz) : xyz            xyz [N,2]
  *   L       = cholesky + cholesky_bound (if given)   cholesky [N,3], bound [3]
  *   colors  = features * rgb_w (if given)            features [N,3], rgb_w [N]
  *   opacity = opacity (if given) else 1              [N]
- * Results are bit-identical to the op path.  meta (device int[2]) <- {M,
- * M > capacity}; capacity = N * tiles never overflows.  The workspace
- * (gsvc_render_frame_workspace_bytes) must have its first
- * gsvc_render_frame_zeroed_bytes zero before the first call; every call
- * leaves them zero.  density_hint as in gsvc_rasterize_sum_forward_ex. */
+ * Results are bit-identical to the op path.  meta (device int[2]) <- {M, 0}.
+ * The workspace (gsvc_render_frame_workspace_bytes) must have its first
+ * gsvc_render_frame_zeroed_bytes zero before the first call; every call leaves
+ * them zero.  frame_index: any integer that alternates parity between
+ * consecutive calls on one workspace (a frame counter).  density_hint as in
+ * gsvc_rasterize_sum_forward_ex. */
 size_t gsvc_render_frame_workspace_bytes(int num_points, unsigned img_height,
-                                         unsigned img_width, long long capacity);
+                                         unsigned img_width);
 size_t gsvc_render_frame_zeroed_bytes(unsigned img_height, unsigned img_width);
 int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_tanh,
                           const float *cholesky, const float *cholesky_bound,
                           const float *features, const float *rgb_w,
                           const float *opacity, const float *background,
-                          unsigned img_height, unsigned img_width, long long capacity,
+                          unsigned img_height, unsigned img_width, int frame_index,
                           int density_hint, int *meta, void *workspace,
                           size_t workspace_bytes, float *out, void *stream);
 

@@ -256,6 +256,27 @@ def test_tanh_matches_torch(cuda):
     assert out.shape == (1, 3, 16, 16)
     from gsvc_amd.render import _workspaces
     fw = _workspaces[(0, torch.cuda.current_stream().cuda_stream)]
-    off = 3 * 256  # counts, cursor, bins slots (each 256-byte aligned)
+    off = 256 + 1024  # counts + M slots (256-aligned), one tile's 256-slot slab
     xys = fw.buf[off: off + 8 * n].view(torch.float32).view(n, 2)
     assert torch.equal(xys, ref)
+
+
+@pytest.mark.parametrize("n,count", [(4000, 64), (4000, 65), (4000, 300), (150000, 150),
+                                     (150000, 600)])
+def test_render_frame_in_kernel_sort(cuda, oracle, n, count):
+    """The frame path leaves each tile's ids in fill order and the rasterizer
+    sorts them (shuffle ranks <= 64 entries, LDS bitmap in 16384-id windows
+    above, stopping at 256): clustered tiles with ids spread over 150k splats
+    against the op path (sorted by the separate segment sort)."""
+    from gsvc_amd.render import render_sum_frame
+    ids = np.unique(np.random.default_rng(count).choice(n, count, replace=False))
+    means, L, colors, opac, H, W = _clustered_frame(n, ids)
+    bg = torch.ones(3, device="cuda")
+    fast = render_sum_frame(T(means), T(L), T(colors), T(opac), H, W, _tb(H, W), bg)
+    with torch.no_grad():
+        ref = _op_path_frame(T(means), T(L), T(colors), T(opac), H, W, bg)
+    assert torch.equal(fast, ref)
+    # and against the oracle image (clamped, planar)
+    o = oracle.render_sum(means, L, colors, opac, H, W)["out"]
+    np.testing.assert_allclose(N(fast)[0], np.clip(o, 0, 1).transpose(2, 0, 1), rtol=1e-6,
+                               atol=1e-5)
