@@ -31,11 +31,14 @@ from .utils import _LazyCount
 
 
 class _FrameWorkspace:
-    def __init__(self):
+    def __init__(self, stream_handle):
+        self.stream = stream_handle
         self.buf = None
+        self.buf_ptr = 0
         self.hw = None
         self.dirty = True
         self.meta = None
+        self.meta_ptr = 0
         self.frame = 0
         self.hint = _LazyCount()
 
@@ -44,14 +47,17 @@ _workspaces = {}
 
 
 def _workspace(dev: torch.device, n: int, H: int, W: int) -> _FrameWorkspace:
-    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    stream_handle = torch.cuda.current_stream(dev).cuda_stream
+    key = (dev.index, stream_handle)
     fw = _workspaces.get(key)
     if fw is None:
-        fw = _workspaces[key] = _FrameWorkspace()
+        fw = _workspaces[key] = _FrameWorkspace(stream_handle)
         fw.meta = torch.zeros((2,), dtype=torch.int32, device=dev)
+        fw.meta_ptr = fw.meta.data_ptr()
     need = L.size("gsvc_render_frame_workspace_bytes", n, H, W)
     if fw.buf is None or fw.buf.numel() < need:
         fw.buf = torch.empty((need,), dtype=torch.uint8, device=dev)
+        fw.buf_ptr = fw.buf.data_ptr()
         fw.dirty = True
     if fw.dirty or fw.hw != (H, W):
         # the per-tile counters start at zero; every call leaves them zero
@@ -62,12 +68,19 @@ def _workspace(dev: torch.device, n: int, H: int, W: int) -> _FrameWorkspace:
     return fw
 
 
-def _f32c(t: Optional[Tensor], name: str) -> Optional[Tensor]:
+def _ptr_f32(t: Optional[Tensor], name: str, numel: int, keep: list) -> int:
+    """Device address of t as contiguous float32 (a converted copy is kept
+    alive in ``keep`` until the launch is enqueued)."""
     if t is None:
-        return None
+        return 0
     if not t.is_cuda:
         raise RuntimeError(f"{name} must be a CUDA tensor")
-    return t.detach().to(torch.float32).contiguous()
+    if t.dtype is not torch.float32 or not t.is_contiguous():
+        t = t.detach().to(torch.float32).contiguous()
+        keep.append(t)
+    if t.numel() != numel:
+        raise ValueError(f"{name} must have {numel} elements, got {t.numel()}")
+    return t.data_ptr()
 
 
 def render_frame_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, img_height: int,
@@ -82,31 +95,24 @@ def render_frame_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, img_height
     H, W = int(img_height), int(img_width)
     n = xyz.shape[0]
     dev = xyz.device
-    xyz_c = _f32c(xyz, "xyz")
-    chol_c = _f32c(cholesky, "cholesky")
-    feat_c = _f32c(features, "features")
-    bound_c = _f32c(cholesky_bound, "cholesky_bound")
-    rgbw_c = _f32c(rgb_w, "rgb_w")
-    opac_c = _f32c(opacity, "opacity")
-    bg_c = _f32c(background, "background")
-    if xyz_c.shape != (n, 2) or chol_c.shape != (n, 3) or feat_c.shape != (n, 3):
-        raise ValueError("xyz [N,2], cholesky [N,3] and features [N,3] expected")
-    if bg_c.numel() != 3 or (bound_c is not None and bound_c.numel() != 3):
-        raise ValueError("background and cholesky_bound need 3 elements")
-    for t, nm in ((rgbw_c, "rgb_w"), (opac_c, "opacity")):
-        if t is not None and t.numel() != n:
-            raise ValueError(f"{nm} needs N elements")
+    keep = []
+    p_xyz = _ptr_f32(xyz, "xyz", 2 * n, keep)
+    p_chol = _ptr_f32(cholesky, "cholesky", 3 * n, keep)
+    p_feat = _ptr_f32(features, "features", 3 * n, keep)
+    p_bound = _ptr_f32(cholesky_bound, "cholesky_bound", 3, keep)
+    p_rgbw = _ptr_f32(rgb_w, "rgb_w", n, keep)
+    p_opac = _ptr_f32(opacity, "opacity", n, keep)
+    p_bg = _ptr_f32(background, "background", 3, keep)
     fw = _workspace(dev, n, H, W)
     out = torch.empty((1, 3, H, W), dtype=torch.float32, device=dev)
-    hint = fw.hint.value
-    try:
-        L.call("gsvc_render_frame_sum", n, L.ptr(xyz_c), 1 if xyz_tanh else 0, L.ptr(chol_c),
-               L.ptr(bound_c), L.ptr(feat_c), L.ptr(rgbw_c), L.ptr(opac_c), L.ptr(bg_c), H, W,
-               fw.frame, hint, L.ptr(fw.meta), L.ptr(fw.buf), fw.buf.numel(), L.ptr(out),
-               L.stream(dev))
-    except Exception:
+    rc = L.load().gsvc_render_frame_sum(
+        n, p_xyz, 1 if xyz_tanh else 0, p_chol, p_bound, p_feat, p_rgbw, p_opac, p_bg, H, W,
+        fw.frame, fw.hint.value, fw.meta_ptr, fw.buf_ptr, fw.buf.numel(), out.data_ptr(),
+        fw.stream)
+    if rc != 0:
         fw.dirty = True
-        raise
+        msg = L.load().gsvc_last_error().decode(errors="replace")
+        raise RuntimeError(f"gsvc_render_frame_sum failed (status {rc}): {msg}")
     fw.frame += 1
     fw.hint.update(fw.meta)
     return out

@@ -45,16 +45,18 @@ class _LazyCount:
         self.event = None
 
     def update(self, m_dev: Tensor) -> int:
+        self.calls += 1
+        if self.calls % self.period != 1 and self.period != 1:
+            return self.value
         if self.event is not None and self.event.query():
             self.value = int(self.buf[0])
             self.event = None
-        if self.event is None and self.calls % self.period == 0:
+        if self.event is None:
             if self.buf is None:
                 self.buf = torch.empty((1,), dtype=torch.int32, pin_memory=True)
             self.buf.copy_(m_dev[:1], non_blocking=True)
             self.event = torch.cuda.Event()
             self.event.record()
-        self.calls += 1
         return self.value
 
 
