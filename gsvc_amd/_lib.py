@@ -29,6 +29,7 @@ _SIGS = {
     "gsvc_abi_version": [],
     "gsvc_last_error": [],
     "gsvc_debug_set": [_I, _I],
+    "gsvc_debug_set_ptr": [_P],
     "gsvc_timing_enable": [_I, _I],
     "gsvc_timing_collect": [_P, _I, _P],
     "gsvc_project_gaussians_2d_forward": [_I, _P, _P, _U, _U, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P],
@@ -60,6 +61,7 @@ _SIGS = {
                                 _P, _P],
 }
 _RESTYPE = {
+    "gsvc_debug_set_ptr": None,
     "gsvc_last_error": ctypes.c_char_p,
     "gsvc_cumsum_workspace_bytes": _SZ,
     "gsvc_sort_pairs_workspace_bytes": _SZ,

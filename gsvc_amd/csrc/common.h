@@ -22,6 +22,7 @@ constexpr float kAlphaMin = 1.0f / 255.0f;
 int set_error(int code, const char *fmt, ...);
 int check_launch(const char *what);
 extern int g_knobs[8];  // gsvc_debug_set(); knob 0 = sum-forward variant
+extern void *g_debug_ptr;  // gsvc_debug_set_ptr(): diagnostic output buffer
 int timing_begin(hipStream_t s);  // timing.hip: -1 when not recording
 void timing_end(hipStream_t s, int slot);
 

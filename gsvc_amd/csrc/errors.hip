@@ -23,6 +23,7 @@ int check_launch(const char *what) {
 }
 
 int g_knobs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+void *g_debug_ptr = nullptr;
 
 }  // namespace gsvc
 
@@ -34,5 +35,7 @@ extern "C" int gsvc_debug_set(int key, int value) {
     gsvc::g_knobs[key] = value;
     return old;
 }
+
+extern "C" void gsvc_debug_set_ptr(void *p) { gsvc::g_debug_ptr = p; }
 
 extern "C" const char *gsvc_last_error(void) { return gsvc::g_last_error; }

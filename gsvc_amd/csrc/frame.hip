@@ -11,28 +11,31 @@
 // order (forward.cu:569-571,613), so the frame path needs no global sort and
 // no scan:
 //   frame_project_kernel  activations + projection (project2d.h, the op's own
-//                         op sequence) + a 48-byte record per splat; each
-//                         visible splat appends its id to a fixed 256-slot
-//                         slab per tile it touches (slot = atomic count;
-//                         ids past 256 are dropped) and the block-reduced
-//                         tile count goes into this frame's M;
-//   raster_sum_fwd_kernel sorts each tile's slab in LDS -- or, for a tile
-//                         with more than 256 entries, rebuilds its first 256
-//                         ids by scanning every splat's bbox in id order --
-//                         blends, writes the clamped [3,H,W] planes, and
-//                         clears the tile's count for the next frame.
-// M lives in two device slots used on alternate frames (frame_index & 1): the
-// projection clears the other slot, which the previous frame has finished
-// with.  Nothing is read back to the host.
+//                         op sequence) + a 48-byte record per splat (its id
+//                         in a spare lane); each visible splat appends its
+//                         record to a fixed 256-slot slab per tile it touches
+//                         (slot = atomic count; records past 256 dropped) and
+//                         the block-reduced tile count goes into this frame's M;
+//   raster_sum_fwd_kernel loads a tile's count and first 8 records in one
+//                         round trip, ranks <= 64 records by id straight into
+//                         its LDS staging (longer slabs: LDS bitmap sort of
+//                         the ids; more than 256 entries: the first 256 ids
+//                         rebuilt by scanning every splat's bbox in id order),
+//                         blends, and writes the clamped [3,H,W] planes.
+// Counts and M live in two parity slots used on alternate frames
+// (frame_index & 1): each frame clears the other parity, which the previous
+// frame has finished with.  Nothing is read back to the host.
 #include "project2d.h"
 #include "raster_sum.h"
 
 namespace gsvc {
 
-// Append splat i to the slab of every tile of its bbox; the slot atomics are
-// issued in batches of 8 before their results are waited for.
-__device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, int tby, int i,
-                                           unsigned *__restrict__ counts, int *__restrict__ slab) {
+// Append splat i's record to the slab of every tile of its bbox; the slot
+// atomics are issued in batches of 8 before their results are waited for.
+__device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, int tby,
+                                           float4 r0, float4 r1, float4 r2,
+                                           unsigned *__restrict__ counts,
+                                           float4 *__restrict__ slab) {
     unsigned x0, y0, x1, y1;
     tile_bbox(cx, cy, (float)r, tbx, tby, x0, y0, x1, y1);
     constexpr int kBatch = 8;
@@ -45,7 +48,12 @@ __device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, i
             if (k < cnt) sl[k] = atomicAdd(counts + tl[k], 1u);
 #pragma unroll
         for (int k = 0; k < kBatch; ++k)
-            if (k < cnt && sl[k] < (unsigned)kTilePix) slab[(size_t)tl[k] * kTilePix + sl[k]] = i;
+            if (k < cnt && sl[k] < (unsigned)kTilePix) {
+                float4 *d = slab + ((size_t)tl[k] * kTilePix + sl[k]) * 3;
+                d[0] = r0;
+                d[1] = r1;
+                d[2] = r2;
+            }
         hits += cnt;
         cnt = 0;
     };
@@ -64,7 +72,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
     const float *__restrict__ chol_bound, const float *__restrict__ feat,
     const float *__restrict__ rgb_w, const float *__restrict__ opac, float hw, float hh, int tbx,
     int tby, float2 *__restrict__ xys, int *__restrict__ radii, float4 *__restrict__ rec,
-    unsigned *__restrict__ counts, int *__restrict__ slab, int *__restrict__ m_acc,
+    unsigned *__restrict__ counts, float4 *__restrict__ slab, int *__restrict__ m_acc,
     int *__restrict__ m_clear) {
     __shared__ int s_hits[kProjThreads / 64];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -93,10 +101,13 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
         const SplatProj P = project_splat(mx, my, l11, l21, l22, hw, hh, tbx, tby);
         xys[i] = P.xy;
         radii[i] = P.rad;
-        rec[3 * i] = make_float4(P.xy.x, P.xy.y, 0.5f * P.c0, P.c1);
-        rec[3 * i + 1] = make_float4(0.5f * P.c2, o, r, g);
-        rec[3 * i + 2] = make_float4(b, 0.0f, 0.0f, 0.0f);
-        if (P.rad > 0) hits = slab_insert(P.xy.x, P.xy.y, P.rad, tbx, tby, i, counts, slab);
+        const float4 r0 = make_float4(P.xy.x, P.xy.y, 0.5f * P.c0, P.c1);
+        const float4 r1 = make_float4(0.5f * P.c2, o, r, g);
+        const float4 r2 = make_float4(b, __int_as_float(i), 0.0f, 0.0f);
+        rec[3 * i] = r0;
+        rec[3 * i + 1] = r1;
+        rec[3 * i + 2] = r2;
+        if (P.rad > 0) hits = slab_insert(P.xy.x, P.xy.y, P.rad, tbx, tby, r0, r1, r2, counts, slab);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) hits += __shfl_xor(hits, off, 64);
@@ -113,9 +124,9 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
 static inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct FrameWs {
-    unsigned *counts;
+    unsigned *counts;  // [2][T]: this frame's and the next frame's
     int *m_slots;
-    int *slab;
+    float4 *slab;
     float2 *xys;
     int *radii;
     float4 *rec;
@@ -131,12 +142,12 @@ static FrameWs frame_ws(char *base, int n, int ntiles) {
         return p;
     };
     const size_t nn = (size_t)(n > 0 ? n : 1), nt = (size_t)(ntiles > 0 ? ntiles : 1);
-    // first: counts[T] and the two M slots, zeroed by the caller once; every
-    // call leaves them zero (the rasterizer clears each tile's count)
-    w.counts = (unsigned *)take(sizeof(unsigned) * nt + 2 * sizeof(int));
-    w.m_slots = (int *)(w.counts + nt);
-    w.zeroed = sizeof(unsigned) * nt + 2 * sizeof(int);
-    w.slab = (int *)take(sizeof(int) * kTilePix * nt);
+    // first: counts[2][T] and the two M slots, zeroed by the caller once;
+    // frame f counts into parity f & 1 while its rasterizer clears the other
+    w.counts = (unsigned *)take(sizeof(unsigned) * 2 * nt + 2 * sizeof(int));
+    w.m_slots = (int *)(w.counts + 2 * nt);
+    w.zeroed = sizeof(unsigned) * 2 * nt + 2 * sizeof(int);
+    w.slab = (float4 *)take(sizeof(float4) * 3 * kTilePix * nt);
     w.xys = (float2 *)take(sizeof(float2) * nn);
     w.radii = (int *)take(sizeof(int) * nn);
     w.rec = (float4 *)take(sizeof(float4) * 3 * nn);
@@ -180,12 +191,14 @@ extern "C" int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_t
                          workspace_bytes, w.bytes);
     hipStream_t s = (hipStream_t)stream;
     const float hw = 0.5f * (float)img_width, hh = 0.5f * (float)img_height;
-    int *m_acc = w.m_slots + (frame_index & 1), *m_clear = w.m_slots + ((frame_index + 1) & 1);
+    const int par = frame_index & 1;
+    int *m_acc = w.m_slots + par, *m_clear = w.m_slots + (par ^ 1);
+    unsigned *counts = w.counts + (size_t)par * ntiles, *counts_next = w.counts + (size_t)(par ^ 1) * ntiles;
     if (num_points > 0)
         hipLaunchKernelGGL(frame_project_kernel, dim3(ceil_div(num_points, kProjThreads)),
                            dim3(kProjThreads), 0, s, num_points, xyz, xyz_tanh, cholesky,
                            cholesky_bound, features, rgb_w, opacity, hw, hh, tbx, tby, w.xys, w.radii,
-                           w.rec, w.counts, w.slab, m_acc, m_clear);
+                           w.rec, counts, w.slab, m_acc, m_clear);
     else if (hipMemsetAsync(m_acc, 0, sizeof(int), s) != hipSuccess)
         return set_error(GSVC_ERR_HIP, "render_frame_sum: memset failed");
     int rc = check_launch("render_frame_sum: projection");
@@ -202,7 +215,8 @@ extern "C" int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_t
     A.bg = background;
     A.sort_ids = true;
     A.slab = w.slab;
-    A.slab_counts = w.counts;
+    A.slab_counts = counts;
+    A.slab_counts_clear = counts_next;
     A.cull_xys = w.xys;
     A.cull_radii = w.radii;
     A.num_points = num_points;

@@ -15,6 +15,7 @@ struct SumFwdArgs {
     int tbx, img_w, img_h, ntiles, sparse_max, layout;
     bool vec;      // HWC: W % 4 == 0 and 16-byte aligned outputs
     bool vec_chw;  // CHW: W % 4 == 0, H*W % 4 == 0, 16-byte aligned
+    bool nt_store;  // CHW: nontemporal plane stores (gsvc_debug_set(7))
     const int *m_dev;  // device num_intersects (NULL: > 0); 0 -> background
     const float *bg;
     const int *ids;
@@ -25,11 +26,15 @@ struct SumFwdArgs {
     // {b, -, -, -} replace the four arrays above (same values)
     const float4 *rec;
     bool sort_ids;  // ids of a tile arrive unsorted; the kernel sorts them in LDS
-    // frame path: per-tile 256-slot slabs with their counts (cleared here for
-    // the next frame); tiles with more than 256 entries are rebuilt from the
-    // splats' bboxes (cull_xys, cull_radii, num_points)
-    const int *slab;
-    unsigned *slab_counts;
+    // frame path: per-tile 256-slot slabs of splat records (3 float4 each:
+    // {x, y, a/2, b}, {c/2, opacity, r, g}, {b, id bits, -, -}) with their
+    // counts for this frame; the kernel clears the other parity's counts
+    // (slab_counts_clear) for the next frame.  Tiles with more than 256
+    // entries are rebuilt from the splats' bboxes (cull_xys, cull_radii,
+    // num_points) and records (rec).
+    const float4 *slab;
+    const unsigned *slab_counts;
+    unsigned *slab_counts_clear;
     const float2 *cull_xys;
     const int *cull_radii;
     int num_points;

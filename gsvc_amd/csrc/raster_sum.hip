@@ -41,6 +41,7 @@
 namespace gsvc {
 
 constexpr int kChunk = 64;
+constexpr int kSpecSlots = 8;  // slab records loaded with the count (frame path)
 constexpr int kSlice = kTilePix * 3 / 4;  // float4s of LDS per wave (3 KB)
 
 // Forward kernel modes.  Production: the launcher picks kModeSparse (one wave
@@ -52,11 +53,13 @@ constexpr int kSlice = kTilePix * 3 / 4;  // float4s of LDS per wave (3 KB)
 //   3 per-tile choice (2 waves per tile) with timestamps (diagnostic)
 //   4 banded, no blending  5 banded, no stores   (ablations)
 //   6 per-tile choice (2 waves per tile; threshold gsvc_debug_set(3, t))
+//   7 sparse path with 4 timestamps per tile (start, staged, blended, stores
+//     drained) into the buffer of gsvc_debug_set_ptr (diagnostic)
 // A per-tile choice inside one launch was measured slower than either pure
 // mode: a 128-thread workgroup whose second wave exits at once still halves
 // the dispatch rate of sparse tiles.
 enum { kModeAdaptive = 6, kModeSparse = 1, kModeBanded = 2, kModeStamp = 3, kModeNoBlend = 4,
-       kModeNoStore = 5 };
+       kModeNoStore = 5, kModeSparseStamp = 7 };
 constexpr int kDenseEntriesPerTile = 5;
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -76,6 +79,33 @@ __device__ __forceinline__ long long stamp() {
 
 typedef float v2f __attribute__((ext_vector_type(2)));
 
+// One splat against two pixels of a row (packed v_pk_fma / v_pk_mul): the
+// reference's per-pixel op sequence (common.h splat_sigma_h, exp_neg) on both
+// lanes of a v2f.  A pair that fails sigma >= 0 and alpha >= 1/255 keeps its
+// accumulators bit for bit (the update is selected, not added as zero).
+__device__ __forceinline__ void blend_pair(float gx, float ha, float b, float bdy, float cq,
+                                           float opac, float cr, float cg, float cb, v2f px,
+                                           int k, v2f &ar, v2f &ag, v2f &ab, int &l0, int &l1) {
+    const v2f dx = gx - px;
+    const v2f q = __builtin_elementwise_fma((v2f)ha, dx, (v2f)bdy);
+    const v2f sg = __builtin_elementwise_fma(q, dx, (v2f)cq);
+    const v2f x = sg * kNegLog2e;
+    const v2f e = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+    const v2f al = opac * e;
+    const v2f a = {fminf(1.0f, al.x), fminf(1.0f, al.y)};
+    const bool v0 = !(sg.x < 0.0f) && !(a.x < kAlphaMin);
+    const bool v1 = !(sg.y < 0.0f) && !(a.y < kAlphaMin);
+    const v2f nr = __builtin_elementwise_fma((v2f)cr, a, ar);
+    const v2f ng = __builtin_elementwise_fma((v2f)cg, a, ag);
+    const v2f nb = __builtin_elementwise_fma((v2f)cb, a, ab);
+    ar = (v2f){v0 ? nr.x : ar.x, v1 ? nr.y : ar.y};
+    ag = (v2f){v0 ? ng.x : ag.x, v1 ? ng.y : ag.y};
+    ab = (v2f){v0 ? nb.x : ab.x, v1 ? nb.y : ab.y};
+    l0 = v0 ? k : l0;
+    l1 = v1 ? k : l1;
+    (void)b;
+}
+
 // Can splat (x, y, conic a b c, opacity o) reach alpha >= 1/255 on any pixel
 // centre of [x0, x1] x [y0, y1]?  false only when provably not: alpha >= 1/255
 // needs sigma <= ln(255 o), i.e. the point inside the ellipse
@@ -93,6 +123,18 @@ __device__ __forceinline__ bool ellipse_hits_rect(float x, float y, float a, flo
     const float ex = sqrtf(S2 * c / det) * 1.001f + 0.01f;
     const float ey = sqrtf(S2 * a / det) * 1.001f + 0.01f;
     return (x + ex >= x0) && (x - ex <= x1) && (y + ey >= y0) && (y - ey <= y1);
+}
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+// Plane stores of the render layout; ``nt``: nontemporal (streaming) stores.
+__device__ __forceinline__ void st_f4(float *p, float a, float b, float c, float d, bool nt) {
+    if (nt) {
+        const v4f v = {a, b, c, d};
+        __builtin_nontemporal_store(v, reinterpret_cast<v4f *>(p));
+    } else {
+        *reinterpret_cast<float4 *>(p) = make_float4(a, b, c, d);
+    }
 }
 
 __device__ __forceinline__ float clamp01(float x) {
@@ -141,14 +183,30 @@ __device__ __forceinline__ void store_pixel(const SumFwdArgs &A, size_t p, float
 // ``bm`` is 512 words of this wave's LDS (free until blending starts).  Ids
 // are unique within a tile, so this is the stable sort's order.
 constexpr int kSortWords = 512;
-__device__ int wave_sorted_tile_ids(const int *__restrict__ ids, int n_all, int *s_ids,
-                                    unsigned *bm) {
+
+// Id of slot j of a tile's segment: a plain int array, or the id lane of a
+// slab record (stride 12 floats).
+struct SegIds {
+    const int *ids;
+    const float4 *recs;
+    __device__ __forceinline__ int operator[](int j) const {
+        return recs ? __float_as_int(recs[3 * j + 2].y) : ids[j];
+    }
+};
+
+__device__ __forceinline__ int rank_below(int v, int n) {
+    // number of lanes k < n whose value is below v (ties impossible: ids unique)
+    int rank = 0;
+    for (int k = 0; k < n; ++k) rank += (__builtin_amdgcn_readlane(v, k) < v) ? 1 : 0;
+    return rank;
+}
+
+__device__ int wave_sorted_tile_ids(SegIds ids, int n_all, int *s_ids, unsigned *bm) {
     const int lane = threadIdx.x & 63;
     if (n_all <= 0) return 0;
     if (n_all <= 64) {
         const int v = lane < n_all ? ids[lane] : 0x7fffffff;
-        int rank = 0;
-        for (int k = 0; k < n_all; ++k) rank += (__shfl(v, k, 64) < v) ? 1 : 0;
+        const int rank = rank_below(v, n_all);
         if (lane < n_all) s_ids[rank] = v;
         wave_lds_sync();
         return n_all;
@@ -237,7 +295,8 @@ __device__ int wave_brute_tile_ids(const SumFwdArgs &A, int tile, int *s_ids) {
 template <int kMode>
 __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, int2 range, int n,
                                                float4 *s_slice, float3 init, bool ids_in_lds,
-                                               const int *s_ids) {
+                                               const int *s_ids, const float4 *seg_rec,
+                                               float4 spec0, float4 spec1, float4 spec2) {
     float4 *s_geo = s_slice;                           // x, y, 0.5a, b
     float4 *s_col = s_slice + kChunk;                  // 0.5c, opacity, r, g
     float *s_blu = (float *)(s_slice + 2 * kChunk);    // b
@@ -247,12 +306,28 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
     const int pj = tx * kTile + ((lane & 3) << 2);
     const float py = (float)pi;
     const float px0 = (float)pj, px1 = (float)(pj + 1), px2 = (float)(pj + 2), px3 = (float)(pj + 3);
-    float r0 = init.x, g0 = init.y, b0 = init.z, r1 = init.x, g1 = init.y, b1 = init.z;
-    float r2 = init.x, g2 = init.y, b2 = init.z, r3 = init.x, g3 = init.y, b3 = init.z;
+    v2f ar01 = {init.x, init.x}, ag01 = {init.y, init.y}, ab01 = {init.z, init.z};
+    v2f ar23 = ar01, ag23 = ag01, ab23 = ab01;
+    const v2f px01 = {px0, px1}, px23 = {px2, px3};
     int l0 = 0, l1 = 0, l2 = 0, l3 = 0;
     for (int base = 0; base < n; base += kChunk) {
         const int cnt = min(kChunk, n - base);
-        if (lane < cnt) {
+        if (seg_rec) {
+            // <= 64 slab records in fill order: staged at their rank by id
+            float4 geo = spec0, col = spec1, bx = spec2;
+            if (lane >= kSpecSlots && lane < cnt) {
+                geo = seg_rec[3 * lane];
+                col = seg_rec[3 * lane + 1];
+                bx = seg_rec[3 * lane + 2];
+            }
+            const int id = lane < cnt ? __float_as_int(bx.y) : 0x7fffffff;
+            const int rank = rank_below(id, cnt);
+            if (lane < cnt) {
+                s_geo[rank] = geo;
+                s_col[rank] = col;
+                s_blu[rank] = bx.x;
+            }
+        } else if (lane < cnt) {
             float4 geo, col;
             float blu;
             const int j = base + lane;
@@ -262,44 +337,39 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
             s_blu[lane] = blu;
         }
         wave_lds_sync();
+        if (kMode == kModeSparseStamp && base == 0 && lane == 0) A.stamps[4 * (size_t)tile + 1] = stamp();
         const int k0 = range.x + base;
         for (int t = 0; t < cnt; ++t) {
             const float4 G = s_geo[t];
             const float4 C = s_col[t];
+            const float bl = s_blu[t];
             const float dy = G.y - py;
             const float cq = (C.x * dy) * dy;
             const float bdy = G.w * dy;
             const int k = k0 + t;
-#define GSVC_SUM_PIXEL(PX, R, GG, B, L)                                  \
-    {                                                                    \
-        const float dx = G.x - (PX);                                     \
-        const float s = fmaf(fmaf(G.z, dx, bdy), dx, cq);                \
-        const float al = fminf(1.0f, C.y * exp_neg(s));                  \
-        if (!(s < 0.0f) && !(al < kAlphaMin)) {                          \
-            R = fmaf(C.z, al, R);                                        \
-            GG = fmaf(C.w, al, GG);                                      \
-            B = fmaf(s_blu[t], al, B);                                   \
-            L = k;                                                       \
-        }                                                                \
-    }
-            GSVC_SUM_PIXEL(px0, r0, g0, b0, l0)
-            GSVC_SUM_PIXEL(px1, r1, g1, b1, l1)
-            GSVC_SUM_PIXEL(px2, r2, g2, b2, l2)
-            GSVC_SUM_PIXEL(px3, r3, g3, b3, l3)
-#undef GSVC_SUM_PIXEL
+            blend_pair(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, px01, k, ar01, ag01, ab01, l0, l1);
+            blend_pair(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, px23, k, ar23, ag23, ab23, l2, l3);
         }
         wave_lds_sync();
     }
+    if (kMode == kModeSparseStamp && lane == 0) A.stamps[4 * (size_t)tile + 2] = stamp();
+    const float r0 = ar01.x, r1 = ar01.y, r2 = ar23.x, r3 = ar23.y;
+    const float g0 = ag01.x, g1 = ag01.y, g2 = ag23.x, g3 = ag23.y;
+    const float b0 = ab01.x, b1 = ab01.y, b2 = ab23.x, b3 = ab23.y;
     if (A.layout == kLayoutCHWClamped && A.vec_chw && (tx + 1) * kTile <= A.img_w) {
         // 4 lanes write a 64-byte row segment of each plane
         if (pi < A.img_h) {
             const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
             float *o = A.out + (size_t)pi * (size_t)A.img_w + (size_t)pj;
-            *reinterpret_cast<float4 *>(o) = make_float4(clamp01(r0), clamp01(r1), clamp01(r2), clamp01(r3));
-            *reinterpret_cast<float4 *>(o + hw) = make_float4(clamp01(g0), clamp01(g1), clamp01(g2), clamp01(g3));
-            *reinterpret_cast<float4 *>(o + 2 * hw) = make_float4(clamp01(b0), clamp01(b1), clamp01(b2), clamp01(b3));
+            st_f4(o, clamp01(r0), clamp01(r1), clamp01(r2), clamp01(r3), A.nt_store);
+            st_f4(o + hw, clamp01(g0), clamp01(g1), clamp01(g2), clamp01(g3), A.nt_store);
+            st_f4(o + 2 * hw, clamp01(b0), clamp01(b1), clamp01(b2), clamp01(b3), A.nt_store);
             if (A.final_idx)
                 *reinterpret_cast<int4 *>(A.final_idx + (o - A.out)) = make_int4(l0, l1, l2, l3);
+        }
+        if (kMode == kModeSparseStamp) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) A.stamps[4 * (size_t)tile + 3] = stamp();
         }
         return;
     }
@@ -341,7 +411,8 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
 template <int kMode>
 __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int band, int2 range,
                                              int n, float4 *s_slice, float3 init, bool ids_in_lds,
-                                             const int *s_ids) {
+                                             const int *s_ids, const float4 *seg_rec,
+                                             float4 spec0, float4 spec1, float4 spec2) {
     float4 *s_geo = s_slice;                                      // x, y, 0.5a, b
     float4 *s_col = s_slice + kChunk;                             // 0.5c, opacity, r, g
     float *s_blu = reinterpret_cast<float *>(s_slice + 2 * kChunk);
@@ -363,14 +434,42 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
         bool keep = false;
         float4 geo = make_float4(0.f, 0.f, 0.f, 0.f), col = geo;
         float blu = 0.f;
+        int id = 0x7fffffff;
         if (j < n) {
-            load_splat(A, ids_in_lds ? s_ids[j] : A.ids[range.x + j], geo, col, blu);
+            if (seg_rec) {  // <= 64 slab records in fill order
+                float4 bx = spec2;
+                geo = spec0;
+                col = spec1;
+                if (lane >= kSpecSlots) {
+                    geo = seg_rec[3 * j];
+                    col = seg_rec[3 * j + 1];
+                    bx = seg_rec[3 * j + 2];
+                }
+                blu = bx.x;
+                id = __float_as_int(bx.y);
+            } else {
+                load_splat(A, ids_in_lds ? s_ids[j] : A.ids[range.x + j], geo, col, blu);
+            }
             // 2 * (a/2) == a except for subnormal a, where culling is off anyway
             keep = ellipse_hits_rect(geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, bx0,
                                      bx0 + 15.0f, by0, by0 + 7.0f);
         }
         const unsigned long long m = __ballot(keep);
-        if (keep) {
+        if (seg_rec) {
+            // kept records in id order; k = rank among all entries (sorted index)
+            int pos = 0, rank = 0;
+            for (int k = 0; k < n; ++k) {
+                const int below = __builtin_amdgcn_readlane(id, k) < id ? 1 : 0;
+                rank += below;
+                pos += below & (int)((m >> k) & 1ull);
+            }
+            if (keep) {
+                s_geo[pos] = geo;
+                s_col[pos] = col;
+                s_blu[pos] = blu;
+                s_k[pos] = range.x + rank;
+            }
+        } else if (keep) {
             const int pos = __popcll(m & lt);
             s_geo[pos] = geo;
             s_col[pos] = col;
@@ -387,23 +486,7 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
             const float dy = G.y - py;
             const float cq = (C.x * dy) * dy;
             const float bdy = G.w * dy;
-            const v2f dx = G.x - pxv;
-            const v2f q = __builtin_elementwise_fma((v2f)G.z, dx, (v2f)bdy);
-            const v2f sg = __builtin_elementwise_fma(q, dx, (v2f)cq);
-            const v2f x = sg * kNegLog2e;
-            const v2f e = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
-            const v2f al = C.y * e;
-            const float a0 = fminf(1.0f, al.x), a1 = fminf(1.0f, al.y);
-            const bool v0 = !(sg.x < 0.0f) && !(a0 < kAlphaMin);
-            const bool v1 = !(sg.y < 0.0f) && !(a1 < kAlphaMin);
-            // fmaf(c, 0, acc) == acc for finite c: a select on alpha keeps the
-            // oracle's op sequence for the valid pairs
-            const v2f wv = {v0 ? a0 : 0.0f, v1 ? a1 : 0.0f};
-            ar = __builtin_elementwise_fma((v2f)C.z, wv, ar);
-            ag = __builtin_elementwise_fma((v2f)C.w, wv, ag);
-            ab = __builtin_elementwise_fma((v2f)bl, wv, ab);
-            l0 = v0 ? k : l0;
-            l1 = v1 ? k : l1;
+            blend_pair(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, pxv, k, ar, ag, ab, l0, l1);
         }
         wave_lds_sync();
     }
@@ -416,9 +499,17 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
         if (pi < A.img_h) {
             const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
             float *o = A.out + (size_t)pi * (size_t)A.img_w + (size_t)pj;
-            *reinterpret_cast<float2 *>(o) = make_float2(clamp01(ar.x), clamp01(ar.y));
-            *reinterpret_cast<float2 *>(o + hw) = make_float2(clamp01(ag.x), clamp01(ag.y));
-            *reinterpret_cast<float2 *>(o + 2 * hw) = make_float2(clamp01(ab.x), clamp01(ab.y));
+            if (A.nt_store) {
+                __builtin_nontemporal_store((v2f){clamp01(ar.x), clamp01(ar.y)}, reinterpret_cast<v2f *>(o));
+                __builtin_nontemporal_store((v2f){clamp01(ag.x), clamp01(ag.y)},
+                                            reinterpret_cast<v2f *>(o + hw));
+                __builtin_nontemporal_store((v2f){clamp01(ab.x), clamp01(ab.y)},
+                                            reinterpret_cast<v2f *>(o + 2 * hw));
+            } else {
+                *reinterpret_cast<float2 *>(o) = make_float2(clamp01(ar.x), clamp01(ar.y));
+                *reinterpret_cast<float2 *>(o + hw) = make_float2(clamp01(ag.x), clamp01(ag.y));
+                *reinterpret_cast<float2 *>(o + 2 * hw) = make_float2(clamp01(ab.x), clamp01(ab.y));
+            }
             if (A.final_idx) *reinterpret_cast<int2 *>(A.final_idx + (o - A.out)) = make_int2(l0, l1);
         }
         return;
@@ -462,36 +553,48 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
 // kModeSparse launches 64-thread workgroups (one wave per tile); every other
 // mode 128-thread workgroups (two waves per tile).
 template <int kMode>
-__global__ __launch_bounds__(kMode == kModeSparse ? 64 : 128, 8) void raster_sum_fwd_kernel(
-    SumFwdArgs A) {
-    __shared__ float4 s_buf[kMode == kModeSparse ? 1 : 2][kSlice];
-    __shared__ int s_ids[kMode == kModeSparse ? 1 : 2][kTilePix];
-    const int w = (kMode == kModeSparse) ? 0 : (threadIdx.x >> 6);
+__global__ __launch_bounds__(kMode == kModeSparse || kMode == kModeSparseStamp ? 64 : 128, 8) void
+raster_sum_fwd_kernel(SumFwdArgs A) {
+    constexpr bool kOneWave = kMode == kModeSparse || kMode == kModeSparseStamp;
+    __shared__ float4 s_buf[kOneWave ? 1 : 2][kSlice];
+    __shared__ int s_ids[kOneWave ? 1 : 2][kTilePix];
+    const int w = kOneWave ? 0 : (threadIdx.x >> 6);
     const int tile = xcd_remap(blockIdx.x, A.ntiles);
     long long t0 = 0;
-    if (kMode == kModeStamp) t0 = stamp();
+    if (kMode == kModeStamp || kMode == kModeSparseStamp) t0 = stamp();
     int2 range;
-    const int *seg;  // the tile's ids (unsorted when A.sort_ids)
+    SegIds seg;  // the tile's ids (unsorted when A.sort_ids)
     int n_all;
+    const float4 *seg_rec = nullptr;  // slab records, when the fast path applies
+    float4 spec0 = make_float4(0.f, 0.f, 0.f, 0.f), spec1 = spec0, spec2 = spec0;
     if (A.slab) {
-        __shared__ int s_cnt;
+        // this frame's count, and the first kSpecSlots records loaded in the
+        // same round trip (speculatively: most tiles have that few)
+        const int lane = threadIdx.x & 63;
+        const float4 *recs = A.slab + (size_t)tile * kTilePix * 3;
+        n_all = (int)__builtin_amdgcn_readfirstlane(A.slab_counts[tile]);
+        if (lane < kSpecSlots) {
+            spec0 = recs[3 * lane];
+            spec1 = recs[3 * lane + 1];
+            spec2 = recs[3 * lane + 2];
+        }
         if (threadIdx.x == 0) {
-            s_cnt = (int)A.slab_counts[tile];
-            A.slab_counts[tile] = 0u;  // for the next frame
+            A.slab_counts_clear[tile] = 0u;  // the next frame's counts
             if (tile == 0) {
                 A.meta_out[0] = *A.m_dev;
                 A.meta_out[1] = 0;
             }
         }
-        __syncthreads();
-        n_all = s_cnt;
         range = make_int2(0, n_all);
-        seg = A.slab + (size_t)tile * kTilePix;
+        seg.ids = nullptr;
+        seg.recs = recs;
+        if (n_all <= kChunk) seg_rec = recs;
     } else {
         range = A.bins[tile];
         n_all = range.y - range.x;
         n_all = n_all < 0 ? 0 : n_all;
-        seg = A.ids + range.x;
+        seg.ids = A.ids + range.x;
+        seg.recs = nullptr;
     }
     int n = n_all > kTilePix ? kTilePix : n_all;
     // rasterize_sum.py:121-127: a frame without intersections is the background
@@ -501,22 +604,27 @@ __global__ __launch_bounds__(kMode == kModeSparse ? 64 : 128, 8) void raster_sum
         init = make_float3(A.bg[0], A.bg[1], A.bg[2]);
     }
     const int ty = tile / A.tbx;
-    const bool sparse = kMode == kModeSparse ||
+    if (kMode == kModeSparseStamp && threadIdx.x == 0) A.stamps[4 * (size_t)tile] = t0;
+    const bool sparse = kMode == kModeSparse || kMode == kModeSparseStamp ||
                         ((kMode == kModeAdaptive || kMode == kModeStamp) && n <= A.sparse_max);
+    if (n == 0) seg_rec = nullptr;
+    const bool by_ids = A.sort_ids && !seg_rec;  // ids sorted into s_ids first
     if (sparse) {
         if (w != 0) return;
-        if (A.sort_ids)
+        if (by_ids)
             n = (A.slab && n_all > kTilePix)
                     ? wave_brute_tile_ids(A, tile, s_ids[0])
                     : wave_sorted_tile_ids(seg, n_all, s_ids[0], reinterpret_cast<unsigned *>(s_buf[0]));
-        sum_fwd_sparse<kMode>(A, tile, range, n, s_buf[0], init, A.sort_ids, s_ids[0]);
+        sum_fwd_sparse<kMode>(A, tile, range, n, s_buf[0], init, by_ids, s_ids[0], seg_rec, spec0,
+                              spec1, spec2);
     } else {
         if (ty * kTile + w * 8 >= A.img_h) return;  // band below the image
-        if (A.sort_ids)
+        if (by_ids)
             n = (A.slab && n_all > kTilePix)
                     ? wave_brute_tile_ids(A, tile, s_ids[w])
                     : wave_sorted_tile_ids(seg, n_all, s_ids[w], reinterpret_cast<unsigned *>(s_buf[w]));
-        sum_fwd_band<kMode>(A, tile, w, range, n, s_buf[w], init, A.sort_ids, s_ids[w]);
+        sum_fwd_band<kMode>(A, tile, w, range, n, s_buf[w], init, by_ids, s_ids[w], seg_rec, spec0,
+                            spec1, spec2);
     }
     if (kMode == kModeStamp && (threadIdx.x & 63) == 0) {
         long long *st = A.stamps + 4 * (size_t)tile;
@@ -675,6 +783,7 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
     A.vec = (A.img_w % 4 == 0) && (((uintptr_t)A.out & 15) == 0) &&
             (((uintptr_t)A.final_idx & 15) == 0) && (((uintptr_t)A.final_Ts & 15) == 0);
     A.vec_chw = A.vec && (((size_t)A.img_w * (size_t)A.img_h) % 4 == 0);
+    A.nt_store = g_knobs[7] == 0;  // streaming stores unless disabled (A/B knob 7)
     const int ntiles = A.ntiles;
     int mode = g_knobs[0];
     if (mode == 0)
@@ -703,6 +812,12 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
             break;
         case kModeAdaptive:
             hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeAdaptive>, dim3(ntiles), dim3(128), 0, s, A);
+            break;
+        case kModeSparseStamp:
+            if (!g_debug_ptr)
+                return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: mode 7 needs gsvc_debug_set_ptr");
+            A.stamps = reinterpret_cast<long long *>(g_debug_ptr);
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeSparseStamp>, dim3(ntiles), dim3(64), 0, s, A);
             break;
         default:
             return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: unknown kernel mode %d", mode);

@@ -60,6 +60,8 @@ int gsvc_timing_collect(float *ms, int max_out, int *count);
  * mode 6; returns the previous value.  Not part of the reference interface;
  * results are identical for every value (modes 4/5 are ablations). */
 int gsvc_debug_set(int key, int value);
+/* Diagnostic device buffer for timestamp kernel variants (int64 per tile x 4). */
+void gsvc_debug_set_ptr(void *ptr);
 
 /* ---------------------------------------------------------------------------
  * 2D projection.

@@ -12,6 +12,7 @@ harmless here since every frame renders the same splats.)
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -33,6 +34,10 @@ def main():
     ap.add_argument("--chol-scale", type=float, default=1.0)
     ap.add_argument("--modes", type=int, nargs="+", default=[0],
                     help="rasterizer modes (gsvc_debug_set(0)); 0 = automatic")
+    ap.add_argument("--knob", type=int, nargs=2, action="append", default=[],
+                    metavar=("KEY", "VALUE"), help="extra gsvc_debug_set for a second pass")
+    ap.add_argument("--stamps", action="store_true",
+                    help="also run the timestamped one-wave kernel (mode 7) and print phases")
     args = ap.parse_args()
     lib = L.load()
     dev = torch.device("cuda:0")
@@ -49,8 +54,12 @@ def main():
         out = torch.empty((1, 3, H, W), device=dev)
         ref = None
         counter = [0]
-        for mode in args.modes:
+        passes = [(mode, None) for mode in args.modes] + [(m, kv) for kv in args.knob
+                                                          for m in args.modes]
+        for mode, kv in passes:
             lib.gsvc_debug_set(0, mode)
+            if kv:
+                lib.gsvc_debug_set(kv[0], kv[1])
 
             def frame():
                 L.call("gsvc_render_frame_sum", n, L.ptr(xyz), 1, L.ptr(chol), L.ptr(bound),
@@ -81,9 +90,29 @@ def main():
             else:
                 same = bool(torch.equal(out, ref))
             m = int(meta[0])
-            print(json.dumps(dict(N=n, M=m, mode=mode,
+            if kv:
+                lib.gsvc_debug_set(kv[0], 0)
+            print(json.dumps(dict(N=n, M=m, mode=mode, knob=kv,
                                   us_per_frame=round(best, 2), fps=round(1e6 / best, 0),
                                   identical=same)), flush=True)
+        if args.stamps:
+            import numpy as np
+            ntiles = ((W + 15) // 16) * ((H + 15) // 16)
+            st = torch.zeros((ntiles, 4), dtype=torch.int64, device=dev)
+            lib.gsvc_debug_set_ptr(ctypes.c_void_p(st.data_ptr()))
+            lib.gsvc_debug_set(0, 7)
+            for _ in range(5):
+                frame()
+            torch.cuda.synchronize()
+            lib.gsvc_debug_set(0, 0)
+            lib.gsvc_debug_set_ptr(None)
+            t = st.cpu().numpy().astype(np.float64) * 0.01  # 100 MHz ticks -> us
+            t0 = t[:, 0].min()
+            q = lambda x: [round(float(np.percentile(x, p)), 2) for p in (0, 10, 50, 90, 100)]  # noqa
+            print(json.dumps(dict(N=n, stamps="percentiles 0/10/50/90/100 (us)",
+                                  start=q(t[:, 0] - t0), staged=q(t[:, 1] - t[:, 0]),
+                                  blend=q(t[:, 2] - t[:, 1]), stores_drained=q(t[:, 3] - t[:, 2]),
+                                  end=q(t[:, 3] - t0))), flush=True)
     lib.gsvc_debug_set(0, 0)
 
 
