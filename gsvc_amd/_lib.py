@@ -53,6 +53,8 @@ _SIGS = {
     "gsvc_render_frame_zeroed_bytes": [_U, _U],
     "gsvc_render_frame_sum": [_I, _P, _I, _P, _P, _P, _P, _P, _P, _U, _U, _I, _I, _P, _P, _SZ, _P,
                               _P],
+    "gsvc_adan_step": [_I, _P, _P, _P, _P, _P, _P, _P] + [ctypes.c_double] * 9 +
+                      [_I, ctypes.c_double, _P],
     "gsvc_rasterize_sum_backward": [_U, _U, _U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                     _P, _P],
     "gsvc_rasterize_forward": [_I, _I, _I, _I, _I, _I, _U, _U, _U, _P, _P, _P, _P, _P, _P, _P,

@@ -70,7 +70,8 @@ class GaussianVideoFrame(nn.Module):
         self.register_buffer("cholesky_bound", torch.tensor([0.5, 0, 0.5]).view(1, 3))
         self.lr = kwargs["lr"]
         self.opt_type = kwargs["opt_type"]
-        self.fused_adan = kwargs.get("fused_adan", False)
+        # the fused HIP Adan on GPU models (numerically the foreach update)
+        self.fused_adan = kwargs.get("fused_adan", str(self.device).startswith("cuda"))
         self.update_optimizer()
         self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=20000, gamma=0.5)
 
@@ -208,7 +209,7 @@ class GaussianVideoFrame(nn.Module):
 
 def make_frame_model(H, W, num_points, device, seed=None, lr=1e-3, isremoval=False,
                      isdensity=False, removal_rate=0.1, max_num_points=None,
-                     densification_interval=100, fused_adan=False):
+                     densification_interval=100, fused_adan=None):
     """Construct like SimpleTrainer2d does (train_video_Represent.py:51-55)."""
     if seed is not None:
         torch.manual_seed(seed)
@@ -217,7 +218,7 @@ def make_frame_model(H, W, num_points, device, seed=None, lr=1e-3, isremoval=Fal
         max_num_points=max_num_points or num_points, densification_interval=densification_interval,
         iterations=30000, H=H, W=W, BLOCK_H=16, BLOCK_W=16, device=device, lr=lr, quantize=False,
         removal_rate=removal_rate, isdensity=isdensity, isremoval=isremoval,
-        fused_adan=fused_adan).to(device)
+        **({} if fused_adan is None else {"fused_adan": fused_adan})).to(device)
     return model
 
 

@@ -432,3 +432,35 @@ __all__ = [
     "map_gaussian_to_intersects", "get_tile_bin_edges", "rasterize_sum_forward",
     "rasterize_sum_backward", "rasterize_forward", "rasterize_backward",
 ]
+
+
+# ---------------------------------------------------------------------------
+# Fused Adan (optimizer.py:296-362)
+
+def adan_step(params, grads, exp_avgs, exp_avg_sqs, exp_avg_diffs, neg_pre_grads, *, beta1,
+              beta2, beta3, bias_correction1, bias_correction2, bias_correction3_sqrt, lr,
+              weight_decay, eps, no_prox, clip_global_grad_norm):
+    """One fused Adan update of every tensor (gsvc_adan_step); same keyword
+    arguments as _multi_tensor_adan.  Tensors must be contiguous fp32 CUDA."""
+    import ctypes
+    lists = (params, grads, exp_avgs, exp_avg_sqs, exp_avg_diffs, neg_pre_grads)
+    n = len(params)
+    if n == 0:
+        return
+    if any(len(x) != n for x in lists):
+        raise RuntimeError("adan_step: tensor lists differ in length")
+    for group in lists:
+        for t in group:
+            if not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous():
+                raise RuntimeError("adan_step: tensors must be contiguous float32 CUDA tensors")
+    for i in range(n):
+        if any(x[i].numel() != params[i].numel() for x in lists):
+            raise RuntimeError("adan_step: tensor sizes differ")
+    P = ctypes.c_void_p * n
+    arrs = [P(*[t.data_ptr() for t in group]) for group in lists]
+    numels = (ctypes.c_longlong * n)(*[t.numel() for t in params])
+    clip = float(clip_global_grad_norm)
+    L.call("gsvc_adan_step", n, numels, *arrs, float(beta1), float(beta2), float(beta3),
+           float(bias_correction1), float(bias_correction2), float(bias_correction3_sqrt),
+           float(lr), float(weight_decay), float(eps), 1 if no_prox else 0, clip,
+           L.stream(params[0].device))

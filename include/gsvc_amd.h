@@ -47,6 +47,20 @@ enum gsvc_status {
 int gsvc_abi_version(void);
 const char *gsvc_last_error(void);
 
+/* ---------------------------------------------------------------------------
+ * Fused Adan step (optimizer.py:296-362 _multi_tensor_adan, one kernel for
+ * all tensors).  Host arrays of ntensors device pointers / element counts;
+ * every tensor contiguous fp32.  Scalars as in the reference (bias
+ * corrections computed by the caller, optimizer.py:171-173,211).  grads are
+ * read, not scaled in place. */
+int gsvc_adan_step(int ntensors, const long long *numels, float *const *params,
+                   const float *const *grads, float *const *exp_avgs,
+                   float *const *exp_avg_sqs, float *const *exp_avg_diffs,
+                   float *const *neg_pre_grads, double beta1, double beta2, double beta3,
+                   double bias_correction1, double bias_correction2,
+                   double bias_correction3_sqrt, double lr, double weight_decay, double eps,
+                   int no_prox, double clip_global_grad_norm, void *stream);
+
 /* Launch timing of the sum-forward composite kernel (every rasterizer entry
  * point above): after gsvc_timing_enable(max, every), every every-th launch
  * is bracketed by HIP events recorded on its stream (up to max launches);
