@@ -53,6 +53,9 @@ _SIGS = {
     "gsvc_render_frame_zeroed_bytes": [_U, _U],
     "gsvc_render_frame_sum": [_I, _P, _I, _P, _P, _P, _P, _P, _P, _U, _U, _I, _I, _P, _P, _SZ, _P,
                               _P],
+    "gsvc_train_step_workspace_bytes": [_I, _U, _U],
+    "gsvc_train_step_sum": [_I, _P, _P, _P, _P, _P, _I, _P, _P, _U, _U, _I, _I, _P, _P, _I, _P, _P,
+                            _P, _P, _SZ, _P],
     "gsvc_adan_step": [_I, _P, _P, _P, _P, _P, _P, _P] + [ctypes.c_double] * 9 +
                       [_I, ctypes.c_double, _P],
     "gsvc_rasterize_sum_backward": [_U, _U, _U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
@@ -71,6 +74,7 @@ _RESTYPE = {
     "gsvc_bin_tiles_counted_workspace_bytes": _SZ,
     "gsvc_render_frame_workspace_bytes": _SZ,
     "gsvc_render_frame_zeroed_bytes": _SZ,
+    "gsvc_train_step_workspace_bytes": _SZ,
 }
 
 ABI_VERSION = 1

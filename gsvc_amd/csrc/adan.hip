@@ -16,7 +16,7 @@
 // itself is not written back (the reference scales p.grad in place, but
 // train_iter clears it right after the step).  fp32 throughout; results
 // agree with the foreach path to rounding (tests/test_adan.py).
-#include "common.h"
+#include "adan.h"
 
 namespace gsvc {
 
@@ -28,29 +28,16 @@ struct AdanArgs {
     float *p[kAdanMaxTensors];
     const float *g[kAdanMaxTensors];
     float *m[kAdanMaxTensors], *v[kAdanMaxTensors], *diff[kAdanMaxTensors], *npg[kAdanMaxTensors];
-    float b1, b2, b3, one_m_b1, one_m_b2, one_m_b3, bc3_sqrt, eps, step, step_diff, clip;
-    float decay_mul, decay_div;  // no_prox: p *= decay_mul first; else p /= decay_div after
-    int no_prox;
+    AdanScalars S;
 };
 
 __device__ __forceinline__ void adan_elem(const AdanArgs &A, int t, long long j) {
-    const float g = A.g[t][j] * A.clip;
-    const float d = A.npg[t][j] + g;
-    const float m = A.m[t][j] * A.b1 + A.one_m_b1 * g;
-    const float df = A.diff[t][j] * A.b2 + A.one_m_b2 * d;
-    const float tt = d * A.b2 + g;
-    const float v = A.v[t][j] * A.b3 + A.one_m_b3 * (tt * tt);
-    const float den = sqrtf(v) / A.bc3_sqrt + A.eps;
-    float p = A.p[t][j];
-    if (A.no_prox) p = p * A.decay_mul;
-    p = p + (-A.step) * (m / den);
-    p = p + (-A.step_diff) * (df / den);
-    if (!A.no_prox) p = p / A.decay_div;
-    A.p[t][j] = p;
+    float m = A.m[t][j], v = A.v[t][j], df = A.diff[t][j], npg = A.npg[t][j];
+    A.p[t][j] = adan_update(A.S, A.p[t][j], A.g[t][j], m, v, df, npg);
     A.m[t][j] = m;
     A.diff[t][j] = df;
     A.v[t][j] = v;
-    A.npg[t][j] = -g;
+    A.npg[t][j] = npg;
 }
 
 __global__ __launch_bounds__(256) void adan_kernel(AdanArgs A) {
@@ -78,21 +65,8 @@ extern "C" int gsvc_adan_step(int ntensors, const long long *numels, float *cons
                                           !exp_avg_sqs || !exp_avg_diffs || !neg_pre_grads)))
         return set_error(GSVC_ERR_ARG, "adan_step: bad arguments");
     AdanArgs A{};
-    // torch's foreach ops take Python-float scalars as fp32 for fp32 tensors
-    A.b1 = (float)beta1;
-    A.b2 = (float)beta2;
-    A.b3 = (float)beta3;
-    A.one_m_b1 = (float)(1.0 - beta1);
-    A.one_m_b2 = (float)(1.0 - beta2);
-    A.one_m_b3 = (float)(1.0 - beta3);
-    A.bc3_sqrt = (float)bias_correction3_sqrt;
-    A.eps = (float)eps;
-    A.step = (float)(lr / bias_correction1);
-    A.step_diff = (float)(lr * beta2 / bias_correction2);
-    A.clip = (float)clip_global_grad_norm;
-    A.decay_mul = (float)(1.0 - lr * weight_decay);
-    A.decay_div = (float)(1.0 + lr * weight_decay);
-    A.no_prox = no_prox;
+    A.S = adan_scalars(beta1, beta2, beta3, bias_correction1, bias_correction2,
+                       bias_correction3_sqrt, lr, weight_decay, eps, no_prox, clip_global_grad_norm);
     hipStream_t s = (hipStream_t)stream;
     for (int base = 0; base < ntensors; base += kAdanMaxTensors) {
         const int k = min(kAdanMaxTensors, ntensors - base);

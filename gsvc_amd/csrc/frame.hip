@@ -25,6 +25,7 @@
 // Counts and M live in two parity slots used on alternate frames
 // (frame_index & 1): each frame clears the other parity, which the previous
 // frame has finished with.  Nothing is read back to the host.
+#include "frame.h"
 #include "project2d.h"
 #include "raster_sum.h"
 
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
     const float *__restrict__ rgb_w, const float *__restrict__ opac, float hw, float hh, int tbx,
     int tby, float2 *__restrict__ xys, int *__restrict__ radii, float4 *__restrict__ rec,
     unsigned *__restrict__ counts, float4 *__restrict__ slab, int *__restrict__ m_acc,
-    int *__restrict__ m_clear) {
+    int *__restrict__ m_clear, float4 *__restrict__ grad_zero) {
     __shared__ int s_hits[kProjThreads / 64];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x == 0) *m_clear = 0;  // the next frame's slot
@@ -103,10 +104,17 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
         radii[i] = P.rad;
         const float4 r0 = make_float4(P.xy.x, P.xy.y, 0.5f * P.c0, P.c1);
         const float4 r1 = make_float4(0.5f * P.c2, o, r, g);
-        const float4 r2 = make_float4(b, __int_as_float(i), 0.0f, 0.0f);
+        const float4 r2 = make_float4(b, __int_as_float(i), P.c0, P.c2);
         rec[3 * i] = r0;
         rec[3 * i + 1] = r1;
         rec[3 * i + 2] = r2;
+        if (grad_zero) {
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            grad_zero[4 * i] = z;
+            grad_zero[4 * i + 1] = z;
+            grad_zero[4 * i + 2] = z;
+            grad_zero[4 * i + 3] = z;
+        }
         if (P.rad > 0) hits = slab_insert(P.xy.x, P.xy.y, P.rad, tbx, tby, r0, r1, r2, counts, slab);
     }
 #pragma unroll
@@ -121,24 +129,12 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
     }
 }
 
-static inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
-
-struct FrameWs {
-    unsigned *counts;  // [2][T]: this frame's and the next frame's
-    int *m_slots;
-    float4 *slab;
-    float2 *xys;
-    int *radii;
-    float4 *rec;
-    size_t zeroed, bytes;
-};
-
-static FrameWs frame_ws(char *base, int n, int ntiles) {
+FrameWs frame_ws(char *base, int n, int ntiles) {
     FrameWs w;
     size_t off = 0;
     auto take = [&](size_t bytes) {
         char *p = base ? base + off : nullptr;
-        off += align_up(bytes);
+        off += ws_align(bytes);
         return p;
     };
     const size_t nn = (size_t)(n > 0 ? n : 1), nt = (size_t)(ntiles > 0 ? ntiles : 1);
@@ -155,8 +151,30 @@ static FrameWs frame_ws(char *base, int n, int ntiles) {
     return w;
 }
 
-static int tiles_of(unsigned h, unsigned w) {
-    return ceil_div((int)w, kTile) * ceil_div((int)h, kTile);
+FrameSlots frame_slots(const FrameWs &w, int ntiles, int frame_index) {
+    const int par = frame_index & 1;
+    FrameSlots f;
+    f.m_acc = w.m_slots + par;
+    f.m_clear = w.m_slots + (par ^ 1);
+    f.counts = w.counts + (size_t)par * ntiles;
+    f.counts_next = w.counts + (size_t)(par ^ 1) * ntiles;
+    return f;
+}
+
+int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *chol,
+                         const float *chol_bound, const float *feat, const float *rgb_w,
+                         const float *opac, unsigned img_h, unsigned img_w, const FrameWs &w,
+                         const FrameSlots &f, float4 *grad_zero, hipStream_t s) {
+    const int tbx = ceil_div((int)img_w, kTile), tby = ceil_div((int)img_h, kTile);
+    const float hw = 0.5f * (float)img_w, hh = 0.5f * (float)img_h;
+    if (n > 0)
+        hipLaunchKernelGGL(frame_project_kernel, dim3(ceil_div(n, kProjThreads)), dim3(kProjThreads),
+                           0, s, n, xyz, xyz_tanh, chol, chol_bound, feat, rgb_w, opac, hw, hh, tbx,
+                           tby, w.xys, w.radii, w.rec, f.counts, w.slab, f.m_acc, f.m_clear,
+                           grad_zero);
+    else if (hipMemsetAsync(f.m_acc, 0, sizeof(int), s) != hipSuccess)
+        return set_error(GSVC_ERR_HIP, "frame projection: memset failed");
+    return check_launch("frame projection");
 }
 
 }  // namespace gsvc
@@ -190,18 +208,9 @@ extern "C" int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_t
         return set_error(GSVC_ERR_WORKSPACE, "render_frame_sum: workspace too small (%zu < %zu)",
                          workspace_bytes, w.bytes);
     hipStream_t s = (hipStream_t)stream;
-    const float hw = 0.5f * (float)img_width, hh = 0.5f * (float)img_height;
-    const int par = frame_index & 1;
-    int *m_acc = w.m_slots + par, *m_clear = w.m_slots + (par ^ 1);
-    unsigned *counts = w.counts + (size_t)par * ntiles, *counts_next = w.counts + (size_t)(par ^ 1) * ntiles;
-    if (num_points > 0)
-        hipLaunchKernelGGL(frame_project_kernel, dim3(ceil_div(num_points, kProjThreads)),
-                           dim3(kProjThreads), 0, s, num_points, xyz, xyz_tanh, cholesky,
-                           cholesky_bound, features, rgb_w, opacity, hw, hh, tbx, tby, w.xys, w.radii,
-                           w.rec, counts, w.slab, m_acc, m_clear);
-    else if (hipMemsetAsync(m_acc, 0, sizeof(int), s) != hipSuccess)
-        return set_error(GSVC_ERR_HIP, "render_frame_sum: memset failed");
-    int rc = check_launch("render_frame_sum: projection");
+    const FrameSlots f = frame_slots(w, ntiles, frame_index);
+    int rc = frame_project_launch(num_points, xyz, xyz_tanh, cholesky, cholesky_bound, features,
+                                  rgb_w, opacity, img_height, img_width, w, f, nullptr, s);
     if (rc) return rc;
     SumFwdArgs A;
     sum_fwd_args_init(A);
@@ -210,13 +219,13 @@ extern "C" int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_t
     A.img_h = (int)img_height;
     A.ntiles = ntiles;
     A.layout = kLayoutCHWClamped;
-    A.m_dev = m_acc;
+    A.m_dev = f.m_acc;
     A.meta_out = meta;
     A.bg = background;
     A.sort_ids = true;
     A.slab = w.slab;
-    A.slab_counts = counts;
-    A.slab_counts_clear = counts_next;
+    A.slab_counts = f.counts;
+    A.slab_counts_clear = f.counts_next;
     A.cull_xys = w.xys;
     A.cull_radii = w.radii;
     A.num_points = num_points;

@@ -1,0 +1,528 @@
+// Fused training step of GSVC's per-frame model (gfx950): one
+// GaussianVideo_frame.train_iter with the L2 (or L1) loss and Adan, in three
+// kernels and one C call, with no host synchronisation.
+//
+// Reference: GaussianSplats_Represent.py:191-207 (train_iter): the forward
+// :83-90 (activations :57-70, project_gaussians_2d, rasterize_gaussians_sum,
+// clamp, NCHW), loss_fn (utils.py:21-28: F.mse_loss / F.l1_loss),
+// loss.backward() through the clamp, the sum rasterizer (backward.cu:696-862),
+// the 2D projection (backward2d.cu:8-51) and the activations, the MSE behind
+// the PSNR (:196-198), and Adan.step (optimizer.py:124-235, 296-362).
+//
+//   frame_project_kernel (frame.hip)  activations + projection + per-tile
+//       256-slot record slabs, exactly as the frame render; also zeroes the
+//       splat's 64-byte gradient record;
+//   train_tile_kernel  one 256-thread workgroup per 16x16 tile: the tile's
+//       first <= 256 entries in splat-id order into LDS (ranks by compare;
+//       a slab that overflowed is rebuilt from the splats' bboxes in id
+//       order); a pixel-parallel forward with the rasterizer's op sequence
+//       (the same image bits as the render), the clamp, the loss gradient
+//       against gt and the tile's error sums; then an entry-parallel backward
+//       of the tile into the splats' gradient records (one atomic request per
+//       (splat, tile)).  Image, final_idx and v_out never reach HBM: per pixel
+//       the step reads gt once;
+//   train_splat_kernel  one lane per splat: projection VJP (the reference's
+//       doubled L cross term), activation VJPs and the Adan update of every
+//       parameter element; block 0 sums the tiles' errors in a fixed order
+//       into the loss.
+#include "adan.h"
+#include "frame.h"
+
+namespace gsvc {
+
+constexpr int kT = kTilePix;  // threads = pixels = entries of one tile
+
+struct TrainTileArgs {
+    int tbx, img_w, img_h, ntiles, num_points, loss_l1;
+    float norm;  // d loss / d pixel scale: float(2 / numel) for L2, 1.0f / numel for L1
+    const float4 *slab;
+    const unsigned *counts;
+    unsigned *counts_clear;
+    const int *m_dev;
+    const float2 *xys;
+    const int *radii;
+    const float4 *rec;
+    const float *bg;
+    const float *gt;  // [3, H, W]
+    float *grad;      // [N, 16]: v_xy 0:2, v_conic 2:5, v_colors 5:8, v_opacity 8
+    float2 *err;      // [ntiles]: sum of squared, sum of absolute errors
+    float *out;       // optional [3, H, W] clamped render
+};
+
+__device__ __forceinline__ float clamp_unit(float x) {
+    // torch.clamp(x, 0, 1): NaN stays NaN
+    return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x);
+}
+
+__device__ __forceinline__ int ceil_log2_i(int n) { return n <= 1 ? 0 : 32 - __clz(n - 1); }
+
+// The first <= 256 ids (ascending) of the splats whose bbox covers tile
+// (tx, ty) -- the slab insertion's own test -- for a tile whose slab kept an
+// arbitrary 256 of more entries: 256 candidates per round, compacted by ballot.
+__device__ int block_brute_ids(const TrainTileArgs &A, int tx, int ty, int *s_gid, int *s_cnt) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tby = (A.img_h + kTile - 1) / kTile;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int written = 0;
+    for (int base = 0; base < A.num_points && written < kT; base += kT) {
+        const int j = base + tid;
+        bool hit = false;
+        if (j < A.num_points) {
+            const int r = A.radii[j];
+            if (r > 0) {
+                const float2 c = A.xys[j];
+                unsigned x0, y0, x1, y1;
+                tile_bbox(c.x, c.y, (float)r, A.tbx, tby, x0, y0, x1, y1);
+                hit = (unsigned)tx >= x0 && (unsigned)tx < x1 && (unsigned)ty >= y0 &&
+                      (unsigned)ty < y1;
+            }
+        }
+        const unsigned long long m = __ballot(hit);
+        if (lane == 0) s_cnt[w] = __popcll(m);
+        __syncthreads();
+        int pos = written + __popcll(m & lt);
+        for (int q = 0; q < w; ++q) pos += s_cnt[q];
+        if (hit && pos < kT) s_gid[pos] = j;
+        written += (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
+        __syncthreads();
+    }
+    return min(written, kT);
+}
+
+__global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
+    __shared__ float4 s_geo[kT];  // x, y, a/2, b
+    __shared__ float4 s_col[kT];  // c/2, opacity, r, g
+    __shared__ float4 s_ext[kT];  // b, id bits, a, c
+    __shared__ float4 s_pix[kT];  // v_out rgb, last contributing entry (bits; -1 outside)
+    __shared__ float s_red[9][kT];
+    __shared__ int s_cnt[4];
+    __shared__ float s_err[2][4];
+    const int tile = xcd_remap(blockIdx.x, A.ntiles);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int ty = tile / A.tbx, tx = tile - ty * A.tbx;
+    const bool empty = *A.m_dev < 1;  // rasterize_sum.py:121-127: background, no gradient
+    const int n_all = empty ? 0 : (int)A.counts[tile];
+    if (tid == 0) A.counts_clear[tile] = 0u;  // the next frame's counts
+
+    // 1. the tile's first <= 256 entries in (tile, splat id) order into LDS
+    int n;
+    if (n_all <= kT) {
+        int *ids = reinterpret_cast<int *>(s_red[0]);
+        float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+        int id = 0x7fffffff;
+        if (tid < n_all) {
+            const float4 *r = A.slab + ((size_t)tile * kT + tid) * 3;
+            r0 = r[0];
+            r1 = r[1];
+            r2 = r[2];
+            id = __float_as_int(r2.y);
+        }
+        ids[tid] = id;
+        __syncthreads();
+        if (tid < n_all) {
+            int rank = 0;
+            for (int j = 0; j < n_all; ++j) rank += ids[j] < id ? 1 : 0;  // ids are unique
+            s_geo[rank] = r0;
+            s_col[rank] = r1;
+            s_ext[rank] = r2;
+        }
+        n = n_all;
+    } else {
+        int *ids = reinterpret_cast<int *>(s_red[0]);
+        n = block_brute_ids(A, tx, ty, ids, s_cnt);
+        if (tid < n) {
+            const int g = ids[tid];
+            s_geo[tid] = A.rec[3 * g];
+            s_col[tid] = A.rec[3 * g + 1];
+            s_ext[tid] = A.rec[3 * g + 2];
+        }
+    }
+    __syncthreads();
+
+    // 2. pixel-parallel forward (the sum rasterizer's op sequence), clamp, loss
+    const int pi = ty * kTile + (tid >> 4), pj = tx * kTile + (tid & 15);
+    const bool inside = pi < A.img_h && pj < A.img_w;
+    float o[3] = {0.f, 0.f, 0.f};
+    if (empty) {
+        o[0] = A.bg[0];
+        o[1] = A.bg[1];
+        o[2] = A.bg[2];
+    }
+    int last = 0;
+    {
+        const float py = (float)pi, px = (float)pj;
+        for (int k = 0; k < n; ++k) {
+            const float4 G = s_geo[k];
+            const float4 C = s_col[k];
+            const float dy = G.y - py;
+            const float cq = (C.x * dy) * dy;
+            const float bdy = G.w * dy;
+            const float dx = G.x - px;
+            const float sg = fmaf(fmaf(G.z, dx, bdy), dx, cq);
+            const float al = fminf(1.0f, C.y * __builtin_amdgcn_exp2f(sg * kNegLog2e));
+            if (!(sg < 0.0f) && !(al < kAlphaMin)) {
+                o[0] = fmaf(C.z, al, o[0]);
+                o[1] = fmaf(C.w, al, o[1]);
+                o[2] = fmaf(s_ext[k].x, al, o[2]);
+                last = k;
+            }
+        }
+    }
+    float v[3] = {0.f, 0.f, 0.f}, se = 0.f, ae = 0.f;
+    if (inside) {
+        const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
+        const size_t p = (size_t)pi * (size_t)A.img_w + (size_t)pj;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float x = clamp_unit(o[c]);
+            const float d = x - A.gt[c * hw + p];
+            se = fmaf(d, d, se);
+            ae += fabsf(d);
+            // mse_loss backward: norm * (a - b) * 1; l1: (1 / numel) * sgn(a - b);
+            // clamp backward passes where 0 <= out <= 1
+            const float sg = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+            const float gv = A.loss_l1 ? A.norm * sg : A.norm * d;
+            v[c] = (o[c] >= 0.0f && o[c] <= 1.0f) ? gv : 0.0f;
+            if (A.out) A.out[c * hw + p] = x;
+        }
+    }
+    s_pix[tid] = make_float4(v[0], v[1], v[2], __int_as_float(inside ? last : -1));
+    int f = inside ? last : -1;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        se += __shfl_xor(se, off, 64);
+        ae += __shfl_xor(ae, off, 64);
+        f = max(f, __shfl_xor(f, off, 64));
+    }
+    if (lane == 0) {
+        s_err[0][w] = se;
+        s_err[1][w] = ae;
+        s_cnt[w] = f;
+    }
+    __syncthreads();
+    if (tid == 0)
+        A.err[tile] = make_float2((s_err[0][0] + s_err[0][1]) + (s_err[0][2] + s_err[0][3]),
+                                  (s_err[1][0] + s_err[1][1]) + (s_err[1][2] + s_err[1][3]));
+    const int maxf = max(max(s_cnt[0], s_cnt[1]), max(s_cnt[2], s_cnt[3]));
+    const int kend = min(n, maxf + 1);  // entries past every pixel's last contribute nothing
+    if (kend <= 0) return;
+
+    // 3. entry-parallel backward: with E = next pow2 >= kend entries, thread t
+    // takes entry t % E against the pixels [E * (t / E), + E), so gradients
+    // accumulate in registers; the 256 / E groups are combined once per entry
+    const int lg = ceil_log2_i(kend);
+    const int E = 1 << lg;
+    const int e = tid & (E - 1);
+    const int p_begin = (tid >> lg) << lg;
+    const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
+    float a_r = 0.f, a_g = 0.f, a_b = 0.f, a_c0 = 0.f, a_c1 = 0.f, a_c2 = 0.f;
+    float a_x = 0.f, a_y = 0.f, a_o = 0.f;
+    if (e < kend) {
+        const float4 G = s_geo[e];
+        const float4 C = s_col[e];
+        const float4 X = s_ext[e];
+        for (int pp = 0; pp < E; ++pp) {
+            const int p = p_begin + pp;
+            const float4 P = s_pix[p];
+            if (e > __float_as_int(P.w)) continue;
+            const float dx = G.x - (tx0 + (float)(p & 15));
+            const float dy = G.y - (ty0 + (float)(p >> 4));
+            const float s = splat_sigma_h(G.z, G.w, C.x, dx, dy);
+            const float vis = exp_neg(s);
+            const float al = fminf(1.0f, C.y * vis);
+            if (s < 0.0f || al < kAlphaMin) continue;
+            const float v_alpha = fmaf(X.x, P.z, fmaf(C.w, P.y, C.z * P.x));
+            const float v_sigma = (-C.y * vis) * v_alpha;
+            a_r = fmaf(al, P.x, a_r);
+            a_g = fmaf(al, P.y, a_g);
+            a_b = fmaf(al, P.z, a_b);
+            const float hs = 0.5f * v_sigma;
+            const float hsdx = hs * dx;
+            a_c0 = fmaf(hsdx, dx, a_c0);
+            a_c1 = fmaf(hsdx, dy, a_c1);
+            a_c2 = fmaf(hs * dy, dy, a_c2);
+            a_x = fmaf(v_sigma, fmaf(X.z, dx, G.w * dy), a_x);
+            a_y = fmaf(v_sigma, fmaf(G.w, dx, X.w * dy), a_y);
+            a_o = fmaf(vis, v_alpha, a_o);
+        }
+    }
+    if (E < 64) {
+        for (int off = 32; off >= E; off >>= 1) {
+            a_r += __shfl_xor(a_r, off, 64);
+            a_g += __shfl_xor(a_g, off, 64);
+            a_b += __shfl_xor(a_b, off, 64);
+            a_c0 += __shfl_xor(a_c0, off, 64);
+            a_c1 += __shfl_xor(a_c1, off, 64);
+            a_c2 += __shfl_xor(a_c2, off, 64);
+            a_x += __shfl_xor(a_x, off, 64);
+            a_y += __shfl_xor(a_y, off, 64);
+            a_o += __shfl_xor(a_o, off, 64);
+        }
+    }
+    const int S = E < 64 ? 64 : E;
+    if (E >= 64 || lane < E) {
+        s_red[0][tid] = a_x;
+        s_red[1][tid] = a_y;
+        s_red[2][tid] = a_c0;
+        s_red[3][tid] = a_c1;
+        s_red[4][tid] = a_c2;
+        s_red[5][tid] = a_r;
+        s_red[6][tid] = a_g;
+        s_red[7][tid] = a_b;
+        s_red[8][tid] = a_o;
+    }
+    __syncthreads();
+    if (tid < kend) {
+        const int reps = kT / S;
+#pragma unroll
+        for (int c = 0; c < 9; ++c) {
+            float val = s_red[c][tid];
+            for (int j = 1; j < reps; ++j) val += s_red[c][tid + j * S];
+            s_red[c][tid] = val;
+        }
+    }
+    __syncthreads();
+    // 16 lanes per entry, 9 of them add one float each into the splat's
+    // 64-byte gradient record: one memory request per (splat, tile)
+    for (int q = tid; q < kend * 16; q += kT) {
+        const int e2 = q >> 4, c = q & 15;
+        if (c < 9) unsafeAtomicAdd(A.grad + (size_t)__float_as_int(s_ext[e2].y) * 16 + c, s_red[c][e2]);
+    }
+}
+
+struct TrainSplatArgs {
+    int n, ntiles, rgbw_train, update;
+    float hw, hh;
+    double inv_count;
+    float *xyz, *chol, *feat, *rgbw;
+    const float *chol_bound;
+    const int *radii;
+    const float4 *rec;
+    const float4 *grad;  // [N][4]
+    float *state[4][4];  // [xyz, chol, feat, rgb_w][exp_avg, exp_avg_sq, exp_avg_diff, neg_pre_grad]
+    int first[4];        // the parameter's first Adan step (optimizer.py:187-189)
+    AdanScalars S;
+    float *grads_out;    // update == 0: [N, 9] = d_xyz 2, d_chol 3, d_feat 3, d_rgbw 1
+    const float2 *err;
+    float *loss;         // [2]: mean squared error, mean absolute error
+};
+
+__device__ __forceinline__ void adan_at(const TrainSplatArgs &A, int q, float *param, size_t j,
+                                        float g) {
+    float m = A.state[q][0][j], v = A.state[q][1][j], df = A.state[q][2][j];
+    float npg = A.first[q] ? -(g * A.S.clip) : A.state[q][3][j];
+    param[j] = adan_update(A.S, param[j], g, m, v, df, npg);
+    A.state[q][0][j] = m;
+    A.state[q][1][j] = v;
+    A.state[q][2][j] = df;
+    A.state[q][3][j] = npg;
+}
+
+__global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
+    if (blockIdx.x == 0) {
+        // the loss: tiles' error sums in a fixed order, in double
+        __shared__ double s_l[2][4];
+        double s2 = 0.0, s1 = 0.0;
+        for (int t = threadIdx.x; t < A.ntiles; t += 256) {
+            const float2 e = A.err[t];
+            s2 += (double)e.x;
+            s1 += (double)e.y;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            s2 += __shfl_xor(s2, off, 64);
+            s1 += __shfl_xor(s1, off, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            s_l[0][threadIdx.x >> 6] = s2;
+            s_l[1][threadIdx.x >> 6] = s1;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            A.loss[0] = (float)(((s_l[0][0] + s_l[0][1]) + (s_l[0][2] + s_l[0][3])) * A.inv_count);
+            A.loss[1] = (float)(((s_l[1][0] + s_l[1][1]) + (s_l[1][2] + s_l[1][3])) * A.inv_count);
+        }
+    }
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.n) return;
+    const float4 g0 = A.grad[4 * i];      // v_xy.x, v_xy.y, v_conic 0, v_conic 1
+    const float4 g1 = A.grad[4 * i + 1];  // v_conic 2, v_colors r g b
+    // 2D projection VJP, backward2d.cu:8-51 (the op's project2d_bwd_kernel sequence)
+    float vl0 = 0.f, vl1 = 0.f, vl2 = 0.f, vmx = 0.f, vmy = 0.f;
+    float l11 = A.chol[3 * i], l21 = A.chol[3 * i + 1], l22 = A.chol[3 * i + 2];
+    if (A.chol_bound) {
+        l11 = l11 + A.chol_bound[0];
+        l21 = l21 + A.chol_bound[1];
+        l22 = l22 + A.chol_bound[2];
+    }
+    if (A.radii[i] > 0) {
+        const float4 r0 = A.rec[3 * i], r2 = A.rec[3 * i + 2];
+        const float X00 = r2.z, X01 = r0.w, X10 = X01, X11 = r2.w;
+        const float G00 = g0.z, G01 = g0.w, G10 = G01, G11 = g1.x;
+        const float N00 = -X00, N01 = -X01, N10 = -X10, N11 = -X11;
+        const float P00 = N00 * G00 + N10 * G01;
+        const float P01 = N01 * G00 + N11 * G01;
+        const float P10 = N00 * G10 + N10 * G11;
+        const float P11 = N01 * G10 + N11 * G11;
+        const float V00 = P00 * X00 + P10 * X01;
+        const float V01 = P01 * X00 + P11 * X01;
+        const float V10 = P00 * X10 + P10 * X11;
+        const float V11 = P01 * X10 + P11 * X11;
+        const float g11 = V00, g12 = V10 + V01, g22 = V11;
+        vl0 = 2.0f * l11 * g11 + 2.0f * g12 * l21;  // doubled cross term: backward2d.cu:39
+        vl1 = 2.0f * l11 * g12 + 2.0f * l21 * g22;
+        vl2 = 2.0f * l22 * g22;
+        vmx = g0.x * A.hw;
+        vmy = g0.y * A.hh;
+    }
+    // activations (GaussianSplats_Represent.py:57-70): tanh, + bound, * rgb_W
+    const float x0 = A.xyz[2 * i], x1 = A.xyz[2 * i + 1];
+    const float t0 = tanhf(x0), t1 = tanhf(x1);
+    const float dx0 = vmx * (1.0f - t0 * t0), dx1 = vmy * (1.0f - t1 * t1);
+    const float w = A.rgbw ? A.rgbw[i] : 1.0f;
+    const float f0 = A.feat[3 * i], f1 = A.feat[3 * i + 1], f2 = A.feat[3 * i + 2];
+    const float df0 = g1.y * w, df1 = g1.z * w, df2 = g1.w * w;
+    const float dw = (g1.y * f0 + g1.z * f1) + g1.w * f2;
+    if (!A.update) {
+        float *o = A.grads_out + 9 * (size_t)i;
+        o[0] = dx0;
+        o[1] = dx1;
+        o[2] = vl0;
+        o[3] = vl1;
+        o[4] = vl2;
+        o[5] = df0;
+        o[6] = df1;
+        o[7] = df2;
+        o[8] = A.rgbw_train ? dw : 0.0f;
+        return;
+    }
+    adan_at(A, 0, A.xyz, 2 * (size_t)i, dx0);
+    adan_at(A, 0, A.xyz, 2 * (size_t)i + 1, dx1);
+    adan_at(A, 1, A.chol, 3 * (size_t)i, vl0);
+    adan_at(A, 1, A.chol, 3 * (size_t)i + 1, vl1);
+    adan_at(A, 1, A.chol, 3 * (size_t)i + 2, vl2);
+    adan_at(A, 2, A.feat, 3 * (size_t)i, df0);
+    adan_at(A, 2, A.feat, 3 * (size_t)i + 1, df1);
+    adan_at(A, 2, A.feat, 3 * (size_t)i + 2, df2);
+    if (A.rgbw_train) adan_at(A, 3, A.rgbw, (size_t)i, dw);
+}
+
+struct TrainWs {
+    FrameWs f;
+    float4 *grad;
+    float2 *err;
+    size_t bytes;
+};
+
+static TrainWs train_ws(char *base, int n, int ntiles) {
+    TrainWs w;
+    w.f = frame_ws(base, n, ntiles);
+    size_t off = w.f.bytes;
+    const size_t nn = (size_t)(n > 0 ? n : 1), nt = (size_t)(ntiles > 0 ? ntiles : 1);
+    w.grad = (float4 *)(base ? base + off : nullptr);
+    off += ws_align(sizeof(float4) * 4 * nn);
+    w.err = (float2 *)(base ? base + off : nullptr);
+    off += ws_align(sizeof(float2) * nt);
+    w.bytes = off;
+    return w;
+}
+
+}  // namespace gsvc
+
+using namespace gsvc;
+
+extern "C" size_t gsvc_train_step_workspace_bytes(int num_points, unsigned img_height,
+                                                  unsigned img_width) {
+    return train_ws(nullptr, num_points, tiles_of(img_height, img_width)).bytes;
+}
+
+extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
+                                   const float *cholesky_bound, float *features, float *rgb_w,
+                                   int rgb_w_trainable, const float *background, const float *gt,
+                                   unsigned img_height, unsigned img_width, int loss_kind,
+                                   int frame_index, float *const *adan_state,
+                                   const double *adan_hparams, int adan_flags, float *loss,
+                                   float *render_out, float *grads_out, void *workspace,
+                                   size_t workspace_bytes, void *stream) {
+    if (num_points < 0 || img_height == 0 || img_width == 0)
+        return set_error(GSVC_ERR_ARG, "train_step_sum: bad sizes");
+    if (!xyz || !cholesky || !features || !background || !gt || !loss || !adan_hparams)
+        return set_error(GSVC_ERR_ARG, "train_step_sum: missing input");
+    if (loss_kind != 0 && loss_kind != 1)
+        return set_error(GSVC_ERR_ARG, "train_step_sum: loss_kind must be 0 (L2) or 1 (L1)");
+    if (rgb_w_trainable && !rgb_w)
+        return set_error(GSVC_ERR_ARG, "train_step_sum: trainable rgb_w needs rgb_w");
+    const bool update = grads_out == nullptr;
+    if (update) {
+        if (!adan_state) return set_error(GSVC_ERR_ARG, "train_step_sum: missing Adan state");
+        for (int q = 0; q < 4; ++q)
+            for (int k = 0; k < 4; ++k)
+                if (!adan_state[4 * q + k] && (q < 3 || rgb_w_trainable))
+                    return set_error(GSVC_ERR_ARG, "train_step_sum: missing Adan state tensor");
+    }
+    const int tbx = ceil_div((int)img_width, kTile), tby = ceil_div((int)img_height, kTile);
+    const int ntiles = tbx * tby;
+    const TrainWs w = train_ws((char *)workspace, num_points, ntiles);
+    if (!workspace || workspace_bytes < w.bytes)
+        return set_error(GSVC_ERR_WORKSPACE, "train_step_sum: workspace too small (%zu < %zu)",
+                         workspace_bytes, w.bytes);
+    hipStream_t s = (hipStream_t)stream;
+    const FrameSlots f = frame_slots(w.f, ntiles, frame_index);
+    int rc = frame_project_launch(num_points, xyz, 1, cholesky, cholesky_bound, features, rgb_w,
+                                  nullptr, img_height, img_width, w.f, f, w.grad, s);
+    if (rc) return rc;
+
+    const double count = 3.0 * (double)img_height * (double)img_width;  // numel of [3, H, W]
+    TrainTileArgs T{};
+    T.tbx = tbx;
+    T.img_w = (int)img_width;
+    T.img_h = (int)img_height;
+    T.ntiles = ntiles;
+    T.num_points = num_points;
+    T.loss_l1 = loss_kind;
+    T.norm = loss_kind ? 1.0f / (float)count : (float)(2.0 / count);
+    T.slab = w.f.slab;
+    T.counts = f.counts;
+    T.counts_clear = f.counts_next;
+    T.m_dev = f.m_acc;
+    T.xys = w.f.xys;
+    T.radii = w.f.radii;
+    T.rec = w.f.rec;
+    T.bg = background;
+    T.gt = gt;
+    T.grad = reinterpret_cast<float *>(w.grad);
+    T.err = w.err;
+    T.out = render_out;
+    hipLaunchKernelGGL(train_tile_kernel, dim3(ntiles), dim3(kT), 0, s, T);
+    rc = check_launch("train_step_sum: tiles");
+    if (rc) return rc;
+
+    TrainSplatArgs P{};
+    P.n = num_points;
+    P.ntiles = ntiles;
+    P.rgbw_train = rgb_w_trainable ? 1 : 0;
+    P.update = update ? 1 : 0;
+    P.hw = 0.5f * (float)img_width;
+    P.hh = 0.5f * (float)img_height;
+    P.inv_count = 1.0 / count;
+    P.xyz = xyz;
+    P.chol = cholesky;
+    P.feat = features;
+    P.rgbw = rgb_w;
+    P.chol_bound = cholesky_bound;
+    P.radii = w.f.radii;
+    P.rec = w.f.rec;
+    P.grad = w.grad;
+    if (update)
+        for (int q = 0; q < 4; ++q)
+            for (int k = 0; k < 4; ++k) P.state[q][k] = adan_state[4 * q + k];
+    for (int q = 0; q < 4; ++q) P.first[q] = (adan_flags >> (1 + q)) & 1;
+    const double *h = adan_hparams;
+    P.S = adan_scalars(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], adan_flags & 1, h[9]);
+    P.grads_out = grads_out;
+    P.err = w.err;
+    P.loss = loss;
+    const int blocks = num_points > 0 ? ceil_div(num_points, 256) : 1;
+    hipLaunchKernelGGL(train_splat_kernel, dim3(blocks), dim3(256), 0, s, P);
+    return check_launch("train_step_sum: splats");
+}

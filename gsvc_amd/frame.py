@@ -20,6 +20,7 @@ from .adan import Adan
 from .project_gaussians_2d import project_gaussians_2d
 from .rasterize_sum import rasterize_gaussians_sum
 from .render import render_frame_sum
+from .train import LOSS_KIND, train_step_sum
 
 
 def loss_fn(pred, target, loss_type="L2", lambda_value=0.7):
@@ -72,6 +73,9 @@ class GaussianVideoFrame(nn.Module):
         self.opt_type = kwargs["opt_type"]
         # the fused HIP Adan on GPU models (numerically the foreach update)
         self.fused_adan = kwargs.get("fused_adan", str(self.device).startswith("cuda"))
+        # whole train_iter as one fused call (gsvc_amd/train.py) where it applies
+        self.fused_train = kwargs.get("fused_train", str(self.device).startswith("cuda"))
+        self.fused_steps = 0
         self.update_optimizer()
         self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=20000, gamma=0.5)
 
@@ -189,7 +193,79 @@ class GaussianVideoFrame(nn.Module):
                 self._remove_lowest(sorted_indices, remove_count)
             self.update_optimizer()
 
+    def _fused_train_params(self, gt_image):
+        """(rgb_W trainable?) when this iteration can run as one fused step
+        (train.py): L2 / L1 loss, Adan without gradient clipping, the model's
+        own parameters in one group, no gradients pending; else None."""
+        if not self.fused_train or self.loss_type not in LOSS_KIND or self.opt_type == "adam":
+            return None
+        if self.BLOCK_H != 16 or self.BLOCK_W != 16 or not self._xyz.is_cuda:
+            return None
+        opt = self.optimizer
+        if not isinstance(opt, Adan) or len(opt.param_groups) != 1 or opt.defaults["max_grad_norm"] > 0:
+            return None
+        rgbw_train = isinstance(self.rgb_W, nn.Parameter) and self.rgb_W.requires_grad
+        params = [self._xyz, self._cholesky, self._features_dc] + ([self.rgb_W] if rgbw_train else [])
+        group = opt.param_groups[0]["params"]
+        if len(group) != len(params) or {id(p) for p in group} != {id(p) for p in params}:
+            return None
+        for p in params:
+            if (p.grad is not None or not p.requires_grad or p.dtype != torch.float32
+                    or not p.is_contiguous()):
+                return None
+        if gt_image.numel() != 3 * self.H * self.W or gt_image.device != self._xyz.device:
+            return None
+        return rgbw_train
+
+    def _train_iter_fused(self, gt_image, rgbw_train):
+        """train_iter (GaussianSplats_Represent.py:191-207) as one fused call:
+        forward, loss, backward and the Adan step of optimizer.py:124-235 with
+        this optimizer's state, step counter and learning rate."""
+        opt = self.optimizer
+        group = opt.param_groups[0]
+        group["step"] = group.get("step", 0) + 1
+        step = group["step"]
+        b1, b2, b3 = group["betas"]
+        hparams = [b1, b2, b3, 1.0 - b1 ** step, 1.0 - b2 ** step, math.sqrt(1.0 - b3 ** step),
+                   group["lr"], group["weight_decay"], group["eps"], 1.0]
+        flags = 1 if group["no_prox"] else 0
+        state = []
+        for q, p in enumerate((self._xyz, self._cholesky, self._features_dc,
+                               self.rgb_W if rgbw_train else None)):
+            if p is None:
+                state += [None] * 4
+                continue
+            st = opt.state[p]
+            if len(st) == 0:
+                st["exp_avg"] = torch.zeros_like(p)
+                st["exp_avg_sq"] = torch.zeros_like(p)
+                st["exp_avg_diff"] = torch.zeros_like(p)
+            if "neg_pre_grad" not in st or step == 1:
+                st["neg_pre_grad"] = torch.empty_like(p)  # the kernel starts it at -grad
+                flags |= 1 << (1 + q)
+            state += [st["exp_avg"], st["exp_avg_sq"], st["exp_avg_diff"], st["neg_pre_grad"]]
+        gt = gt_image.detach()
+        if gt.dtype != torch.float32 or not gt.is_contiguous():
+            gt = gt.float().contiguous()
+        losses = train_step_sum(self._xyz.data, self._cholesky.data, self._features_dc.data,
+                                self.rgb_W.data, rgbw_train, self.cholesky_bound, self.background,
+                                gt, self.H, self.W, self.loss_type, state, hparams, flags)
+        loss = losses[LOSS_KIND[self.loss_type]]
+        psnr = 10 * math.log10(1.0 / float(losses[0]))
+        # the step ran (keeps StepLR's call-order check quiet; the scheduler may
+        # hold the optimizer from before update_optimizer, as in the reference)
+        opt._opt_called = True
+        self.scheduler.optimizer._opt_called = True
+        self.fused_steps += 1
+        self.scheduler.step()
+        return loss, psnr
+
     def train_iter(self, gt_image, iter):
+        controls = (((iter == 1 or iter % self.densification_interval == 0) and self.isdensity)
+                    or (iter % self.densification_interval == 0 and self.isremoval))
+        rgbw_train = None if controls else self._fused_train_params(gt_image)
+        if rgbw_train is not None:
+            return self._train_iter_fused(gt_image, rgbw_train)
         render_pkg = self.forward()
         image = render_pkg["render"]
         loss = loss_fn(image.squeeze(0), gt_image.squeeze(0), self.loss_type, lambda_value=0)
@@ -209,7 +285,7 @@ class GaussianVideoFrame(nn.Module):
 
 def make_frame_model(H, W, num_points, device, seed=None, lr=1e-3, isremoval=False,
                      isdensity=False, removal_rate=0.1, max_num_points=None,
-                     densification_interval=100, fused_adan=None):
+                     densification_interval=100, fused_adan=None, fused_train=None):
     """Construct like SimpleTrainer2d does (train_video_Represent.py:51-55)."""
     if seed is not None:
         torch.manual_seed(seed)
@@ -218,7 +294,8 @@ def make_frame_model(H, W, num_points, device, seed=None, lr=1e-3, isremoval=Fal
         max_num_points=max_num_points or num_points, densification_interval=densification_interval,
         iterations=30000, H=H, W=W, BLOCK_H=16, BLOCK_W=16, device=device, lr=lr, quantize=False,
         removal_rate=removal_rate, isdensity=isdensity, isremoval=isremoval,
-        **({} if fused_adan is None else {"fused_adan": fused_adan})).to(device)
+        **({} if fused_adan is None else {"fused_adan": fused_adan}),
+        **({} if fused_train is None else {"fused_train": fused_train})).to(device)
     return model
 
 

@@ -244,6 +244,44 @@ int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_tanh,
                           int density_hint, int *meta, void *workspace,
                           size_t workspace_bytes, float *out, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * Fused training step of GSVC's per-frame model: one
+ * GaussianVideo_frame.train_iter (GaussianSplats_Represent.py:191-207) with
+ * the L2 (loss_kind 0, F.mse_loss) or L1 (loss_kind 1, F.l1_loss) loss and
+ * Adan (optimizer.py:124-235, 296-362), in three kernels, no host sync:
+ *   forward  means2d = tanh(xyz), L = cholesky + cholesky_bound (if given),
+ *            colors = features * rgb_w (if given), opacity 1; the sum
+ *            rasterizer; clamp(0, 1) -- the same image bits as
+ *            gsvc_render_frame_sum (render_out [3,H,W], optional);
+ *   loss     against gt [3,H,W]; loss[0] <- mean squared error (the PSNR's
+ *            MSE), loss[1] <- mean absolute error;
+ *   backward through clamp, rasterizer, projection (doubled L cross term,
+ *            backward2d.cu:39-41) and the activations;
+ *   Adan     every element of xyz [N,2], cholesky [N,3], features [N,3] and,
+ *            when rgb_w_trainable, rgb_w [N] is updated in place.
+ * adan_state: host array of 16 device pointers, per parameter (xyz,
+ * cholesky, features, rgb_w) its {exp_avg, exp_avg_sq, exp_avg_diff,
+ * neg_pre_grad} (rgb_w's may be NULL when not trainable).  adan_hparams: host
+ * double[10] = {beta1, beta2, beta3, bias_correction1, bias_correction2,
+ * sqrt(bias_correction3), lr, weight_decay, eps, clip_global_grad_norm}.
+ * adan_flags: bit 0 no_prox; bit 1 + q: parameter q takes its first step
+ * (neg_pre_grad starts from -grad, optimizer.py:187-189).
+ * grads_out (test hook): when non-NULL nothing is updated and the parameter
+ * gradients go to grads_out [N,9] = {d_xyz 2, d_cholesky 3, d_features 3,
+ * d_rgb_w 1}.  Workspace: gsvc_train_step_workspace_bytes; its first
+ * gsvc_render_frame_zeroed_bytes(H, W) bytes zero before the first call (every
+ * call leaves them zero); frame_index alternates parity between calls. */
+size_t gsvc_train_step_workspace_bytes(int num_points, unsigned img_height,
+                                       unsigned img_width);
+int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
+                        const float *cholesky_bound, float *features, float *rgb_w,
+                        int rgb_w_trainable, const float *background, const float *gt,
+                        unsigned img_height, unsigned img_width, int loss_kind,
+                        int frame_index, float *const *adan_state,
+                        const double *adan_hparams, int adan_flags, float *loss,
+                        float *render_out, float *grads_out, void *workspace,
+                        size_t workspace_bytes, void *stream);
+
 /* Replaces _C.rasterize_sum_backward (bindings.cu:706-779 -> backward.cu:696-862).
  * Gradients are written into one 64-byte record per splat,
  * grad_records [N,16] float: [0:2] v_xy, [2:5] v_conic, [5:8] v_colors,
