@@ -152,7 +152,10 @@ def secondary(device, steps=50, warmup=10):
     return {"workload": "1920x1080, 50000 splats (BASELINE configs[2])",
             "train_iters_per_s": 1.0 / t_train, "train_ms_per_iter": 1e3 * t_train,
             "render_fps": 1.0 / t_render, "psnr_after_iters": psnr,
-            "train_iter": "forward + L2 + backward + PSNR .item() + Adan + zero_grad + StepLR"}
+            "train_iter": "forward + L2 + backward + PSNR .item() + Adan + zero_grad + StepLR",
+            "train_iter_path": ("fused: gsvc_train_step_sum (projection+slabs, per-tile "
+                                "forward/loss/backward, per-splat VJP+Adan)"
+                                if model.fused_steps else "op by op")}
 
 
 def main():

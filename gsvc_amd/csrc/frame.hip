@@ -31,14 +31,18 @@
 
 namespace gsvc {
 
-// Append splat i's record to the slab of every tile of its bbox; the slot
-// atomics are issued in batches of 8 before their results are waited for.
-__device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, int tby,
+// Append splat i's record to the slab of tiles sub, sub + K, ... of its bbox
+// (row-major), one of the K lanes of the splat; the slot atomics are issued in
+// batches of 8 before their results are waited for.
+template <int K>
+__device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, int tby, int sub,
                                            float4 r0, float4 r1, float4 r2,
                                            unsigned *__restrict__ counts,
                                            float4 *__restrict__ slab) {
     unsigned x0, y0, x1, y1;
     tile_bbox(cx, cy, (float)r, tbx, tby, x0, y0, x1, y1);
+    if (x1 <= x0 || y1 <= y0) return 0;
+    const unsigned bw = x1 - x0;
     constexpr int kBatch = 8;
     unsigned tl[kBatch];
     int cnt = 0, hits = 0;
@@ -58,16 +62,25 @@ __device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, i
         hits += cnt;
         cnt = 0;
     };
-    for (unsigned y = y0; y < y1; ++y)
-        for (unsigned x = x0; x < x1; ++x) {
-            tl[cnt < kBatch ? cnt : 0] = y * (unsigned)tbx + x;
-            if (++cnt == kBatch) flush();
+    unsigned y = y0 + (unsigned)sub / bw, x = x0 + (unsigned)sub % bw;
+    while (y < y1) {
+        tl[cnt < kBatch ? cnt : 0] = y * (unsigned)tbx + x;
+        if (++cnt == kBatch) flush();
+        x += K;
+        while (x >= x1) {
+            x -= bw;
+            ++y;
         }
+    }
     if (cnt) flush();
     return hits;
 }
 
+// K lanes per splat: each computes the (cheap) projection, lane s writes part
+// of the splat's outputs and inserts every K-th tile of its bbox (K = 1 in
+// production: more lanes did not shorten the insertion, see the launcher).
 constexpr int kProjThreads = 256;
+template <int K>
 __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
     int n, const float *__restrict__ xyz, int xyz_tanh, const float *__restrict__ chol,
     const float *__restrict__ chol_bound, const float *__restrict__ feat,
@@ -76,7 +89,8 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
     unsigned *__restrict__ counts, float4 *__restrict__ slab, int *__restrict__ m_acc,
     int *__restrict__ m_clear, float4 *__restrict__ grad_zero) {
     __shared__ int s_hits[kProjThreads / 64];
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = t / K, sub = t % K;
     if (blockIdx.x == 0 && threadIdx.x == 0) *m_clear = 0;  // the next frame's slot
     int hits = 0;
     if (i < n) {
@@ -100,32 +114,31 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
         }
         const float o = opac ? opac[i] : 1.0f;
         const SplatProj P = project_splat(mx, my, l11, l21, l22, hw, hh, tbx, tby);
-        xys[i] = P.xy;
-        radii[i] = P.rad;
         const float4 r0 = make_float4(P.xy.x, P.xy.y, 0.5f * P.c0, P.c1);
         const float4 r1 = make_float4(0.5f * P.c2, o, r, g);
         const float4 r2 = make_float4(b, __int_as_float(i), P.c0, P.c2);
-        rec[3 * i] = r0;
-        rec[3 * i + 1] = r1;
-        rec[3 * i + 2] = r2;
-        if (grad_zero) {
-            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-            grad_zero[4 * i] = z;
-            grad_zero[4 * i + 1] = z;
-            grad_zero[4 * i + 2] = z;
-            grad_zero[4 * i + 3] = z;
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = sub; q < 4; q += K) {
+            if (q < 3) rec[3 * i + q] = q == 0 ? r0 : (q == 1 ? r1 : r2);
+            if (q == 3) {
+                xys[i] = P.xy;
+                radii[i] = P.rad;
+            }
+            if (grad_zero) grad_zero[4 * i + q] = z;
         }
-        if (P.rad > 0) hits = slab_insert(P.xy.x, P.xy.y, P.rad, tbx, tby, r0, r1, r2, counts, slab);
+        if (P.rad > 0)
+            hits = slab_insert<K>(P.xy.x, P.xy.y, P.rad, tbx, tby, sub, r0, r1, r2, counts, slab);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) hits += __shfl_xor(hits, off, 64);
     if ((threadIdx.x & 63) == 0) s_hits[threadIdx.x >> 6] = hits;
     __syncthreads();
     if (threadIdx.x == 0) {
-        int t = 0;
+        int tot = 0;
 #pragma unroll
-        for (int k = 0; k < kProjThreads / 64; ++k) t += s_hits[k];
-        if (t) atomicAdd(m_acc, t);
+        for (int k = 0; k < kProjThreads / 64; ++k) tot += s_hits[k];
+        if (tot) atomicAdd(m_acc, tot);
     }
 }
 
@@ -167,12 +180,23 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
                          const FrameSlots &f, float4 *grad_zero, hipStream_t s) {
     const int tbx = ceil_div((int)img_w, kTile), tby = ceil_div((int)img_h, kTile);
     const float hw = 0.5f * (float)img_w, hh = 0.5f * (float)img_h;
-    if (n > 0)
-        hipLaunchKernelGGL(frame_project_kernel, dim3(ceil_div(n, kProjThreads)), dim3(kProjThreads),
-                           0, s, n, xyz, xyz_tanh, chol, chol_bound, feat, rgb_w, opac, hw, hh, tbx,
-                           tby, w.xys, w.radii, w.rec, f.counts, w.slab, f.m_acc, f.m_clear,
-                           grad_zero);
-    else if (hipMemsetAsync(f.m_acc, 0, sizeof(int), s) != hipSuccess)
+    // lanes per splat: 1 unless gsvc_debug_set(4, k) picks 2, 4 or 8 (A/B knob;
+    // measured at 1080p: equal at 10k splats, 1 lane fastest at 50k)
+    const int k = g_knobs[4] == 2 || g_knobs[4] == 4 || g_knobs[4] == 8 ? g_knobs[4] : 1;
+    if (n > 0) {
+        const dim3 grid(ceil_div(n, kProjThreads / k));
+#define GSVC_FRAME_PROJECT(K)                                                                    \
+    hipLaunchKernelGGL(frame_project_kernel<K>, grid, dim3(kProjThreads), 0, s, n, xyz, xyz_tanh, \
+                       chol, chol_bound, feat, rgb_w, opac, hw, hh, tbx, tby, w.xys, w.radii,     \
+                       w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero)
+        switch (k) {
+            case 2: GSVC_FRAME_PROJECT(2); break;
+            case 8: GSVC_FRAME_PROJECT(8); break;
+            case 4: GSVC_FRAME_PROJECT(4); break;
+            default: GSVC_FRAME_PROJECT(1); break;
+        }
+#undef GSVC_FRAME_PROJECT
+    } else if (hipMemsetAsync(f.m_acc, 0, sizeof(int), s) != hipSuccess)
         return set_error(GSVC_ERR_HIP, "frame projection: memset failed");
     return check_launch("frame projection");
 }

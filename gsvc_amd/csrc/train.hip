@@ -54,6 +54,31 @@ __device__ __forceinline__ float clamp_unit(float x) {
     return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x);
 }
 
+// Rows of the 16x16 tile at (tx0, ty0) on which splat (x, y, conic a b c,
+// opacity o) can reach alpha >= 1/255 at some pixel centre (bit r = row r);
+// 0 only when provably none.  alpha >= 1/255 needs sigma <= ln(255 o), i.e.
+// d^T C d <= 2 ln(255 o), an ellipse with half-extents sqrt(2 ln(255 o) c / det)
+// and sqrt(2 ln(255 o) a / det); the margins (0.1 % + 0.01 px) dwarf fp32
+// rounding (the banded forward's test, raster_sum.hip ellipse_hits_rect).  A
+// culled (entry, pixel) pair contributes nothing in the reference either.
+__device__ __forceinline__ unsigned ellipse_rows(float x, float y, float a, float b, float c,
+                                                 float o, float tx0, float ty0) {
+    if (!(o > 0.0f)) return (o <= 0.0f) ? 0u : 0xffffu;  // o <= 0: alpha never valid; NaN: keep
+    const float det = a * c - b * b;
+    if (!(a > 0.0f) || !(det > 0.0f) || !(o < 3.0e38f) || !(fabsf(x) < 1e30f) || !(fabsf(y) < 1e30f))
+        return 0xffffu;  // not positive definite / non-finite: no culling
+    const float lg = __logf(255.0f * o);
+    if (lg < -0.01f) return 0u;  // o < e^-0.01 / 255: alpha < 1/255 everywhere
+    const float S2 = 2.0f * (lg * 1.001f + 0.01f);
+    const float ex = sqrtf(S2 * c / det) * 1.001f + 0.01f;
+    const float ey = sqrtf(S2 * a / det) * 1.001f + 0.01f;
+    if (x + ex < tx0 || x - ex > tx0 + 15.0f) return 0u;
+    const float lo = fmaxf(ceilf(y - ey - ty0), 0.0f), hi = fminf(floorf(y + ey - ty0), 15.0f);
+    if (!(lo <= hi)) return 0u;
+    const unsigned l = (unsigned)lo, h = (unsigned)hi;
+    return ((2u << h) - 1u) & ~((1u << l) - 1u);
+}
+
 __device__ __forceinline__ int ceil_log2_i(int n) { return n <= 1 ? 0 : 32 - __clz(n - 1); }
 
 // The first <= 256 ids (ascending) of the splats whose bbox covers tile
@@ -90,25 +115,37 @@ __device__ int block_brute_ids(const TrainTileArgs &A, int tx, int ty, int *s_gi
 }
 
 __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
-    __shared__ float4 s_geo[kT];  // x, y, a/2, b
-    __shared__ float4 s_col[kT];  // c/2, opacity, r, g
-    __shared__ float4 s_ext[kT];  // b, id bits, a, c
-    __shared__ float4 s_pix[kT];  // v_out rgb, last contributing entry (bits; -1 outside)
-    __shared__ float s_red[9][kT];
+    // LDS: geo / col / pix, reused as the 9 x 256 gradient reduction buffer
+    // once the backward loop is done (16.5 KB per workgroup)
+    __shared__ float4 s_buf[3 * kT];
+    __shared__ float4 s_ext[kT];     // b, id bits, a, c
+    __shared__ unsigned s_rows[kT];  // rows of the tile the entry can reach
     __shared__ int s_cnt[4];
     __shared__ float s_err[2][4];
+    float4 *s_geo = s_buf;           // x, y, a/2, b
+    float4 *s_col = s_buf + kT;      // c/2, opacity, r, g
+    float4 *s_pix = s_buf + 2 * kT;  // v_out rgb, last contributing entry (bits; -1 outside)
+    float(*s_red)[kT] = reinterpret_cast<float(*)[kT]>(s_buf);
+    int *s_ids = reinterpret_cast<int *>(s_pix);  // unsorted ids while staging
     const int tile = xcd_remap(blockIdx.x, A.ntiles);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int ty = tile / A.tbx, tx = tile - ty * A.tbx;
+    const int pi = ty * kTile + (tid >> 4), pj = tx * kTile + (tid & 15);
+    const bool inside = pi < A.img_h && pj < A.img_w;
+    const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
+    // this pixel's target, loaded first: its latency overlaps the staging
+    const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
+    const size_t pix = inside ? (size_t)pi * (size_t)A.img_w + (size_t)pj : 0;
+    const float gt0 = A.gt[pix], gt1 = A.gt[hw + pix], gt2 = A.gt[2 * hw + pix];
     const bool empty = *A.m_dev < 1;  // rasterize_sum.py:121-127: background, no gradient
     const int n_all = empty ? 0 : (int)A.counts[tile];
     if (tid == 0) A.counts_clear[tile] = 0u;  // the next frame's counts
 
     // 1. the tile's first <= 256 entries in (tile, splat id) order into LDS
     int n;
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+    int rank = tid;
     if (n_all <= kT) {
-        int *ids = reinterpret_cast<int *>(s_red[0]);
-        float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
         int id = 0x7fffffff;
         if (tid < n_all) {
             const float4 *r = A.slab + ((size_t)tile * kT + tid) * 3;
@@ -117,31 +154,32 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
             r2 = r[2];
             id = __float_as_int(r2.y);
         }
-        ids[tid] = id;
+        s_ids[tid] = id;
         __syncthreads();
         if (tid < n_all) {
-            int rank = 0;
-            for (int j = 0; j < n_all; ++j) rank += ids[j] < id ? 1 : 0;  // ids are unique
-            s_geo[rank] = r0;
-            s_col[rank] = r1;
-            s_ext[rank] = r2;
+            rank = 0;
+            for (int j = 0; j < n_all; ++j) rank += s_ids[j] < id ? 1 : 0;  // ids are unique
         }
         n = n_all;
     } else {
-        int *ids = reinterpret_cast<int *>(s_red[0]);
-        n = block_brute_ids(A, tx, ty, ids, s_cnt);
+        n = block_brute_ids(A, tx, ty, s_ids, s_cnt);
         if (tid < n) {
-            const int g = ids[tid];
-            s_geo[tid] = A.rec[3 * g];
-            s_col[tid] = A.rec[3 * g + 1];
-            s_ext[tid] = A.rec[3 * g + 2];
+            const int g = s_ids[tid];
+            r0 = A.rec[3 * g];
+            r1 = A.rec[3 * g + 1];
+            r2 = A.rec[3 * g + 2];
         }
+    }
+    __syncthreads();  // s_ids (in s_pix) read
+    if (tid < n) {
+        s_geo[rank] = r0;
+        s_col[rank] = r1;
+        s_ext[rank] = r2;
+        s_rows[rank] = ellipse_rows(r0.x, r0.y, r2.z, r0.w, r2.w, r1.y, tx0, ty0);
     }
     __syncthreads();
 
     // 2. pixel-parallel forward (the sum rasterizer's op sequence), clamp, loss
-    const int pi = ty * kTile + (tid >> 4), pj = tx * kTile + (tid & 15);
-    const bool inside = pi < A.img_h && pj < A.img_w;
     float o[3] = {0.f, 0.f, 0.f};
     if (empty) {
         o[0] = A.bg[0];
@@ -152,6 +190,7 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
     {
         const float py = (float)pi, px = (float)pj;
         for (int k = 0; k < n; ++k) {
+            if (!((s_rows[k] >> (4 * w)) & 0xfu)) continue;  // no row of this wave reachable
             const float4 G = s_geo[k];
             const float4 C = s_col[k];
             const float dy = G.y - py;
@@ -168,23 +207,23 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
             }
         }
     }
-    float v[3] = {0.f, 0.f, 0.f}, se = 0.f, ae = 0.f;
-    if (inside) {
-        const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
-        const size_t p = (size_t)pi * (size_t)A.img_w + (size_t)pj;
+    float v[3], se = 0.f, ae = 0.f;
+    {
+        const float gtv[3] = {gt0, gt1, gt2};
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             const float x = clamp_unit(o[c]);
-            const float d = x - A.gt[c * hw + p];
+            const float d = x - gtv[c];
             se = fmaf(d, d, se);
             ae += fabsf(d);
             // mse_loss backward: norm * (a - b) * 1; l1: (1 / numel) * sgn(a - b);
             // clamp backward passes where 0 <= out <= 1
             const float sg = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
             const float gv = A.loss_l1 ? A.norm * sg : A.norm * d;
-            v[c] = (o[c] >= 0.0f && o[c] <= 1.0f) ? gv : 0.0f;
-            if (A.out) A.out[c * hw + p] = x;
+            v[c] = (inside && o[c] >= 0.0f && o[c] <= 1.0f) ? gv : 0.0f;
+            if (A.out && inside) A.out[c * hw + pix] = x;
         }
+        if (!inside) se = ae = 0.0f;
     }
     s_pix[tid] = make_float4(v[0], v[1], v[2], __int_as_float(inside ? last : -1));
     int f = inside ? last : -1;
@@ -214,10 +253,13 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
     const int E = 1 << lg;
     const int e = tid & (E - 1);
     const int p_begin = (tid >> lg) << lg;
-    const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
     float a_r = 0.f, a_g = 0.f, a_b = 0.f, a_c0 = 0.f, a_c1 = 0.f, a_c2 = 0.f;
     float a_x = 0.f, a_y = 0.f, a_o = 0.f;
-    if (e < kend) {
+    // rows of this thread's pixel group; skip an entry that reaches none
+    const unsigned grp_rows = E >= kTile ? (((2u << ((p_begin + E - 1) >> 4)) - 1u) &
+                                            ~((1u << (p_begin >> 4)) - 1u))
+                                         : (1u << (p_begin >> 4));
+    if (e < kend && (s_rows[e] & grp_rows)) {
         const float4 G = s_geo[e];
         const float4 C = s_col[e];
         const float4 X = s_ext[e];
@@ -260,6 +302,7 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
         }
     }
     const int S = E < 64 ? 64 : E;
+    __syncthreads();  // s_geo / s_col / s_pix read: the buffer becomes s_red
     if (E >= 64 || lane < E) {
         s_red[0][tid] = a_x;
         s_red[1][tid] = a_y;
@@ -306,17 +349,6 @@ struct TrainSplatArgs {
     const float2 *err;
     float *loss;         // [2]: mean squared error, mean absolute error
 };
-
-__device__ __forceinline__ void adan_at(const TrainSplatArgs &A, int q, float *param, size_t j,
-                                        float g) {
-    float m = A.state[q][0][j], v = A.state[q][1][j], df = A.state[q][2][j];
-    float npg = A.first[q] ? -(g * A.S.clip) : A.state[q][3][j];
-    param[j] = adan_update(A.S, param[j], g, m, v, df, npg);
-    A.state[q][0][j] = m;
-    A.state[q][1][j] = v;
-    A.state[q][2][j] = df;
-    A.state[q][3][j] = npg;
-}
 
 __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
     if (blockIdx.x == 0) {
@@ -396,15 +428,43 @@ __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
         o[8] = A.rgbw_train ? dw : 0.0f;
         return;
     }
-    adan_at(A, 0, A.xyz, 2 * (size_t)i, dx0);
-    adan_at(A, 0, A.xyz, 2 * (size_t)i + 1, dx1);
-    adan_at(A, 1, A.chol, 3 * (size_t)i, vl0);
-    adan_at(A, 1, A.chol, 3 * (size_t)i + 1, vl1);
-    adan_at(A, 1, A.chol, 3 * (size_t)i + 2, vl2);
-    adan_at(A, 2, A.feat, 3 * (size_t)i, df0);
-    adan_at(A, 2, A.feat, 3 * (size_t)i + 1, df1);
-    adan_at(A, 2, A.feat, 3 * (size_t)i + 2, df2);
-    if (A.rgbw_train) adan_at(A, 3, A.rgbw, (size_t)i, dw);
+    // Adan on the 8 (9 with rgb_W) elements of this splat.  Every operand is
+    // loaded before the first store: the state pointers may alias as far as
+    // the compiler knows, so interleaving would serialise nine round trips.
+    const float g[9] = {dx0, dx1, vl0, vl1, vl2, df0, df1, df2, dw};
+    float pv[9], m[9], v[9], df[9], npg[9];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+        const int q = e < 2 ? 0 : (e < 5 ? 1 : (e < 8 ? 2 : 3));
+        if (q == 3 && !A.rgbw_train) continue;
+        const size_t j = q == 0 ? 2 * (size_t)i + e : (q == 1 ? 3 * (size_t)i + (e - 2)
+                                                  : (q == 2 ? 3 * (size_t)i + (e - 5) : (size_t)i));
+        float *param = q == 0 ? A.xyz : (q == 1 ? A.chol : (q == 2 ? A.feat : A.rgbw));
+        pv[e] = param[j];
+        m[e] = A.state[q][0][j];
+        v[e] = A.state[q][1][j];
+        df[e] = A.state[q][2][j];
+        npg[e] = A.first[q] ? -(g[e] * A.S.clip) : A.state[q][3][j];
+    }
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+        const int q = e < 2 ? 0 : (e < 5 ? 1 : (e < 8 ? 2 : 3));
+        if (q == 3 && !A.rgbw_train) continue;
+        pv[e] = adan_update(A.S, pv[e], g[e], m[e], v[e], df[e], npg[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+        const int q = e < 2 ? 0 : (e < 5 ? 1 : (e < 8 ? 2 : 3));
+        if (q == 3 && !A.rgbw_train) continue;
+        const size_t j = q == 0 ? 2 * (size_t)i + e : (q == 1 ? 3 * (size_t)i + (e - 2)
+                                                  : (q == 2 ? 3 * (size_t)i + (e - 5) : (size_t)i));
+        float *param = q == 0 ? A.xyz : (q == 1 ? A.chol : (q == 2 ? A.feat : A.rgbw));
+        param[j] = pv[e];
+        A.state[q][0][j] = m[e];
+        A.state[q][1][j] = v[e];
+        A.state[q][2][j] = df[e];
+        A.state[q][3][j] = npg[e];
+    }
 }
 
 struct TrainWs {

@@ -23,7 +23,10 @@ import os
 from collections import defaultdict
 
 KERNELS = {"raster_sum_fwd_kernel": "rasterize_sum_forward",
-           "raster_sum_bwd_kernel": "rasterize_sum_backward"}
+           "raster_sum_bwd_kernel": "rasterize_sum_backward",
+           "train_tile_kernel": "train_tile",
+           "train_splat_kernel": "train_splat",
+           "frame_project_kernel": "frame_project"}
 
 
 def _short(name):
@@ -65,6 +68,20 @@ def pmc_per_launch(d, counter):
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
+def pmc_all(dirs):
+    """{kernel: {counter: average per dispatch}} over every counter in the
+    --pmc pass directories ``dirs``."""
+    vals = defaultdict(lambda: defaultdict(list))
+    for d in dirs:
+        for f in _csvs(d, "*counter_collection.csv"):
+            with open(f) as fh:
+                for r in csv.DictReader(fh):
+                    k = _short(r["Kernel_Name"])
+                    if k:
+                        vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in vals.items()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--trace")
@@ -72,7 +89,10 @@ def main():
     ap.add_argument("--write")
     ap.add_argument("--out")
     ap.add_argument("--key", default="10000")
+    ap.add_argument("--pmc-dirs", nargs="*", help="print every counter per kernel")
     a = ap.parse_args()
+    if a.pmc_dirs:
+        print(json.dumps(pmc_all(a.pmc_dirs), indent=1))
     if a.trace:
         st = trace_stats(a.trace)
         for name, s in sorted(st.items(), key=lambda kv: -kv[1]["avg_us"] * kv[1]["calls"]):
