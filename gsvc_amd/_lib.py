@@ -56,6 +56,7 @@ _SIGS = {
     "gsvc_train_step_workspace_bytes": [_I, _U, _U],
     "gsvc_train_step_sum": [_I, _P, _P, _P, _P, _P, _I, _P, _P, _U, _U, _I, _I, _P, _P, _I, _P, _P,
                             _P, _P, _SZ, _P],
+    "gsvc_i420_to_rgb": [_P, _I, _I, _P, _P],
     "gsvc_adan_step": [_I, _P, _P, _P, _P, _P, _P, _P] + [ctypes.c_double] * 9 +
                       [_I, ctypes.c_double, _P],
     "gsvc_rasterize_sum_backward": [_U, _U, _U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,

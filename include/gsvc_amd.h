@@ -318,6 +318,13 @@ int gsvc_rasterize_backward(
     const int *final_idx, const float *v_output, const float *v_output_alpha,
     float *grad_records, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * Video input (utils.py:134-156 process_yuv_video + ToTensor,
+ * train_video_Represent.py:204-207): one planar I420 frame (Y H*W bytes, then
+ * U and V (H/2)*(W/2) each, device memory) to out [3,H,W] float RGB / 255 with
+ * OpenCV's COLOR_YUV2RGB_I420 fixed-point BT.601 arithmetic.  H, W even. */
+int gsvc_i420_to_rgb(const unsigned char *yuv, int height, int width, float *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -242,3 +242,24 @@ def synthetic_frame(n: int, seed: int, rgb_w: float = 1.0, chol_scale: float = 1
     colors = (rng.random((n, 3), dtype=np.float32) * np.float32(rgb_w)).astype(F32)
     opac = np.ones((n, 1), F32)
     return means, chol, colors, opac
+
+
+def i420_to_rgb(yuv: np.ndarray, h: int, w: int) -> np.ndarray:
+    """OpenCV's COLOR_YUV2RGB_I420 (fixed-point ITU-R BT.601, 20-bit, as in
+    utils.py:153 ``cv2.cvtColor``) then ToTensor's / 255: [3, h, w] float32.
+    Restated from OpenCV's published constants; cv2 itself is absent here, so
+    this is parity-unpinned against it."""
+    CY, CUB, CUG, CVG, CVR, SH = 1220542, 2116026, -409993, -852492, 1673527, 20
+    yuv = np.asarray(yuv, np.uint8).reshape(-1)
+    Y = yuv[: h * w].reshape(h, w).astype(np.int64)
+    U = yuv[h * w: h * w + (h // 2) * (w // 2)].reshape(h // 2, w // 2).astype(np.int64) - 128
+    V = yuv[h * w + (h // 2) * (w // 2):].reshape(h // 2, w // 2).astype(np.int64) - 128
+    U = np.repeat(np.repeat(U, 2, 0), 2, 1)
+    V = np.repeat(np.repeat(V, 2, 0), 2, 1)
+    y = np.maximum(0, Y - 16) * CY
+    half = 1 << (SH - 1)
+    r = (y + half + CVR * V) >> SH
+    g = (y + half + CVG * V + CUG * U) >> SH
+    b = (y + half + CUB * U) >> SH
+    rgb = np.clip(np.stack([r, g, b]), 0, 255).astype(np.float32)
+    return (rgb / np.float32(255.0)).astype(np.float32)

@@ -1,0 +1,177 @@
+"""The video driver (gsvc_amd/video.py, restating train_video_Represent.py):
+
+CPU: the reference helpers against fixtures the reference's own utils.py
+produced (tests/golden/make_video_golden.py); the I420 oracle's known values;
+the GOP-sharded per-frame loop at world size 2 over gloo (a stub trainer in
+place of the GPU one) -- K-frames from scratch, P-frames from the previous
+frame's model, one all_reduce of the metrics.
+GPU: the I420 kernel against the oracle (bit-exact) and a small synthetic
+video end to end through the real trainer.
+"""
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO, load_golden
+
+
+def test_outlier_detector_and_early_stopping_match_reference():
+    from gsvc_amd.video import EarlyStopping, detect_outliers_mean_diff
+    z = load_golden("video_helpers")
+    for case in range(6):
+        got = detect_outliers_mean_diff(list(z[f"outliers_in_{case}"]))
+        assert got == z[f"outliers_out_{case}"].tolist(), case
+    for case in range(4):
+        es = EarlyStopping(patience=100, min_delta=1e-9)
+        stop = -1
+        for i, v in enumerate(z[f"early_in_{case}"]):
+            if es(float(v)):
+                stop = i
+                break
+        assert stop == int(z[f"early_stop_{case}"]), case
+
+
+def test_i420_oracle_known_values(oracle):
+    h, w = 2, 4
+    # black, white, and the BT.601 limits: Y 16 -> 0, Y 235 -> 255 with neutral chroma
+    y = np.array([[16, 235, 16, 235], [100, 100, 100, 100]], np.uint8)
+    u = np.array([[128, 128]], np.uint8)
+    v = np.array([[128, 128]], np.uint8)
+    rgb = oracle.i420_to_rgb(np.concatenate([y.ravel(), u.ravel(), v.ravel()]), h, w)
+    assert rgb.shape == (3, h, w)
+    np.testing.assert_array_equal(rgb[:, 0, 0], [0, 0, 0])
+    np.testing.assert_array_equal(rgb[:, 0, 1], [1, 1, 1])
+    assert np.all(rgb[:, 1, 0] == rgb[0, 1, 0])  # grey stays grey
+    # strong V (red) saturates red and lowers green
+    rgb2 = oracle.i420_to_rgb(np.concatenate([np.full(8, 128, np.uint8), [128, 128],
+                                              [255, 255]]).astype(np.uint8), h, w)
+    assert rgb2[0, 0, 0] == 1.0 and rgb2[1, 0, 0] < rgb2[2, 0, 0] < rgb2[0, 0, 0]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class _Args:
+    num_points = 100
+    iterations = 5
+    lr = 1e-3
+    loss_type = "L2"
+    densification_interval = 100
+    removal_rate = 0.1
+    is_rm = True
+    is_ad = True
+    backend = "gloo"
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, REPO)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import gsvc_amd.video as V
+
+        calls = []
+
+        class StubTrainer:
+            def __init__(self, image, frame_num, loss_type, num_points, max_num_points, iterations,
+                         lr, densification_interval=100, trained_model=None, isdensity=False,
+                         isremoval=True, removal_rate=0.25):
+                self.f = frame_num
+                self.parent = None if trained_model is None else int(trained_model["frame"])
+                calls.append(dict(frame=frame_num, parent=self.parent, isdensity=isdensity,
+                                  isremoval=isremoval, num_points=num_points))
+
+            def train(self):
+                return dict(psnr=30.0 + self.f, ms_ssim=float("nan"), training_time=1.0,
+                            eval_time=0.001, eval_fps=1000.0, num_gaussians=100 + self.f,
+                            loss=0.01, iterations=5,
+                            model={"frame": torch.tensor(self.f)})
+
+        V.FrameTrainer = StubTrainer
+        frames = 12
+        k = sorted({1, 5, 9} | set(V.forced_k_frames(frames, world)))
+        res = V.train_video(lambda i: torch.zeros(1, 3, 4, 4), frames, k, _Args(), rank, world,
+                            torch.device("cpu"))
+        q.put((rank, calls, res["average"], res["gops"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_video_loop_world2_gops_and_allreduce():
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    frames_seen = []
+    for rank, calls, avg, gops in res:
+        assert avg["frames"] == 12
+        assert avg["psnr"] == pytest.approx(30.0 + 6.5)  # mean over all 12 frames of both ranks
+        for c in calls:
+            frames_seen.append(c["frame"])
+            start = max(s for s, e in gops if s <= c["frame"])
+            if c["frame"] == start:  # K-frame: scratch, pruning (is_rm), no densify
+                assert c["parent"] is None and c["isremoval"] and not c["isdensity"]
+                assert c["num_points"] == 100
+            else:  # P-frame: previous frame's model, densify (is_ad)
+                assert c["parent"] == c["frame"] - 1 and c["isdensity"]
+                assert c["num_points"] == 100 + c["frame"] - 1
+    assert sorted(frames_seen) == list(range(1, 13))
+    assert res[0][3][0][0] == 1 and res[1][3][0][0] == 7  # forced K-frame at the shard boundary
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("h,w", [(2, 2), (64, 96), (1080, 1920)])
+def test_i420_kernel_matches_oracle(cuda, oracle, h, w):
+    from gsvc_amd.video import i420_to_rgb
+    rng = np.random.default_rng(h * w)
+    yuv = rng.integers(0, 256, h * w * 3 // 2, dtype=np.uint8)
+    got = i420_to_rgb(torch.from_numpy(yuv).to(cuda), h, w)
+    ref = oracle.i420_to_rgb(yuv, h, w)
+    np.testing.assert_array_equal(got[0].cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+def test_video_driver_end_to_end(cuda, tmp_path):
+    """Six synthetic 64x96 frames, K-frames 1 and 4: two GOPs, the real
+    trainer (fused steps), outputs written as the reference lays them out."""
+    import torch.nn.functional as F
+    from gsvc_amd import video as V
+    res = V.main(["--synthetic", "6", "--height", "64", "--width", "96", "--num_points", "300",
+                  "--iterations", "600", "--k_frames", "1,4", "--root", str(tmp_path),
+                  "--is_rm", "--is_ad", "--densification_interval", "50"])
+    assert [r["frame"] for r in res["frames"]] == list(range(1, 7))
+    psnr = [r["psnr"] for r in res["frames"]]
+    # an untrained model's render of frame 1, for scale
+    torch.manual_seed(1)
+    fresh = V.FrameTrainer(V.synthetic_video(6, 64, 96, 1)(0).to(cuda), 1, num_points=300)
+    with torch.no_grad():
+        mse0 = float(F.mse_loss(fresh.model()["render"], fresh.gt_image))
+    assert all(np.isfinite(psnr)) and min(psnr) > 10 * np.log10(1 / mse0) + 3.0
+    # P-frames start from the previous frame's model: they fit better than frame 1
+    assert psnr[1] > psnr[0] and psnr[4] > psnr[3]
+    base = tmp_path / "result" / "Synthetic"
+    assert (base / "K_frames.txt").read_text().split() == ["1", "4"]
+    line = json.loads((base / "GaussianVideo_600_300" / "train.txt").read_text().splitlines()[-1])
+    assert line["frames"] == 6 and line["avg_psnr"] == pytest.approx(np.mean(psnr))
+    models = torch.load(tmp_path / "models" / "Synthetic" / "GaussianVideo_600_300" /
+                        "gmodels_state_dict.pth", weights_only=True)
+    assert sorted(models) == [f"frame_{i}" for i in range(1, 7)]
+    assert set(models["frame_2"]) == {"_xyz", "_cholesky", "_features_dc"}
