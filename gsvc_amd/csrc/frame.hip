@@ -80,16 +80,27 @@ __device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, i
 // of the splat's outputs and inserts every K-th tile of its bbox (K = 1 in
 // production: more lanes did not shorten the insertion, see the launcher).
 constexpr int kProjThreads = 256;
-template <int K>
+
+// Diagnostic only (gsvc_debug_set(5, 1) with gsvc_debug_set_ptr): s_memrealtime
+// (100 MHz) stamps per wave -- start, projected, inserted, end -- as int64[4].
+__device__ __forceinline__ long long proj_stamp() {
+    long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+
+template <int K, bool kStamp>
 __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
     int n, const float *__restrict__ xyz, int xyz_tanh, const float *__restrict__ chol,
     const float *__restrict__ chol_bound, const float *__restrict__ feat,
     const float *__restrict__ rgb_w, const float *__restrict__ opac, float hw, float hh, int tbx,
     int tby, float2 *__restrict__ xys, int *__restrict__ radii, float4 *__restrict__ rec,
     unsigned *__restrict__ counts, float4 *__restrict__ slab, int *__restrict__ m_acc,
-    int *__restrict__ m_clear, float4 *__restrict__ grad_zero) {
+    int *__restrict__ m_clear, float4 *__restrict__ grad_zero, long long *stamps) {
     __shared__ int s_hits[kProjThreads / 64];
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    long long *st = kStamp ? stamps + 4 * (size_t)(t >> 6) : nullptr;
+    if (kStamp && (threadIdx.x & 63) == 0) st[0] = proj_stamp();
     const int i = t / K, sub = t % K;
     if (blockIdx.x == 0 && threadIdx.x == 0) *m_clear = 0;  // the next frame's slot
     int hits = 0;
@@ -127,8 +138,13 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
             }
             if (grad_zero) grad_zero[4 * i + q] = z;
         }
+        if (kStamp && (threadIdx.x & 63) == 0) st[1] = proj_stamp();
         if (P.rad > 0)
             hits = slab_insert<K>(P.xy.x, P.xy.y, P.rad, tbx, tby, sub, r0, r1, r2, counts, slab);
+    }
+    if (kStamp) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if ((threadIdx.x & 63) == 0) st[2] = proj_stamp();
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) hits += __shfl_xor(hits, off, 64);
@@ -139,6 +155,10 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
 #pragma unroll
         for (int k = 0; k < kProjThreads / 64; ++k) tot += s_hits[k];
         if (tot) atomicAdd(m_acc, tot);
+    }
+    if (kStamp) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if ((threadIdx.x & 63) == 0) st[3] = proj_stamp();
     }
 }
 
@@ -186,9 +206,20 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
     if (n > 0) {
         const dim3 grid(ceil_div(n, kProjThreads / k));
 #define GSVC_FRAME_PROJECT(K)                                                                    \
-    hipLaunchKernelGGL(frame_project_kernel<K>, grid, dim3(kProjThreads), 0, s, n, xyz, xyz_tanh, \
-                       chol, chol_bound, feat, rgb_w, opac, hw, hh, tbx, tby, w.xys, w.radii,     \
-                       w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero)
+    {                                                                                            \
+        auto kfn = frame_project_kernel<K, false>;                                               \
+        hipLaunchKernelGGL(kfn, grid, dim3(kProjThreads), 0, s, n, xyz, xyz_tanh, chol,          \
+                           chol_bound, feat, rgb_w, opac, hw, hh, tbx, tby, w.xys, w.radii,      \
+                           w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero, nullptr);     \
+    }
+        if (g_knobs[5] == 1 && g_debug_ptr) {  // diagnostic: per-wave stamps
+            auto kfn = frame_project_kernel<1, true>;
+            hipLaunchKernelGGL(kfn, grid, dim3(kProjThreads), 0, s, n, xyz, xyz_tanh, chol,
+                               chol_bound, feat, rgb_w, opac, hw, hh, tbx, tby, w.xys, w.radii,
+                               w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero,
+                               reinterpret_cast<long long *>(g_debug_ptr));
+            return check_launch("frame projection");
+        }
         switch (k) {
             case 2: GSVC_FRAME_PROJECT(2); break;
             case 8: GSVC_FRAME_PROJECT(8); break;

@@ -38,6 +38,8 @@ def main():
                     metavar=("KEY", "VALUE"), help="extra gsvc_debug_set for a second pass")
     ap.add_argument("--stamps", action="store_true",
                     help="also run the timestamped one-wave kernel (mode 7) and print phases")
+    ap.add_argument("--proj-stamps", action="store_true",
+                    help="also stamp the projection kernel's waves (knob 5) and print phases")
     args = ap.parse_args()
     lib = L.load()
     dev = torch.device("cuda:0")
@@ -112,6 +114,24 @@ def main():
             print(json.dumps(dict(N=n, stamps="percentiles 0/10/50/90/100 (us)",
                                   start=q(t[:, 0] - t0), staged=q(t[:, 1] - t[:, 0]),
                                   blend=q(t[:, 2] - t[:, 1]), stores_drained=q(t[:, 3] - t[:, 2]),
+                                  end=q(t[:, 3] - t0))), flush=True)
+        if args.proj_stamps:
+            import numpy as np
+            waves = (n + 63) // 64
+            st = torch.zeros((waves + 8, 4), dtype=torch.int64, device=dev)
+            lib.gsvc_debug_set_ptr(ctypes.c_void_p(st.data_ptr()))
+            lib.gsvc_debug_set(5, 1)
+            for _ in range(5):
+                frame()
+            torch.cuda.synchronize()
+            lib.gsvc_debug_set(5, 0)
+            lib.gsvc_debug_set_ptr(None)
+            t = st[:waves].cpu().numpy().astype(np.float64) * 0.01
+            t0 = t[:, 0].min()
+            q = lambda x: [round(float(np.percentile(x, p)), 2) for p in (0, 10, 50, 90, 100)]  # noqa
+            print(json.dumps(dict(N=n, proj_stamps="percentiles 0/10/50/90/100 (us)",
+                                  start=q(t[:, 0] - t0), project=q(t[:, 1] - t[:, 0]),
+                                  insert=q(t[:, 2] - t[:, 1]), reduce=q(t[:, 3] - t[:, 2]),
                                   end=q(t[:, 3] - t0))), flush=True)
     lib.gsvc_debug_set(0, 0)
 
