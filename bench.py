@@ -78,24 +78,31 @@ def all_max(x, world, device):
     return float(t.item())
 
 
-def composite_bytes(model):
+def composite_bytes_of(means2d, L, tile_bounds):
     """SURVEY §8d B_fwd = 36 N_vis + 4 M_eff + 8 T + 12 P for the render
-    (inference) forward: the [3,H,W] clamped image is written once and no
-    final_idx (the 16 P of the autograd forward counts its 4 B/px final_idx)."""
+    (inference) forward of one frame: the [3,H,W] clamped image is written
+    once and no final_idx (the 16 P of the autograd forward counts its 4 B/px
+    final_idx)."""
     from gsvc_amd import ops
     from gsvc_amd.utils import bin_and_sort_for_raster
+    n = means2d.shape[0]
     with torch.no_grad():
         xys, depths, radii, conics, nth = ops.project_gaussians_2d_forward(
-            model._xyz.shape[0], model.get_xyz, model.get_cholesky_elements, H, W,
-            model.tile_bounds, 0.01)
-        m, gids, bins = bin_and_sort_for_raster(model._xyz.shape[0], xys, depths, radii, nth,
-                                                model.tile_bounds)
-        counts = (bins[:, 1] - bins[:, 0]).clamp(min=0, max=256)
-        m_eff = int(counts.sum())
+            n, means2d, L, H, W, tile_bounds, 0.01)
+        m, gids, bins = bin_and_sort_for_raster(n, xys, depths, radii, nth, tile_bounds)
+        if bins is None:
+            m_eff = 0
+        else:
+            m_eff = int((bins[:, 1] - bins[:, 0]).clamp(min=0, max=256).sum())
         n_vis = int((nth > 0).sum())
-    T = model.tile_bounds[0] * model.tile_bounds[1]
+    T = tile_bounds[0] * tile_bounds[1]
     P = H * W
     return 36 * n_vis + 4 * m_eff + 8 * T + 12 * P, dict(N_vis=n_vis, M=m, M_eff=m_eff, T=T, P=P)
+
+
+def composite_bytes(model):
+    return composite_bytes_of(model.get_xyz.detach(), model.get_cholesky_elements.detach(),
+                              model.tile_bounds)
 
 
 def load_traffic(n_splats):
@@ -124,6 +131,49 @@ def cpu_baseline(n_splats, seconds):
     return {"value": frames / el, "unit": "frames/s", "cores": 1, "kind": "port",
             "sample": f"{frames} renders of one 1920x1080 / {n_splats}-splat frame "
                       f"(project+bin+sort+sum-raster) by oracle/oracle.c, 1 thread, {el:.1f} s"}
+
+
+def video_decode(device, frames=8, splats=10000, steps=50, warmup=5):
+    """A GOP of ``frames`` distinct 1920x1080 frame models (10k splats each,
+    the reference init distributions) rendered by ONE gsvc_render_frames_sum
+    call per step -- a video decoder's workload; the composite kernel then
+    spans frames x tiles.  Reported beside (not instead of) the single-frame
+    headline."""
+    from gsvc_amd import ops
+    from gsvc_amd.render import render_frames_sum
+    g = torch.Generator().manual_seed(4242)
+    xyz = torch.atanh(2 * (torch.rand(frames * splats, 2, generator=g) - 0.5)).to(device)
+    chol = torch.rand(frames * splats, 3, generator=g).to(device)
+    feat = torch.rand(frames * splats, 3, generator=g).to(device)
+    bound = torch.tensor([0.5, 0.0, 0.5], device=device)
+    bg = torch.ones(3, device=device)
+    sizes = [splats] * frames
+    for _ in range(warmup):
+        render_frames_sum(xyz, chol, feat, sizes, H, W, bg, cholesky_bound=bound)
+    torch.cuda.synchronize()
+    ops.composite_timing(True, max_launches=steps, every=4)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        render_frames_sum(xyz, chol, feat, sizes, H, W, bg, cholesky_bound=bound)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kt = ops.composite_times_ms(steps)
+    ops.composite_timing(False)
+    tb = ((W + 15) // 16, (H + 15) // 16, 1)
+    nbytes = 0
+    for b in range(frames):
+        sl = slice(b * splats, (b + 1) * splats)
+        nb, _ = composite_bytes_of(torch.tanh(xyz[sl]), chol[sl] + bound, tb)
+        nbytes += nb
+    avg_ms = sum(kt) / len(kt)
+    ach = nbytes / (avg_ms * 1e-3) / 1e9
+    return {"workload": f"GOP of {frames} distinct 1920x1080 frame models x {splats} splats, one "
+                        "gsvc_render_frames_sum call per step",
+            "frames_per_s": frames * steps / el, "ms_per_call": 1e3 * el / steps,
+            "roofline": {"kernel": "rasterize_sum_forward (frames x tiles)", "bound": "hbm",
+                         "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "avg_kernel_us": round(avg_ms * 1e3, 2),
+                         "algorithmic_bytes_per_launch": nbytes}}
 
 
 def secondary(device, steps=50, warmup=10):
@@ -218,6 +268,7 @@ def main():
         line["cpu_baseline"] = cpu_baseline(args.splats, args.cpu_seconds)
     if world == 1 and not args.no_secondary:
         line["secondary"] = secondary(device)
+        line["video_decode"] = video_decode(device)
     print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -57,6 +57,10 @@ _SIGS = {
     "gsvc_train_step_sum": [_I, _P, _P, _P, _P, _P, _I, _P, _P, _U, _U, _I, _I, _P, _P, _I, _P, _P,
                             _P, _P, _SZ, _P],
     "gsvc_i420_to_rgb": [_P, _I, _I, _P, _P],
+    "gsvc_render_frames_workspace_bytes": [_I, _I, _U, _U],
+    "gsvc_render_frames_zeroed_bytes": [_I, _U, _U],
+    "gsvc_render_frames_sum": [_I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _U, _U, _I, _I, _P, _P,
+                               _SZ, _P, _P],
     "gsvc_adan_step": [_I, _P, _P, _P, _P, _P, _P, _P] + [ctypes.c_double] * 9 +
                       [_I, ctypes.c_double, _P],
     "gsvc_rasterize_sum_backward": [_U, _U, _U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
@@ -76,6 +80,8 @@ _RESTYPE = {
     "gsvc_render_frame_workspace_bytes": _SZ,
     "gsvc_render_frame_zeroed_bytes": _SZ,
     "gsvc_train_step_workspace_bytes": _SZ,
+    "gsvc_render_frames_workspace_bytes": _SZ,
+    "gsvc_render_frames_zeroed_bytes": _SZ,
 }
 
 ABI_VERSION = 1

@@ -13,24 +13,26 @@ inline int tiles_of(unsigned h, unsigned w) {
     return ceil_div((int)w, kTile) * ceil_div((int)h, kTile);
 }
 
-// Workspace of one frame model (base NULL: sizes only).  The first ``zeroed``
-// bytes (counts[2][T] and the two M slots) must be zero before the first call;
-// every call leaves them zero.
+// Workspace of F frame models rendered together (base NULL: sizes only).  The
+// first ``zeroed`` bytes (counts and M slots) must be zero before the first
+// call; every call leaves them zero.
 struct FrameWs {
-    unsigned *counts;  // [2][T]: this frame's and the next frame's
-    int *m_slots;      // [2]
-    float4 *slab;      // [T][256][3] splat records
-    float2 *xys;       // [N]
+    unsigned *counts;  // [F][2][T]: per frame, this call's and the next call's
+    int *m_slots;      // [F][2]
+    float4 *slab;      // [F][T][256][3] splat records
+    float2 *xys;       // [N] (N = splats of all F frames)
     int *radii;        // [N]
     float4 *rec;       // [N][3] splat records
     size_t zeroed, bytes;
 };
-FrameWs frame_ws(char *base, int n, int ntiles);
+FrameWs frame_ws(char *base, int n, int ntiles, int frames = 1);
 
-// Frame f counts into parity f & 1 while its consumer clears the other parity.
+// Call f counts into parity f & 1 while its consumer clears the other parity
+// (pointers of frame 0; frame b's are counts_stride / m_stride further).
 struct FrameSlots {
     unsigned *counts, *counts_next;
     int *m_acc, *m_clear;
+    int counts_stride, m_stride;
 };
 FrameSlots frame_slots(const FrameWs &w, int ntiles, int frame_index);
 
@@ -39,9 +41,12 @@ FrameSlots frame_slots(const FrameWs &w, int ntiles, int frame_index);
 // and its insertion into the 256-slot slab of every tile it touches; this
 // frame's M into f.m_acc.  grad_zero (optional): [N][4] float4 gradient
 // records zeroed for the consumer's atomics.
+// frames > 1: the splats of frame b are [frame_off[b], frame_off[b + 1]) of
+// the n (device array frame_off) and max_frame_n is the largest frame.
 int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *chol,
                          const float *chol_bound, const float *feat, const float *rgb_w,
                          const float *opac, unsigned img_h, unsigned img_w, const FrameWs &w,
-                         const FrameSlots &f, float4 *grad_zero, hipStream_t s);
+                         const FrameSlots &f, float4 *grad_zero, hipStream_t s, int frames = 1,
+                         const int *frame_off = nullptr, int max_frame_n = 0);
 
 }  // namespace gsvc

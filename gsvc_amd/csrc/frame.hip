@@ -96,15 +96,27 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
     const float *__restrict__ rgb_w, const float *__restrict__ opac, float hw, float hh, int tbx,
     int tby, float2 *__restrict__ xys, int *__restrict__ radii, float4 *__restrict__ rec,
     unsigned *__restrict__ counts, float4 *__restrict__ slab, int *__restrict__ m_acc,
-    int *__restrict__ m_clear, float4 *__restrict__ grad_zero, long long *stamps) {
+    int *__restrict__ m_clear, float4 *__restrict__ grad_zero, long long *stamps,
+    const int *__restrict__ frame_off, int counts_stride, int m_stride, size_t slab_stride) {
     __shared__ int s_hits[kProjThreads / 64];
+    // batched frames (grid.y): this block's frame owns splats [begin, end)
+    int begin = 0, end = n;
+    if (frame_off) {
+        const int b = blockIdx.y;
+        begin = frame_off[b];
+        end = frame_off[b + 1];
+        counts += (size_t)b * counts_stride;
+        slab += b * slab_stride;
+        m_acc += (size_t)b * m_stride;
+        m_clear += (size_t)b * m_stride;
+    }
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     long long *st = kStamp ? stamps + 4 * (size_t)(t >> 6) : nullptr;
     if (kStamp && (threadIdx.x & 63) == 0) st[0] = proj_stamp();
-    const int i = t / K, sub = t % K;
+    const int i = begin + t / K, sub = t % K;
     if (blockIdx.x == 0 && threadIdx.x == 0) *m_clear = 0;  // the next frame's slot
     int hits = 0;
-    if (i < n) {
+    if (i < end) {
         float mx = xyz[2 * i], my = xyz[2 * i + 1];
         if (xyz_tanh) {  // get_xyz (GaussianSplats_Represent.py:57-59)
             mx = tanhf(mx);
@@ -162,7 +174,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
     }
 }
 
-FrameWs frame_ws(char *base, int n, int ntiles) {
+FrameWs frame_ws(char *base, int n, int ntiles, int frames) {
     FrameWs w;
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -171,12 +183,13 @@ FrameWs frame_ws(char *base, int n, int ntiles) {
         return p;
     };
     const size_t nn = (size_t)(n > 0 ? n : 1), nt = (size_t)(ntiles > 0 ? ntiles : 1);
-    // first: counts[2][T] and the two M slots, zeroed by the caller once;
-    // frame f counts into parity f & 1 while its rasterizer clears the other
-    w.counts = (unsigned *)take(sizeof(unsigned) * 2 * nt + 2 * sizeof(int));
-    w.m_slots = (int *)(w.counts + 2 * nt);
-    w.zeroed = sizeof(unsigned) * 2 * nt + 2 * sizeof(int);
-    w.slab = (float4 *)take(sizeof(float4) * 3 * kTilePix * nt);
+    const size_t nf = (size_t)(frames > 0 ? frames : 1);
+    // first: counts[F][2][T] and the M slots [F][2], zeroed by the caller once;
+    // call f counts into parity f & 1 while its rasterizer clears the other
+    w.counts = (unsigned *)take(sizeof(unsigned) * 2 * nt * nf + 2 * nf * sizeof(int));
+    w.m_slots = (int *)(w.counts + 2 * nt * nf);
+    w.zeroed = sizeof(unsigned) * 2 * nt * nf + 2 * nf * sizeof(int);
+    w.slab = (float4 *)take(sizeof(float4) * 3 * kTilePix * nt * nf);
     w.xys = (float2 *)take(sizeof(float2) * nn);
     w.radii = (int *)take(sizeof(int) * nn);
     w.rec = (float4 *)take(sizeof(float4) * 3 * nn);
@@ -187,6 +200,8 @@ FrameWs frame_ws(char *base, int n, int ntiles) {
 FrameSlots frame_slots(const FrameWs &w, int ntiles, int frame_index) {
     const int par = frame_index & 1;
     FrameSlots f;
+    f.counts_stride = 2 * ntiles;
+    f.m_stride = 2;
     f.m_acc = w.m_slots + par;
     f.m_clear = w.m_slots + (par ^ 1);
     f.counts = w.counts + (size_t)par * ntiles;
@@ -197,27 +212,42 @@ FrameSlots frame_slots(const FrameWs &w, int ntiles, int frame_index) {
 int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *chol,
                          const float *chol_bound, const float *feat, const float *rgb_w,
                          const float *opac, unsigned img_h, unsigned img_w, const FrameWs &w,
-                         const FrameSlots &f, float4 *grad_zero, hipStream_t s) {
+                         const FrameSlots &f, float4 *grad_zero, hipStream_t s, int frames,
+                         const int *frame_off, int max_frame_n) {
     const int tbx = ceil_div((int)img_w, kTile), tby = ceil_div((int)img_h, kTile);
     const float hw = 0.5f * (float)img_w, hh = 0.5f * (float)img_h;
     // lanes per splat: 1 unless gsvc_debug_set(4, k) picks 2, 4 or 8 (A/B knob;
     // measured at 1080p: equal at 10k splats, 1 lane fastest at 50k)
     const int k = g_knobs[4] == 2 || g_knobs[4] == 4 || g_knobs[4] == 8 ? g_knobs[4] : 1;
-    if (n > 0) {
-        const dim3 grid(ceil_div(n, kProjThreads / k));
+    const size_t slab_stride = (size_t)3 * kTilePix * (size_t)(tbx * tby);
+    if (frames > 1 && !frame_off) return set_error(GSVC_ERR_ARG, "frame projection: frame offsets");
+    const int per = frames > 1 ? max_frame_n : n;
+    if (frames > 1 && per <= 0) {
+        // no splats anywhere: only the M slots (memset of the whole [F][2] block)
+        if (hipMemsetAsync(f.m_acc < f.m_clear ? f.m_acc : f.m_clear, 0,
+                           sizeof(int) * 2 * (size_t)frames, s) != hipSuccess)
+            return set_error(GSVC_ERR_HIP, "frame projection: memset failed");
+        return check_launch("frame projection");
+    }
+    if (per > 0) {
+        const dim3 grid(ceil_div(per, kProjThreads / k), frames > 1 ? frames : 1);
 #define GSVC_FRAME_PROJECT(K)                                                                    \
     {                                                                                            \
         auto kfn = frame_project_kernel<K, false>;                                               \
         hipLaunchKernelGGL(kfn, grid, dim3(kProjThreads), 0, s, n, xyz, xyz_tanh, chol,          \
                            chol_bound, feat, rgb_w, opac, hw, hh, tbx, tby, w.xys, w.radii,      \
-                           w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero, nullptr);     \
+                           w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero, nullptr,      \
+                           frames > 1 ? frame_off : nullptr, f.counts_stride, f.m_stride,        \
+                           slab_stride);                                                         \
     }
         if (g_knobs[5] == 1 && g_debug_ptr) {  // diagnostic: per-wave stamps
             auto kfn = frame_project_kernel<1, true>;
             hipLaunchKernelGGL(kfn, grid, dim3(kProjThreads), 0, s, n, xyz, xyz_tanh, chol,
                                chol_bound, feat, rgb_w, opac, hw, hh, tbx, tby, w.xys, w.radii,
                                w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero,
-                               reinterpret_cast<long long *>(g_debug_ptr));
+                               reinterpret_cast<long long *>(g_debug_ptr),
+                               frames > 1 ? frame_off : nullptr, f.counts_stride, f.m_stride,
+                               slab_stride);
             return check_launch("frame projection");
         }
         switch (k) {
@@ -236,36 +266,36 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
 
 using namespace gsvc;
 
-extern "C" size_t gsvc_render_frame_workspace_bytes(int num_points, unsigned img_height,
-                                                    unsigned img_width) {
-    return frame_ws(nullptr, num_points, tiles_of(img_height, img_width)).bytes;
-}
+namespace gsvc {
 
-extern "C" size_t gsvc_render_frame_zeroed_bytes(unsigned img_height, unsigned img_width) {
-    return frame_ws(nullptr, 1, tiles_of(img_height, img_width)).zeroed;
-}
-
-extern "C" int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_tanh,
-                                     const float *cholesky, const float *cholesky_bound,
-                                     const float *features, const float *rgb_w,
-                                     const float *opacity, const float *background,
-                                     unsigned img_height, unsigned img_width, int frame_index,
-                                     int density_hint, int *meta, void *workspace,
-                                     size_t workspace_bytes, float *out, void *stream) {
-    if (num_points < 0 || img_height == 0 || img_width == 0)
-        return set_error(GSVC_ERR_ARG, "render_frame_sum: bad sizes");
-    if (!xyz || !cholesky || !features || !background || !meta || !out)
-        return set_error(GSVC_ERR_ARG, "render_frame_sum: missing input");
+// The one-call render of ``frames`` frames (frame b: splats [frame_off[b],
+// frame_off[b + 1]), image out + b * 3HW); frames == 1: splats [0, n).
+static int render_frames(int frames, const int *frame_off_host, const int *frame_off_dev,
+                         int num_points, const float *xyz, int xyz_tanh, const float *cholesky,
+                         const float *cholesky_bound, const float *features, const float *rgb_w,
+                         const float *opacity, const float *background, unsigned img_height,
+                         unsigned img_width, int frame_index, int density_hint, int *meta,
+                         void *workspace, size_t workspace_bytes, float *out, hipStream_t s) {
     const int tbx = ceil_div((int)img_width, kTile), tby = ceil_div((int)img_height, kTile);
     const int ntiles = tbx * tby;
-    const FrameWs w = frame_ws((char *)workspace, num_points, ntiles);
+    const FrameWs w = frame_ws((char *)workspace, num_points, ntiles, frames);
     if (!workspace || workspace_bytes < w.bytes)
         return set_error(GSVC_ERR_WORKSPACE, "render_frame_sum: workspace too small (%zu < %zu)",
                          workspace_bytes, w.bytes);
-    hipStream_t s = (hipStream_t)stream;
+    int max_n = num_points;
+    if (frames > 1) {
+        max_n = 0;
+        for (int b = 0; b < frames; ++b) {
+            const int nb = frame_off_host[b + 1] - frame_off_host[b];
+            if (nb < 0 || frame_off_host[b] < 0 || frame_off_host[b + 1] > num_points)
+                return set_error(GSVC_ERR_ARG, "render_frames_sum: bad frame offsets");
+            max_n = nb > max_n ? nb : max_n;
+        }
+    }
     const FrameSlots f = frame_slots(w, ntiles, frame_index);
     int rc = frame_project_launch(num_points, xyz, xyz_tanh, cholesky, cholesky_bound, features,
-                                  rgb_w, opacity, img_height, img_width, w, f, nullptr, s);
+                                  rgb_w, opacity, img_height, img_width, w, f, nullptr, s, frames,
+                                  frame_off_dev, max_n);
     if (rc) return rc;
     SumFwdArgs A;
     sum_fwd_args_init(A);
@@ -286,5 +316,73 @@ extern "C" int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_t
     A.num_points = num_points;
     A.rec = w.rec;
     A.out = out;
+    if (frames > 1) {
+        A.frames = frames;
+        A.frame_off = frame_off_dev;
+        A.counts_stride = f.counts_stride;
+        A.m_stride = f.m_stride;
+        A.slab_stride = (size_t)3 * kTilePix * (size_t)ntiles;
+        A.out_stride = (size_t)3 * img_width * img_height;
+    }
     return sum_forward_launch(A, density_hint, s);
+}
+
+}  // namespace gsvc
+
+extern "C" size_t gsvc_render_frames_workspace_bytes(int frames, int num_points,
+                                                     unsigned img_height, unsigned img_width) {
+    return frame_ws(nullptr, num_points, tiles_of(img_height, img_width), frames).bytes;
+}
+
+extern "C" size_t gsvc_render_frames_zeroed_bytes(int frames, unsigned img_height,
+                                                  unsigned img_width) {
+    return frame_ws(nullptr, 1, tiles_of(img_height, img_width), frames).zeroed;
+}
+
+extern "C" int gsvc_render_frames_sum(int frames, const int *frame_offsets_host,
+                                      const int *frame_offsets_dev, const float *xyz, int xyz_tanh,
+                                      const float *cholesky, const float *cholesky_bound,
+                                      const float *features, const float *rgb_w,
+                                      const float *opacity, const float *background,
+                                      unsigned img_height, unsigned img_width, int call_index,
+                                      int density_hint, int *meta, void *workspace,
+                                      size_t workspace_bytes, float *out, void *stream) {
+    if (frames < 1 || frames > 4096 || img_height == 0 || img_width == 0)
+        return set_error(GSVC_ERR_ARG, "render_frames_sum: bad sizes");
+    if (!frame_offsets_host || !frame_offsets_dev || !background || !meta || !out)
+        return set_error(GSVC_ERR_ARG, "render_frames_sum: missing input");
+    if (frame_offsets_host[0] != 0)
+        return set_error(GSVC_ERR_ARG, "render_frames_sum: frame offsets must start at 0");
+    const int n = frame_offsets_host[frames];
+    if (n > 0 && (!xyz || !cholesky || !features))
+        return set_error(GSVC_ERR_ARG, "render_frames_sum: missing input");
+    return render_frames(frames, frame_offsets_host, frame_offsets_dev, n, xyz, xyz_tanh, cholesky,
+                         cholesky_bound, features, rgb_w, opacity, background, img_height,
+                         img_width, call_index, density_hint, meta, workspace, workspace_bytes, out,
+                         (hipStream_t)stream);
+}
+
+extern "C" size_t gsvc_render_frame_workspace_bytes(int num_points, unsigned img_height,
+                                                    unsigned img_width) {
+    return frame_ws(nullptr, num_points, tiles_of(img_height, img_width)).bytes;
+}
+
+extern "C" size_t gsvc_render_frame_zeroed_bytes(unsigned img_height, unsigned img_width) {
+    return frame_ws(nullptr, 1, tiles_of(img_height, img_width)).zeroed;
+}
+
+extern "C" int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_tanh,
+                                     const float *cholesky, const float *cholesky_bound,
+                                     const float *features, const float *rgb_w,
+                                     const float *opacity, const float *background,
+                                     unsigned img_height, unsigned img_width, int frame_index,
+                                     int density_hint, int *meta, void *workspace,
+                                     size_t workspace_bytes, float *out, void *stream) {
+    if (num_points < 0 || img_height == 0 || img_width == 0)
+        return set_error(GSVC_ERR_ARG, "render_frame_sum: bad sizes");
+    if ((num_points > 0 && (!xyz || !cholesky || !features)) || !background || !meta || !out)
+        return set_error(GSVC_ERR_ARG, "render_frame_sum: missing input");
+    return render_frames(1, nullptr, nullptr, num_points, xyz, xyz_tanh, cholesky, cholesky_bound,
+                         features, rgb_w, opacity, background, img_height, img_width, frame_index,
+                         density_hint, meta, workspace, workspace_bytes, out, (hipStream_t)stream);
 }

@@ -39,6 +39,15 @@ struct SumFwdArgs {
     const int *cull_radii;
     int num_points;
     int *meta_out;  // frame path: meta[0] <- M (from m_dev), meta[1] <- 0
+    // batched frame path (gsvc_render_frames_sum): the grid covers frames x
+    // tiles; frame b's slab-path buffers sit at these strides from frame 0's
+    // (slab, counts, counts_clear, m_dev, meta_out, out) and its splats are
+    // [frame_off[b], frame_off[b + 1]) of the global id range (device array;
+    // NULL: one frame, splats [splat_begin = 0, num_points))
+    int frames, counts_stride, m_stride;
+    size_t slab_stride, out_stride;
+    const int *frame_off;
+    int splat_begin;
     float *out;
     int *final_idx;
     float *final_Ts;

@@ -270,7 +270,7 @@ __device__ int wave_brute_tile_ids(const SumFwdArgs &A, int tile, int *s_ids) {
     const int tby = (A.img_h + kTile - 1) / kTile;
     const unsigned long long lt = (1ull << lane) - 1ull;
     int written = 0;
-    for (int base = 0; base < A.num_points && written < kTilePix; base += 64) {
+    for (int base = A.splat_begin; base < A.num_points && written < kTilePix; base += 64) {
         const int j = base + lane;
         bool hit = false;
         if (j < A.num_points) {
@@ -559,7 +559,19 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
     __shared__ float4 s_buf[kOneWave ? 1 : 2][kSlice];
     __shared__ int s_ids[kOneWave ? 1 : 2][kTilePix];
     const int w = kOneWave ? 0 : (threadIdx.x >> 6);
-    const int tile = xcd_remap(blockIdx.x, A.ntiles);
+    int tile = xcd_remap(blockIdx.x, A.ntiles * A.frames);
+    if (A.frames > 1) {  // batched frames: this block's frame and tile
+        const int b = tile / A.ntiles;
+        tile -= b * A.ntiles;
+        A.slab += b * A.slab_stride;
+        A.slab_counts += (size_t)b * A.counts_stride;
+        A.slab_counts_clear += (size_t)b * A.counts_stride;
+        A.m_dev += (size_t)b * A.m_stride;
+        A.meta_out += (size_t)b * A.m_stride;
+        A.out += b * A.out_stride;
+        A.splat_begin = A.frame_off[b];
+        A.num_points = A.frame_off[b + 1];
+    }
     long long t0 = 0;
     if (kMode == kModeStamp || kMode == kModeSparseStamp) t0 = stamp();
     int2 range;
@@ -777,6 +789,7 @@ void sum_fwd_args_init(SumFwdArgs &A) {
     A = SumFwdArgs{};
     A.sparse_max = g_knobs[3] > 0 ? g_knobs[3] : 8;
     A.layout = kLayoutHWC;
+    A.frames = 1;
 }
 
 int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
@@ -787,37 +800,41 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
     const int ntiles = A.ntiles;
     int mode = g_knobs[0];
     if (mode == 0)
-        mode = ((long long)density_hint > (long long)kDenseEntriesPerTile * ntiles) ? kModeBanded
-                                                                                     : kModeSparse;
+        mode = ((long long)density_hint > (long long)kDenseEntriesPerTile * ntiles * A.frames)
+                   ? kModeBanded
+                   : kModeSparse;
     if (mode == kModeStamp && A.layout != kLayoutHWC)
         return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: stamp mode needs the HWC layout");
+    if (A.frames > 1 && (mode == kModeStamp || mode == kModeSparseStamp))
+        return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: stamp modes render one frame");
     const int tslot = timing_begin(s);
+    const dim3 grid(ntiles * A.frames);
     switch (mode) {
         case kModeSparse:
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeSparse>, dim3(ntiles), dim3(64), 0, s, A);
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeSparse>, grid, dim3(64), 0, s, A);
             break;
         case kModeBanded:
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeBanded>, dim3(ntiles), dim3(128), 0, s, A);
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeBanded>, grid, dim3(128), 0, s, A);
             break;
         case kModeStamp:
             A.stamps = reinterpret_cast<long long *>(A.final_Ts);
             A.final_Ts = nullptr;
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeStamp>, dim3(ntiles), dim3(128), 0, s, A);
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeStamp>, grid, dim3(128), 0, s, A);
             break;
         case kModeNoBlend:
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeNoBlend>, dim3(ntiles), dim3(128), 0, s, A);
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeNoBlend>, grid, dim3(128), 0, s, A);
             break;
         case kModeNoStore:
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeNoStore>, dim3(ntiles), dim3(128), 0, s, A);
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeNoStore>, grid, dim3(128), 0, s, A);
             break;
         case kModeAdaptive:
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeAdaptive>, dim3(ntiles), dim3(128), 0, s, A);
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeAdaptive>, grid, dim3(128), 0, s, A);
             break;
         case kModeSparseStamp:
             if (!g_debug_ptr)
                 return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: mode 7 needs gsvc_debug_set_ptr");
             A.stamps = reinterpret_cast<long long *>(g_debug_ptr);
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeSparseStamp>, dim3(ntiles), dim3(64), 0, s, A);
+            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeSparseStamp>, grid, dim3(64), 0, s, A);
             break;
         default:
             return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: unknown kernel mode %d", mode);

@@ -136,3 +136,95 @@ def render_sum_frame(means2d: Tensor, L_elements: Tensor, colors: Tensor, opacit
         background = torch.ones(3, dtype=torch.float32, device=colors.device)
     return render_frame_sum(means2d, L_elements, colors, img_height, img_width, background,
                             xyz_tanh=False, opacity=opacity)
+
+
+class _BatchWorkspace:
+    def __init__(self):
+        self.buf = None
+        self.key = None
+        self.call = 0
+        self.meta = None
+        self.offs = None
+        self.offs_host = None
+        # total M of a recent call for the kernel choice: meta [F, 2] copied to
+        # pinned memory without a sync every 16 calls (stale values only cost speed)
+        self.hint = 0
+        self.pinned = None
+        self.event = None
+
+    def update_hint(self):
+        if self.event is not None and self.event.query():
+            self.hint = int(self.pinned[:, 0].sum())
+            self.event = None
+        if self.event is None and self.call % 16 == 1:
+            if self.pinned is None or self.pinned.shape != self.meta.shape:
+                self.pinned = torch.empty(self.meta.shape, dtype=torch.int32, pin_memory=True)
+            self.pinned.copy_(self.meta, non_blocking=True)
+            self.event = torch.cuda.Event()
+            self.event.record()
+
+
+_batch_workspaces = {}
+
+
+def render_frames_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, frame_sizes,
+                      img_height: int, img_width: int, background: Tensor, xyz_tanh: bool = True,
+                      cholesky_bound: Optional[Tensor] = None, rgb_w: Optional[Tensor] = None,
+                      opacity: Optional[Tensor] = None) -> Tensor:
+    """Render a batch of frame models of one video in one call (two kernels
+    over all frames; gsvc_render_frames_sum): the inputs are the frames'
+    splats concatenated (frame b has ``frame_sizes[b]`` of them, in order),
+    the output [F, 3, H, W] -- each image bit-identical to
+    ``render_frame_sum`` of that frame alone.  A video decoder's GOP: GSVC
+    stores one model per frame (train_video_Represent.py:379-384)."""
+    import ctypes
+    H, W = int(img_height), int(img_width)
+    sizes = [int(x) for x in frame_sizes]
+    F = len(sizes)
+    if F < 1 or any(x < 0 for x in sizes):
+        raise ValueError("frame_sizes must be a non-empty list of non-negative counts")
+    n = xyz.shape[0]
+    if sum(sizes) != n:
+        raise ValueError(f"frame_sizes sum to {sum(sizes)}, inputs have {n} splats")
+    dev = xyz.device
+    keep = []
+    p_xyz = _ptr_f32(xyz, "xyz", 2 * n, keep)
+    p_chol = _ptr_f32(cholesky, "cholesky", 3 * n, keep)
+    p_feat = _ptr_f32(features, "features", 3 * n, keep)
+    p_bound = _ptr_f32(cholesky_bound, "cholesky_bound", 3, keep)
+    p_rgbw = _ptr_f32(rgb_w, "rgb_w", n, keep)
+    p_opac = _ptr_f32(opacity, "opacity", n, keep)
+    p_bg = _ptr_f32(background, "background", 3, keep)
+    stream_handle = torch.cuda.current_stream(dev).cuda_stream
+    key = (dev.index, stream_handle)
+    bw = _batch_workspaces.get(key)
+    if bw is None:
+        bw = _batch_workspaces[key] = _BatchWorkspace()
+    need = L.size("gsvc_render_frames_workspace_bytes", F, n, H, W)
+    if bw.buf is None or bw.buf.numel() < need or bw.key != (F, H, W):
+        if bw.buf is None or bw.buf.numel() < need:
+            bw.buf = torch.empty((need,), dtype=torch.uint8, device=dev)
+        bw.buf[: L.size("gsvc_render_frames_zeroed_bytes", F, H, W)].zero_()
+        bw.meta = torch.zeros((F, 2), dtype=torch.int32, device=dev)
+        bw.key = (F, H, W)
+        bw.call = 0
+        bw.offs_host = None
+        bw.hint, bw.event, bw.pinned = 0, None, None
+    offs = [0]
+    for x in sizes:
+        offs.append(offs[-1] + x)
+    if bw.offs_host is None or list(bw.offs_host) != offs:
+        bw.offs_host = (ctypes.c_int * (F + 1))(*offs)
+        bw.offs = torch.tensor(offs, dtype=torch.int32, device=dev)
+    out = torch.empty((F, 3, H, W), dtype=torch.float32, device=dev)
+    rc = L.load().gsvc_render_frames_sum(
+        F, bw.offs_host, bw.offs.data_ptr(), p_xyz, 1 if xyz_tanh else 0, p_chol, p_bound, p_feat,
+        p_rgbw, p_opac, p_bg, H, W, bw.call, bw.hint, bw.meta.data_ptr(), bw.buf.data_ptr(),
+        bw.buf.numel(), out.data_ptr(), stream_handle)
+    if rc != 0:
+        bw.key = None
+        msg = L.load().gsvc_last_error().decode(errors="replace")
+        raise RuntimeError(f"gsvc_render_frames_sum failed (status {rc}): {msg}")
+    bw.call += 1
+    bw.update_hint()
+    return out

@@ -282,6 +282,27 @@ int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
                         float *render_out, float *grads_out, void *workspace,
                         size_t workspace_bytes, void *stream);
 
+/* The same render for a batch of ``frames`` frame models of one video (a
+ * decoder's GOP: frame k of GSVC's gmodels_state_dict is its own model), one
+ * call, two kernels over all frames: frame b's splats are
+ * [frame_offsets[b], frame_offsets[b + 1]) of the concatenated inputs (host
+ * and device copies of the int[frames + 1] offsets, offsets[0] = 0); its
+ * image is out + b * 3*H*W (out [frames,3,H,W]); meta int[frames][2].
+ * Images are bit-identical to per-frame gsvc_render_frame_sum calls.
+ * Workspace sized by gsvc_render_frames_workspace_bytes, first
+ * gsvc_render_frames_zeroed_bytes zero before the first call; call_index
+ * alternates parity between calls on one workspace. */
+size_t gsvc_render_frames_workspace_bytes(int frames, int num_points, unsigned img_height,
+                                          unsigned img_width);
+size_t gsvc_render_frames_zeroed_bytes(int frames, unsigned img_height, unsigned img_width);
+int gsvc_render_frames_sum(int frames, const int *frame_offsets_host,
+                           const int *frame_offsets_dev, const float *xyz, int xyz_tanh,
+                           const float *cholesky, const float *cholesky_bound,
+                           const float *features, const float *rgb_w, const float *opacity,
+                           const float *background, unsigned img_height, unsigned img_width,
+                           int call_index, int density_hint, int *meta, void *workspace,
+                           size_t workspace_bytes, float *out, void *stream);
+
 /* Replaces _C.rasterize_sum_backward (bindings.cu:706-779 -> backward.cu:696-862).
  * Gradients are written into one 64-byte record per splat,
  * grad_records [N,16] float: [0:2] v_xy, [2:5] v_conic, [5:8] v_colors,

@@ -280,3 +280,55 @@ def test_render_frame_in_kernel_sort(cuda, oracle, n, count):
     o = oracle.render_sum(means, L, colors, opac, H, W)["out"]
     np.testing.assert_allclose(N(fast)[0], np.clip(o, 0, 1).transpose(2, 0, 1), rtol=1e-6,
                                atol=1e-5)
+
+
+def _frame_models(sizes, H, W, seed, cluster_frame=None):
+    g = torch.Generator().manual_seed(seed)
+    xyz, chol, feat = [], [], []
+    for b, n in enumerate(sizes):
+        x = torch.atanh(2 * (torch.rand(n, 2, generator=g) - 0.5) * 0.999)
+        c = torch.rand(n, 3, generator=g)
+        if b == 1 and n:  # a frame whose splats are all degenerate: M = 0, background
+            c = -torch.tensor([0.5, 0.0, 0.5]).expand(n, 3).clone()
+        if b == cluster_frame:  # > 256 entries on the tiles around one spot
+            k = n // 2
+            x[:k] = torch.atanh(torch.full((k, 2), -0.3) + 0.02 * torch.rand(k, 2, generator=g))
+            c[:k] = torch.tensor([2.0, 0.2, 1.5])
+        xyz.append(x)
+        chol.append(c)
+        feat.append(torch.rand(n, 3, generator=g))
+    return torch.cat(xyz).cuda(), torch.cat(chol).cuda(), torch.cat(feat).cuda()
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("H,W,sizes,cluster", [
+    (72, 120, [300, 200, 0, 1200, 50], 3),
+    (1080, 1920, [10000] * 8, None),
+])
+def test_render_frames_batch_matches_single(cuda, mode, H, W, sizes, cluster):
+    """gsvc_render_frames_sum: every frame of the batch bit-identical to its
+    own one-frame render -- empty frames, an all-background frame, tiles past
+    256 entries (the id-range brute rebuild of the frame's own splats)."""
+    from gsvc_amd import _lib
+    from gsvc_amd.render import render_frame_sum, render_frames_sum
+    xyz, chol, feat = _frame_models(sizes, H, W, seed=len(sizes) + H, cluster_frame=cluster)
+    bound = torch.tensor([0.5, 0.0, 0.5], device="cuda")
+    rgbw = torch.rand(sum(sizes), 1, device="cuda") + 0.5
+    bg = torch.tensor([0.3, 0.6, 0.9], device="cuda")
+    lib = _lib.load()
+    prev = lib.gsvc_debug_set(0, mode)
+    try:
+        outs = [render_frames_sum(xyz, chol, feat, sizes, H, W, bg, cholesky_bound=bound,
+                                  rgb_w=rgbw) for _ in range(3)]  # parity slots reused
+        off = 0
+        for b, n in enumerate(sizes):
+            sl = slice(off, off + n)
+            one = render_frame_sum(xyz[sl], chol[sl], feat[sl], H, W, bg, cholesky_bound=bound,
+                                   rgb_w=rgbw[sl])
+            for o in outs:
+                assert torch.equal(o[b], one[0]), (b, n)
+            off += n
+    finally:
+        lib.gsvc_debug_set(0, prev)
+    if sizes[2] == 0:  # a frame without splats is the background
+        assert torch.equal(outs[0][2], bg.view(3, 1, 1).expand(3, H, W))
