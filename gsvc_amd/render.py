@@ -41,19 +41,24 @@ class _FrameWorkspace:
         self.meta_ptr = 0
         self.frame = 0
         self.hint = _LazyCount()
+        self.shape = None
 
 
 _workspaces = {}
+_raw_stream = torch._C._cuda_getCurrentRawStream  # current stream handle, no Stream object
 
 
 def _workspace(dev: torch.device, n: int, H: int, W: int) -> _FrameWorkspace:
-    stream_handle = torch.cuda.current_stream(dev).cuda_stream
+    stream_handle = _raw_stream(dev.index)
     key = (dev.index, stream_handle)
     fw = _workspaces.get(key)
     if fw is None:
         fw = _workspaces[key] = _FrameWorkspace(stream_handle)
         fw.meta = torch.zeros((2,), dtype=torch.int32, device=dev)
         fw.meta_ptr = fw.meta.data_ptr()
+    if fw.shape == (n, H, W) and not fw.dirty:
+        return fw
+    fw.shape = (n, H, W)
     need = L.size("gsvc_render_frame_workspace_bytes", n, H, W)
     if fw.buf is None or fw.buf.numel() < need:
         fw.buf = torch.empty((need,), dtype=torch.uint8, device=dev)
@@ -68,11 +73,16 @@ def _workspace(dev: torch.device, n: int, H: int, W: int) -> _FrameWorkspace:
     return fw
 
 
+_F32 = torch.float32
+
+
 def _ptr_f32(t: Optional[Tensor], name: str, numel: int, keep: list) -> int:
     """Device address of t as contiguous float32 (a converted copy is kept
     alive in ``keep`` until the launch is enqueued)."""
     if t is None:
         return 0
+    if t.dtype is _F32 and t.is_cuda and t.is_contiguous() and t.numel() == numel:
+        return t.data_ptr()  # the common case, checked first
     if not t.is_cuda:
         raise RuntimeError(f"{name} must be a CUDA tensor")
     if t.dtype is not torch.float32 or not t.is_contiguous():
@@ -81,6 +91,16 @@ def _ptr_f32(t: Optional[Tensor], name: str, numel: int, keep: list) -> int:
     if t.numel() != numel:
         raise ValueError(f"{name} must have {numel} elements, got {t.numel()}")
     return t.data_ptr()
+
+
+_render_fn = None
+
+
+def _render_frame_fn():
+    global _render_fn
+    if _render_fn is None:
+        _render_fn = L.load().gsvc_render_frame_sum
+    return _render_fn
 
 
 def render_frame_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, img_height: int,
@@ -105,7 +125,7 @@ def render_frame_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, img_height
     p_bg = _ptr_f32(background, "background", 3, keep)
     fw = _workspace(dev, n, H, W)
     out = torch.empty((1, 3, H, W), dtype=torch.float32, device=dev)
-    rc = L.load().gsvc_render_frame_sum(
+    rc = _render_frame_fn()(
         n, p_xyz, 1 if xyz_tanh else 0, p_chol, p_bound, p_feat, p_rgbw, p_opac, p_bg, H, W,
         fw.frame, fw.hint.value, fw.meta_ptr, fw.buf_ptr, fw.buf.numel(), out.data_ptr(),
         fw.stream)
