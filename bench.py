@@ -222,9 +222,9 @@ def main():
         for _ in range(args.warmup):
             model()
         torch.cuda.synchronize()
-        # HIP events around every 8th composite launch of the timed region,
+        # HIP events around every 16th composite launch of the timed region,
         # recorded by the library on the kernel's own stream
-        ops.composite_timing(True, max_launches=args.steps, every=8)
+        ops.composite_timing(True, max_launches=args.steps, every=16)
         barrier(world)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
