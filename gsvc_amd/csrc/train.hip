@@ -47,6 +47,7 @@ struct TrainTileArgs {
     float *grad;      // [N, 16]: v_xy 0:2, v_conic 2:5, v_colors 5:8, v_opacity 8
     float2 *err;      // [ntiles]: sum of squared, sum of absolute errors
     float *out;       // optional [3, H, W] clamped render
+    long long *stamps;  // diagnostic: int64[ntiles][8]
 };
 
 __device__ __forceinline__ float clamp_unit(float x) {
@@ -54,32 +55,33 @@ __device__ __forceinline__ float clamp_unit(float x) {
     return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x);
 }
 
-// Rows of the 16x16 tile at (tx0, ty0) on which splat (x, y, conic a b c,
-// opacity o) can reach alpha >= 1/255 at some pixel centre (bit r = row r);
-// 0 only when provably none.  alpha >= 1/255 needs sigma <= ln(255 o), i.e.
+// The pixels of the 16x16 tile at (tx0, ty0) at whose centres splat (x, y,
+// conic a b c, opacity o) can reach alpha >= 1/255, as a rectangle of tile
+// coordinates packed {x0, x1, y0, y1} (4 bits each, inclusive); 0xffffffff
+// when provably none.  alpha >= 1/255 needs sigma <= ln(255 o), i.e.
 // d^T C d <= 2 ln(255 o), an ellipse with half-extents sqrt(2 ln(255 o) c / det)
 // and sqrt(2 ln(255 o) a / det); the margins (0.1 % + 0.01 px) dwarf fp32
 // rounding (the banded forward's test, raster_sum.hip ellipse_hits_rect).  A
 // culled (entry, pixel) pair contributes nothing in the reference either.
-__device__ __forceinline__ unsigned ellipse_rows(float x, float y, float a, float b, float c,
+constexpr unsigned kNoRect = 0xffffffffu;
+constexpr unsigned kFullRect = 0xf0f0u;  // x 0..15, y 0..15
+
+__device__ __forceinline__ unsigned ellipse_rect(float x, float y, float a, float b, float c,
                                                  float o, float tx0, float ty0) {
-    if (!(o > 0.0f)) return (o <= 0.0f) ? 0u : 0xffffu;  // o <= 0: alpha never valid; NaN: keep
+    if (!(o > 0.0f)) return (o <= 0.0f) ? kNoRect : kFullRect;  // o <= 0: never valid; NaN: keep
     const float det = a * c - b * b;
     if (!(a > 0.0f) || !(det > 0.0f) || !(o < 3.0e38f) || !(fabsf(x) < 1e30f) || !(fabsf(y) < 1e30f))
-        return 0xffffu;  // not positive definite / non-finite: no culling
+        return kFullRect;  // not positive definite / non-finite: no culling
     const float lg = __logf(255.0f * o);
-    if (lg < -0.01f) return 0u;  // o < e^-0.01 / 255: alpha < 1/255 everywhere
+    if (lg < -0.01f) return kNoRect;  // o < e^-0.01 / 255: alpha < 1/255 everywhere
     const float S2 = 2.0f * (lg * 1.001f + 0.01f);
     const float ex = sqrtf(S2 * c / det) * 1.001f + 0.01f;
     const float ey = sqrtf(S2 * a / det) * 1.001f + 0.01f;
-    if (x + ex < tx0 || x - ex > tx0 + 15.0f) return 0u;
-    const float lo = fmaxf(ceilf(y - ey - ty0), 0.0f), hi = fminf(floorf(y + ey - ty0), 15.0f);
-    if (!(lo <= hi)) return 0u;
-    const unsigned l = (unsigned)lo, h = (unsigned)hi;
-    return ((2u << h) - 1u) & ~((1u << l) - 1u);
+    const float x0 = fmaxf(ceilf(x - ex - tx0), 0.0f), x1 = fminf(floorf(x + ex - tx0), 15.0f);
+    const float y0 = fmaxf(ceilf(y - ey - ty0), 0.0f), y1 = fminf(floorf(y + ey - ty0), 15.0f);
+    if (!(x0 <= x1) || !(y0 <= y1)) return kNoRect;
+    return (unsigned)x0 | ((unsigned)x1 << 4) | ((unsigned)y0 << 8) | ((unsigned)y1 << 12);
 }
-
-__device__ __forceinline__ int ceil_log2_i(int n) { return n <= 1 ? 0 : 32 - __clz(n - 1); }
 
 // The first <= 256 ids (ascending) of the splats whose bbox covers tile
 // (tx, ty) -- the slab insertion's own test -- for a tile whose slab kept an
@@ -114,21 +116,34 @@ __device__ int block_brute_ids(const TrainTileArgs &A, int tx, int ty, int *s_gi
     return min(written, kT);
 }
 
+// Diagnostic only (gsvc_debug_set(5, 2) with gsvc_debug_set_ptr): s_memrealtime
+// stamps per tile by thread 0 -- start, staged, forward done, scan done,
+// items done, end -- as int64[8].
+__device__ __forceinline__ long long tstamp() {
+    long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+
+template <bool kStamp>
 __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
     // LDS: geo / col / pix, reused as the 9 x 256 gradient reduction buffer
     // once the backward loop is done (16.5 KB per workgroup)
     __shared__ float4 s_buf[3 * kT];
     __shared__ float4 s_ext[kT];     // b, id bits, a, c
-    __shared__ unsigned s_rows[kT];  // rows of the tile the entry can reach
+    __shared__ unsigned s_rect[kT];  // pixels of the tile the entry can reach (ellipse_rect)
+    __shared__ float s_part[9][kT];  // backward: per-item partial gradients
+    __shared__ int s_off[kT + 1];    // backward: first work item of each entry
     __shared__ int s_cnt[4];
     __shared__ float s_err[2][4];
     float4 *s_geo = s_buf;           // x, y, a/2, b
     float4 *s_col = s_buf + kT;      // c/2, opacity, r, g
     float4 *s_pix = s_buf + 2 * kT;  // v_out rgb, last contributing entry (bits; -1 outside)
-    float(*s_red)[kT] = reinterpret_cast<float(*)[kT]>(s_buf);
     int *s_ids = reinterpret_cast<int *>(s_pix);  // unsorted ids while staging
     const int tile = xcd_remap(blockIdx.x, A.ntiles);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    long long *st = kStamp ? A.stamps + 8 * (size_t)tile : nullptr;
+    if (kStamp && tid == 0) st[0] = tstamp();
     const int ty = tile / A.tbx, tx = tile - ty * A.tbx;
     const int pi = ty * kTile + (tid >> 4), pj = tx * kTile + (tid & 15);
     const bool inside = pi < A.img_h && pj < A.img_w;
@@ -137,23 +152,32 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
     const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
     const size_t pix = inside ? (size_t)pi * (size_t)A.img_w + (size_t)pj : 0;
     const float gt0 = A.gt[pix], gt1 = A.gt[hw + pix], gt2 = A.gt[2 * hw + pix];
+    // slots below kSpec are loaded speculatively in the same round trip as the
+    // count (most tiles have that few entries); the rest once the count is known
+    constexpr int kSpec = 32;
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+    if (tid < kSpec) {
+        const float4 *r = A.slab + ((size_t)tile * kT + tid) * 3;
+        r0 = r[0];
+        r1 = r[1];
+        r2 = r[2];
+    }
     const bool empty = *A.m_dev < 1;  // rasterize_sum.py:121-127: background, no gradient
     const int n_all = empty ? 0 : (int)A.counts[tile];
     if (tid == 0) A.counts_clear[tile] = 0u;  // the next frame's counts
 
     // 1. the tile's first <= 256 entries in (tile, splat id) order into LDS
     int n;
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
     int rank = tid;
     if (n_all <= kT) {
         int id = 0x7fffffff;
-        if (tid < n_all) {
+        if (tid >= kSpec && tid < n_all) {
             const float4 *r = A.slab + ((size_t)tile * kT + tid) * 3;
             r0 = r[0];
             r1 = r[1];
             r2 = r[2];
-            id = __float_as_int(r2.y);
         }
+        if (tid < n_all) id = __float_as_int(r2.y);
         s_ids[tid] = id;
         __syncthreads();
         if (tid < n_all) {
@@ -175,9 +199,10 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
         s_geo[rank] = r0;
         s_col[rank] = r1;
         s_ext[rank] = r2;
-        s_rows[rank] = ellipse_rows(r0.x, r0.y, r2.z, r0.w, r2.w, r1.y, tx0, ty0);
+        s_rect[rank] = ellipse_rect(r0.x, r0.y, r2.z, r0.w, r2.w, r1.y, tx0, ty0);
     }
     __syncthreads();
+    if (kStamp && tid == 0) st[1] = tstamp();
 
     // 2. pixel-parallel forward (the sum rasterizer's op sequence), clamp, loss
     float o[3] = {0.f, 0.f, 0.f};
@@ -190,7 +215,10 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
     {
         const float py = (float)pi, px = (float)pj;
         for (int k = 0; k < n; ++k) {
-            if (!((s_rows[k] >> (4 * w)) & 0xfu)) continue;  // no row of this wave reachable
+            // skip an entry that reaches none of this wave's 4 rows
+            const unsigned rc = s_rect[k];
+            if (rc == kNoRect || (int)((rc >> 12) & 15u) < 4 * w || (int)((rc >> 8) & 15u) > 4 * w + 3)
+                continue;
             const float4 G = s_geo[k];
             const float4 C = s_col[k];
             const float dy = G.y - py;
@@ -242,95 +270,122 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
     if (tid == 0)
         A.err[tile] = make_float2((s_err[0][0] + s_err[0][1]) + (s_err[0][2] + s_err[0][3]),
                                   (s_err[1][0] + s_err[1][1]) + (s_err[1][2] + s_err[1][3]));
+    if (kStamp && tid == 0) st[2] = tstamp();
     const int maxf = max(max(s_cnt[0], s_cnt[1]), max(s_cnt[2], s_cnt[3]));
     const int kend = min(n, maxf + 1);  // entries past every pixel's last contribute nothing
     if (kend <= 0) return;
 
-    // 3. entry-parallel backward: with E = next pow2 >= kend entries, thread t
-    // takes entry t % E against the pixels [E * (t / E), + E), so gradients
-    // accumulate in registers; the 256 / E groups are combined once per entry
-    const int lg = ceil_log2_i(kend);
-    const int E = 1 << lg;
-    const int e = tid & (E - 1);
-    const int p_begin = (tid >> lg) << lg;
-    float a_r = 0.f, a_g = 0.f, a_b = 0.f, a_c0 = 0.f, a_c1 = 0.f, a_c2 = 0.f;
-    float a_x = 0.f, a_y = 0.f, a_o = 0.f;
-    // rows of this thread's pixel group; skip an entry that reaches none
-    const unsigned grp_rows = E >= kTile ? (((2u << ((p_begin + E - 1) >> 4)) - 1u) &
-                                            ~((1u << (p_begin >> 4)) - 1u))
-                                         : (1u << (p_begin >> 4));
-    if (e < kend && (s_rows[e] & grp_rows)) {
-        const float4 G = s_geo[e];
-        const float4 C = s_col[e];
-        const float4 X = s_ext[e];
-        for (int pp = 0; pp < E; ++pp) {
-            const int p = p_begin + pp;
-            const float4 P = s_pix[p];
-            if (e > __float_as_int(P.w)) continue;
-            const float dx = G.x - (tx0 + (float)(p & 15));
-            const float dy = G.y - (ty0 + (float)(p >> 4));
-            const float s = splat_sigma_h(G.z, G.w, C.x, dx, dy);
-            const float vis = exp_neg(s);
-            const float al = fminf(1.0f, C.y * vis);
-            if (s < 0.0f || al < kAlphaMin) continue;
-            const float v_alpha = fmaf(X.x, P.z, fmaf(C.w, P.y, C.z * P.x));
-            const float v_sigma = (-C.y * vis) * v_alpha;
-            a_r = fmaf(al, P.x, a_r);
-            a_g = fmaf(al, P.y, a_g);
-            a_b = fmaf(al, P.z, a_b);
-            const float hs = 0.5f * v_sigma;
-            const float hsdx = hs * dx;
-            a_c0 = fmaf(hsdx, dx, a_c0);
-            a_c1 = fmaf(hsdx, dy, a_c1);
-            a_c2 = fmaf(hs * dy, dy, a_c2);
-            a_x = fmaf(v_sigma, fmaf(X.z, dx, G.w * dy), a_x);
-            a_y = fmaf(v_sigma, fmaf(G.w, dx, X.w * dy), a_y);
-            a_o = fmaf(vis, v_alpha, a_o);
-        }
-    }
-    if (E < 64) {
-        for (int off = 32; off >= E; off >>= 1) {
-            a_r += __shfl_xor(a_r, off, 64);
-            a_g += __shfl_xor(a_g, off, 64);
-            a_b += __shfl_xor(a_b, off, 64);
-            a_c0 += __shfl_xor(a_c0, off, 64);
-            a_c1 += __shfl_xor(a_c1, off, 64);
-            a_c2 += __shfl_xor(a_c2, off, 64);
-            a_x += __shfl_xor(a_x, off, 64);
-            a_y += __shfl_xor(a_y, off, 64);
-            a_o += __shfl_xor(a_o, off, 64);
-        }
-    }
-    const int S = E < 64 ? 64 : E;
-    __syncthreads();  // s_geo / s_col / s_pix read: the buffer becomes s_red
-    if (E >= 64 || lane < E) {
-        s_red[0][tid] = a_x;
-        s_red[1][tid] = a_y;
-        s_red[2][tid] = a_c0;
-        s_red[3][tid] = a_c1;
-        s_red[4][tid] = a_c2;
-        s_red[5][tid] = a_r;
-        s_red[6][tid] = a_g;
-        s_red[7][tid] = a_b;
-        s_red[8][tid] = a_o;
-    }
-    __syncthreads();
+    // 3. backward over compact work items: entry e's reachable rectangle
+    // (ellipse_rect) is cut into runs of kRun pixels (row-major), one item per
+    // thread per round, so lanes only evaluate (entry, pixel) pairs that can
+    // contribute; an item's 9 partial sums go to LDS and each entry adds its
+    // items' partials in item order (deterministic within the tile)
+    constexpr int kRun = 8;
+    int items = 0;
     if (tid < kend) {
-        const int reps = kT / S;
-#pragma unroll
-        for (int c = 0; c < 9; ++c) {
-            float val = s_red[c][tid];
-            for (int j = 1; j < reps; ++j) val += s_red[c][tid + j * S];
-            s_red[c][tid] = val;
+        const unsigned rc = s_rect[tid];
+        if (rc != kNoRect) {
+            const int rw = (int)((rc >> 4) & 15u) - (int)(rc & 15u) + 1;
+            const int rh = (int)((rc >> 12) & 15u) - (int)((rc >> 8) & 15u) + 1;
+            items = (rw * rh + kRun - 1) / kRun;
         }
+    }
+    // exclusive scan of items over the entries (wave scan + LDS)
+    int incl = items;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int u = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += u;
+    }
+    if (lane == 63) s_cnt[w] = incl;
+    __syncthreads();
+    int wave_off = 0;
+    for (int q = 0; q < w; ++q) wave_off += s_cnt[q];
+    const int total = (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
+    if (tid < kend) s_off[tid] = wave_off + incl - items;
+    if (tid == 0) s_off[kend] = total;
+    if (kStamp && tid == 0) st[3] = tstamp();
+    float acc[9];
+#pragma unroll
+    for (int c = 0; c < 9; ++c) acc[c] = 0.0f;
+    for (int base = 0; base < total; base += kT) {
+        __syncthreads();  // s_off written / the previous round's partials summed
+        const int item = base + tid;
+        float g[9];
+#pragma unroll
+        for (int c = 0; c < 9; ++c) g[c] = 0.0f;
+        if (item < total) {
+            // entry of this item: the last e with s_off[e] <= item
+            int lo = 0, hi = kend - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_off[mid] <= item) lo = mid;
+                else hi = mid - 1;
+            }
+            const int e = lo;
+            const unsigned rc = s_rect[e];
+            const int rx0 = (int)(rc & 15u), rw = (int)((rc >> 4) & 15u) - rx0 + 1;
+            const int ry0 = (int)((rc >> 8) & 15u);
+            const int area = rw * ((int)((rc >> 12) & 15u) - ry0 + 1);
+            const int q0 = (item - s_off[e]) * kRun;
+            int yy = q0 / rw, xx = q0 - yy * rw;
+            const float4 G = s_geo[e];
+            const float4 C = s_col[e];
+            const float4 X = s_ext[e];
+            for (int q = q0; q < q0 + kRun && q < area; ++q) {
+                const int pxl = (ry0 + yy) * kTile + rx0 + xx;
+                if (++xx == rw) {
+                    xx = 0;
+                    ++yy;
+                }
+                const float4 P = s_pix[pxl];
+                if (e > __float_as_int(P.w)) continue;
+                const float dx = G.x - (tx0 + (float)(pxl & 15));
+                const float dy = G.y - (ty0 + (float)(pxl >> 4));
+                const float sgm = splat_sigma_h(G.z, G.w, C.x, dx, dy);
+                const float vis = exp_neg(sgm);
+                const float al = fminf(1.0f, C.y * vis);
+                if (sgm < 0.0f || al < kAlphaMin) continue;
+                const float v_alpha = fmaf(X.x, P.z, fmaf(C.w, P.y, C.z * P.x));
+                const float v_sigma = (-C.y * vis) * v_alpha;
+                g[5] = fmaf(al, P.x, g[5]);
+                g[6] = fmaf(al, P.y, g[6]);
+                g[7] = fmaf(al, P.z, g[7]);
+                const float hs = 0.5f * v_sigma;
+                const float hsdx = hs * dx;
+                g[2] = fmaf(hsdx, dx, g[2]);
+                g[3] = fmaf(hsdx, dy, g[3]);
+                g[4] = fmaf(hs * dy, dy, g[4]);
+                g[0] = fmaf(v_sigma, fmaf(X.z, dx, G.w * dy), g[0]);
+                g[1] = fmaf(v_sigma, fmaf(G.w, dx, X.w * dy), g[1]);
+                g[8] = fmaf(vis, v_alpha, g[8]);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 9; ++c) s_part[c][tid] = g[c];
+        __syncthreads();
+        if (tid < kend) {
+            const int i0 = max(s_off[tid], base), i1 = min(s_off[tid + 1], base + kT);
+            for (int it = i0; it < i1; ++it) {
+#pragma unroll
+                for (int c = 0; c < 9; ++c) acc[c] += s_part[c][it - base];
+            }
+        }
+    }
+    __syncthreads();  // the last round's partials read: s_part becomes the entry sums
+    if (kStamp && tid == 0) st[4] = tstamp();
+    if (tid < kend) {
+#pragma unroll
+        for (int c = 0; c < 9; ++c) s_part[c][tid] = acc[c];
     }
     __syncthreads();
     // 16 lanes per entry, 9 of them add one float each into the splat's
     // 64-byte gradient record: one memory request per (splat, tile)
     for (int q = tid; q < kend * 16; q += kT) {
         const int e2 = q >> 4, c = q & 15;
-        if (c < 9) unsafeAtomicAdd(A.grad + (size_t)__float_as_int(s_ext[e2].y) * 16 + c, s_red[c][e2]);
+        if (c < 9) unsafeAtomicAdd(A.grad + (size_t)__float_as_int(s_ext[e2].y) * 16 + c, s_part[c][e2]);
     }
+    if (kStamp && tid == 0) st[5] = tstamp();
 }
 
 struct TrainSplatArgs {
@@ -355,10 +410,18 @@ __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
         // the loss: tiles' error sums in a fixed order, in double
         __shared__ double s_l[2][4];
         double s2 = 0.0, s1 = 0.0;
-        for (int t = threadIdx.x; t < A.ntiles; t += 256) {
-            const float2 e = A.err[t];
-            s2 += (double)e.x;
-            s1 += (double)e.y;
+        for (int t0 = threadIdx.x; t0 < A.ntiles; t0 += 8 * 256) {
+            float2 e[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {  // 8 independent loads in flight
+                const int t = t0 + 256 * k;
+                e[k] = t < A.ntiles ? A.err[t] : make_float2(0.f, 0.f);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                s2 += (double)e[k].x;
+                s1 += (double)e[k].y;
+            }
         }
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
@@ -553,7 +616,14 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     T.grad = reinterpret_cast<float *>(w.grad);
     T.err = w.err;
     T.out = render_out;
-    hipLaunchKernelGGL(train_tile_kernel, dim3(ntiles), dim3(kT), 0, s, T);
+    if (g_knobs[5] == 2 && g_debug_ptr) {  // diagnostic: per-tile stamps
+        T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
+        auto kfn = train_tile_kernel<true>;
+        hipLaunchKernelGGL(kfn, dim3(ntiles), dim3(kT), 0, s, T);
+    } else {
+        auto kfn = train_tile_kernel<false>;
+        hipLaunchKernelGGL(kfn, dim3(ntiles), dim3(kT), 0, s, T);
+    }
     rc = check_launch("train_step_sum: tiles");
     if (rc) return rc;
 

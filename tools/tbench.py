@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--foreach-adan", action="store_true")
     ap.add_argument("--op-by-op", action="store_true", help="disable the fused training step")
+    ap.add_argument("--stamps", action="store_true",
+                    help="also stamp the fused step's tile kernel (knob 5 = 2) and print phases")
     a = ap.parse_args()
     from gsvc_amd.frame import make_frame_model, synthetic_gt
     dev = torch.device("cuda:0")
@@ -42,6 +44,28 @@ def main():
         _, psnr = model.train_iter(gt, it)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.iters
+    if a.stamps:
+        import ctypes
+        import numpy as np
+        from gsvc_amd import _lib as L
+        lib = L.load()
+        ntiles = ((W + 15) // 16) * ((H + 15) // 16)
+        st = torch.zeros((ntiles, 8), dtype=torch.int64, device=dev)
+        lib.gsvc_debug_set_ptr(ctypes.c_void_p(st.data_ptr()))
+        lib.gsvc_debug_set(5, 2)
+        model.train_iter(gt, a.warmup + a.iters + 1)
+        torch.cuda.synchronize()
+        lib.gsvc_debug_set(5, 0)
+        lib.gsvc_debug_set_ptr(None)
+        t = st.cpu().numpy().astype(np.float64) * 0.01
+        t = t[t[:, 5] > 0]
+        t0 = t[:, 0].min()
+        q = lambda x: [round(float(np.percentile(x, p)), 2) for p in (0, 10, 50, 90, 100)]  # noqa
+        print(json.dumps(dict(stamps="percentiles 0/10/50/90/100 (us)", tiles=int(len(t)),
+                              start=q(t[:, 0] - t0), staged=q(t[:, 1] - t[:, 0]),
+                              forward=q(t[:, 2] - t[:, 1]), scan=q(t[:, 3] - t[:, 2]),
+                              items=q(t[:, 4] - t[:, 3]), atomics=q(t[:, 5] - t[:, 4]),
+                              life=q(t[:, 5] - t[:, 0]), end=q(t[:, 5] - t0))), flush=True)
     print(json.dumps(dict(splats=a.splats, fused_adan=model.fused_adan,
                           fused_train=model.fused_steps > 0, iters_per_s=round(1 / dt, 1),
                           ms_per_iter=round(1e3 * dt, 4), psnr=round(psnr, 3))), flush=True)
