@@ -116,21 +116,35 @@ def load_traffic(n_splats):
 
 
 def cpu_baseline(n_splats, seconds):
+    """The CPU oracle rendering the workload's frame on this host: 1 thread
+    (``value``) and every core this process may use (``all_cores``; the
+    per-tile loop of the sum rasterizer in OpenMP, the binning serial)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     means, L, colors, opac = O.synthetic_frame(n_splats, seed=0)
-    O.render_sum(means, L, colors, opac, H, W)  # warm-up / lib build
-    t0 = time.perf_counter()
-    frames = 0
-    while True:
-        O.render_sum(means, L, colors, opac, H, W)
-        frames += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": frames / el, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{frames} renders of one 1920x1080 / {n_splats}-splat frame "
-                      f"(project+bin+sort+sum-raster) by oracle/oracle.c, 1 thread, {el:.1f} s"}
+
+    def rate(threads, budget):
+        O.set_threads(threads)
+        O.render_sum(means, L, colors, opac, H, W)  # warm-up / lib build
+        t0 = time.perf_counter()
+        frames = 0
+        while True:
+            O.render_sum(means, L, colors, opac, H, W)
+            frames += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return frames, el
+
+    # the box's CPU share: OMP_NUM_THREADS (16 per GPU there), at most the affinity set
+    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
+    f1, e1 = rate(1, seconds)
+    fn, en = rate(cores, max(2.0, seconds / 3))
+    O.set_threads(1)
+    return {"value": f1 / e1, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{f1} renders of one 1920x1080 / {n_splats}-splat frame "
+                      f"(project+bin+sort+sum-raster) by oracle/oracle.c, 1 thread, {e1:.1f} s",
+            "all_cores": {"value": fn / en, "cores": cores,
+                          "sample": f"{fn} renders, OpenMP per-tile rasterizer, {en:.1f} s"}}
 
 
 def video_decode(device, frames=8, splats=10000, steps=50, warmup=5):

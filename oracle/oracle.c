@@ -34,6 +34,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <limits.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define TILE 16
 #define TILE_PIX 256
@@ -236,6 +239,19 @@ static inline float splat_sigma(float a, float b, float c, float dx, float dy) {
     return fmaf(q, dx, cq);
 }
 
+/* Threads of the per-tile loops below (OpenMP; 1 unless set -- tiles are
+ * independent, so any count gives the same results).  Used by bench.py's
+ * all-core CPU baseline. */
+int oracle_set_threads(int n) {
+#ifdef _OPENMP
+    omp_set_num_threads(n > 0 ? n : 1);
+    return n > 0 ? n : 1;
+#else
+    (void)n;
+    return 1;
+#endif
+}
+
 /* forward.cu:512-627.  One tile = 16x16 pixels; only the first 256 sorted
  * entries of a tile are blended (forward.cu:569-571,613). */
 void oracle_raster_sum_forward(int tbx, int tby, int img_w, int img_h,
@@ -243,37 +259,37 @@ void oracle_raster_sum_forward(int tbx, int tby, int img_w, int img_h,
                                const float *xys, const float *conics,
                                const float *colors, const float *opac,
                                float *out_img, float *final_Ts, int *final_idx) {
-    for (int ty = 0; ty < tby; ++ty)
-        for (int tx = 0; tx < tbx; ++tx) {
-            int tile = ty * tbx + tx;
-            int r0 = bins[2 * tile], r1 = bins[2 * tile + 1];
-            int end = r1;
-            if (end - r0 > TILE_PIX) end = r0 + TILE_PIX;
-            for (int ly = 0; ly < TILE; ++ly)
-                for (int lx = 0; lx < TILE; ++lx) {
-                    int i = ty * TILE + ly, j = tx * TILE + lx;
-                    if (i >= img_h || j >= img_w) continue;
-                    float px = (float)j, py = (float)i;
-                    float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f;
-                    int last = 0;
-                    for (int k = r0; k < end; ++k) {
-                        int g = ids[k];
-                        float dx = xys[2 * g] - px, dy = xys[2 * g + 1] - py;
-                        float s = splat_sigma(conics[3 * g], conics[3 * g + 1], conics[3 * g + 2], dx, dy);
-                        float e = exp2f(s * NEG_LOG2E);
-                        float alpha = fminf(1.0f, opac[g] * e);
-                        if (s < 0.0f || alpha < 1.0f / 255.0f) continue;
-                        acc0 = fmaf(colors[3 * g], alpha, acc0);
-                        acc1 = fmaf(colors[3 * g + 1], alpha, acc1);
-                        acc2 = fmaf(colors[3 * g + 2], alpha, acc2);
-                        last = k;
-                    }
-                    size_t p = (size_t)i * (size_t)img_w + (size_t)j;
-                    out_img[3 * p] = acc0; out_img[3 * p + 1] = acc1; out_img[3 * p + 2] = acc2;
-                    final_Ts[p] = 1.0f;
-                    final_idx[p] = last;
+#pragma omp parallel for schedule(dynamic, 8)
+    for (int tile = 0; tile < tbx * tby; ++tile) {
+        int ty = tile / tbx, tx = tile - ty * tbx;
+        int r0 = bins[2 * tile], r1 = bins[2 * tile + 1];
+        int end = r1;
+        if (end - r0 > TILE_PIX) end = r0 + TILE_PIX;
+        for (int ly = 0; ly < TILE; ++ly)
+            for (int lx = 0; lx < TILE; ++lx) {
+                int i = ty * TILE + ly, j = tx * TILE + lx;
+                if (i >= img_h || j >= img_w) continue;
+                float px = (float)j, py = (float)i;
+                float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f;
+                int last = 0;
+                for (int k = r0; k < end; ++k) {
+                    int g = ids[k];
+                    float dx = xys[2 * g] - px, dy = xys[2 * g + 1] - py;
+                    float s = splat_sigma(conics[3 * g], conics[3 * g + 1], conics[3 * g + 2], dx, dy);
+                    float e = exp2f(s * NEG_LOG2E);
+                    float alpha = fminf(1.0f, opac[g] * e);
+                    if (s < 0.0f || alpha < 1.0f / 255.0f) continue;
+                    acc0 = fmaf(colors[3 * g], alpha, acc0);
+                    acc1 = fmaf(colors[3 * g + 1], alpha, acc1);
+                    acc2 = fmaf(colors[3 * g + 2], alpha, acc2);
+                    last = k;
                 }
-        }
+                size_t p = (size_t)i * (size_t)img_w + (size_t)j;
+                out_img[3 * p] = acc0; out_img[3 * p + 1] = acc1; out_img[3 * p + 2] = acc2;
+                final_Ts[p] = 1.0f;
+                final_idx[p] = last;
+            }
+    }
 }
 
 /* backward.cu:696-862.  Gradients are accumulated in double (the GPU sums by

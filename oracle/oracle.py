@@ -46,7 +46,14 @@ def lib():
         ):
             build()
         _lib = ctypes.CDLL(_LIB_PATH)
+        _lib.oracle_set_threads(1)  # single-threaded unless a caller asks for more
     return _lib
+
+
+def set_threads(n: int) -> int:
+    """OpenMP threads of the per-tile oracle loops (sum forward); results do
+    not depend on it.  Returns the count in effect."""
+    return int(lib().oracle_set_threads(int(n)))
 
 
 def _p(a: np.ndarray):
