@@ -105,14 +105,18 @@ def composite_bytes(model):
                               model.tile_bounds)
 
 
-def load_traffic(n_splats):
+def load_profile(n_splats):
+    """(PMC HBM bytes per launch, rocprofv3 kernel-trace average duration in
+    us) of the composite kernel from profiles/pmc_traffic.json (written by
+    tools/gpu_bench_prof.sh from rocprofv3 runs of this same command)."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            rec = json.load(f)
-        return rec.get(str(n_splats), {}).get("rasterize_sum_forward_bytes_per_launch")
+            rec = json.load(f).get(str(n_splats), {})
+        return (rec.get("rasterize_sum_forward_bytes_per_launch"),
+                rec.get("rasterize_sum_forward_trace_avg_us"))
     except (OSError, ValueError):
-        return None
+        return None, None
 
 
 def cpu_baseline(n_splats, seconds):
@@ -261,10 +265,16 @@ def main():
     nbytes, shape = composite_bytes(model)
     avg_ms = sum(kt) / len(kt)
     achieved = nbytes / (avg_ms * 1e-3) / 1e9
+    traffic, trace_us = load_profile(args.splats)
     roof = {"kernel": "rasterize_sum_forward", "bound": "hbm", "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": load_traffic(args.splats), "avg_kernel_us": round(avg_ms * 1e3, 2),
+            "traffic": traffic, "avg_kernel_us": round(avg_ms * 1e3, 2),
             "algorithmic_bytes_per_launch": nbytes, "shape": shape}
+    if trace_us:
+        # the same kernel's duration in the committed rocprofv3 kernel trace: the
+        # HIP events above include ~2-3 us of event-packet / dispatch latency
+        roof["trace_avg_kernel_us"] = round(trace_us, 2)
+        roof["frac_by_trace"] = round(nbytes / (trace_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,

@@ -93,12 +93,15 @@ def main():
     a = ap.parse_args()
     if a.pmc_dirs:
         print(json.dumps(pmc_all(a.pmc_dirs), indent=1))
+    rec = {}
     if a.trace:
         st = trace_stats(a.trace)
         for name, s in sorted(st.items(), key=lambda kv: -kv[1]["avg_us"] * kv[1]["calls"]):
             print(f"{s['calls']:6d}  avg {s['avg_us']:9.2f} us  med {s['median_us']:9.2f}  "
                   f"min {s['min_us']:9.2f}  {name[:110]}")
-    rec = {}
+            k = _short(name)
+            if k:
+                rec.setdefault(k, {})["trace_avg_us"] = s["avg_us"]
     if a.fetch:
         for k, v in pmc_per_launch(a.fetch, "FETCH_SIZE").items():
             rec.setdefault(k, {})["fetch_bytes"] = 2.0 * v * 1024.0
@@ -117,9 +120,12 @@ def main():
         for k, r in rec.items():
             if "fetch_bytes" in r and "write_bytes" in r:
                 entry[f"{k}_bytes_per_launch"] = r["fetch_bytes"] + r["write_bytes"]
-            entry[f"{k}_pmc"] = r
+                entry[f"{k}_pmc"] = {x: r[x] for x in ("fetch_bytes", "write_bytes")}
+            if "trace_avg_us" in r:
+                entry[f"{k}_trace_avg_us"] = r["trace_avg_us"]
         entry["note"] = ("FETCH_SIZE x2 (gfx950 half-count, MI355X_MICROARCH.md HBM) + WRITE_SIZE; "
-                         "KiB -> bytes; average per dispatch")
+                         "KiB -> bytes; average per dispatch; trace_avg_us: rocprofv3 "
+                         "--kernel-trace duration of the same command")
         with open(a.out, "w") as fh:
             json.dump(allrec, fh, indent=1)
 
