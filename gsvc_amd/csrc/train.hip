@@ -130,9 +130,10 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
     // LDS: geo / col / pix, reused as the 9 x 256 gradient reduction buffer
     // once the backward loop is done (16.5 KB per workgroup)
     __shared__ float4 s_buf[3 * kT];
-    __shared__ float4 s_ext[kT];     // b, id bits, a, c
+    __shared__ float2 s_ext[kT];     // b, id bits
     __shared__ unsigned s_rect[kT];  // pixels of the tile the entry can reach (ellipse_rect)
-    __shared__ float s_part[9][kT];  // backward: per-item partial gradients
+    constexpr int kHalf = kT / 2;
+    __shared__ float s_part[9][kHalf];  // backward: partial gradients of half a round of items
     __shared__ int s_off[kT + 1];    // backward: first work item of each entry
     __shared__ int s_cnt[4];
     __shared__ float s_err[2][4];
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
     if (tid < n) {
         s_geo[rank] = r0;
         s_col[rank] = r1;
-        s_ext[rank] = r2;
+        s_ext[rank] = make_float2(r2.x, r2.y);
         s_rect[rank] = ellipse_rect(r0.x, r0.y, r2.z, r0.w, r2.w, r1.y, tx0, ty0);
     }
     __syncthreads();
@@ -331,7 +332,9 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
             int yy = q0 / rw, xx = q0 - yy * rw;
             const float4 G = s_geo[e];
             const float4 C = s_col[e];
-            const float4 X = s_ext[e];
+            const float2 X = s_ext[e];
+            // full conic a, c: 2 * (a / 2) is exact for every normal float
+            const float fa = 2.0f * G.z, fc = 2.0f * C.x;
             for (int q = q0; q < q0 + kRun && q < area; ++q) {
                 const int pxl = (ry0 + yy) * kTile + rx0 + xx;
                 if (++xx == rw) {
@@ -356,34 +359,44 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
                 g[2] = fmaf(hsdx, dx, g[2]);
                 g[3] = fmaf(hsdx, dy, g[3]);
                 g[4] = fmaf(hs * dy, dy, g[4]);
-                g[0] = fmaf(v_sigma, fmaf(X.z, dx, G.w * dy), g[0]);
-                g[1] = fmaf(v_sigma, fmaf(G.w, dx, X.w * dy), g[1]);
+                g[0] = fmaf(v_sigma, fmaf(fa, dx, G.w * dy), g[0]);
+                g[1] = fmaf(v_sigma, fmaf(G.w, dx, fc * dy), g[1]);
                 g[8] = fmaf(vis, v_alpha, g[8]);
             }
         }
+        // the two halves of the round publish their partials in turn (4.5 KB
+        // of LDS instead of 9 KB: one more workgroup per CU)
+        for (int h = 0; h < 2; ++h) {
+            const int hb = base + h * kHalf;
+            if (hb >= total) break;
+            if (h == 1) __syncthreads();  // the first half consumed
+            if ((tid >> 7) == h) {
 #pragma unroll
-        for (int c = 0; c < 9; ++c) s_part[c][tid] = g[c];
-        __syncthreads();
-        if (tid < kend) {
-            const int i0 = max(s_off[tid], base), i1 = min(s_off[tid + 1], base + kT);
-            for (int it = i0; it < i1; ++it) {
+                for (int c = 0; c < 9; ++c) s_part[c][tid - h * kHalf] = g[c];
+            }
+            __syncthreads();
+            if (tid < kend) {
+                const int i0 = max(s_off[tid], hb), i1 = min(s_off[tid + 1], hb + kHalf);
+                for (int it = i0; it < i1; ++it) {
 #pragma unroll
-                for (int c = 0; c < 9; ++c) acc[c] += s_part[c][it - base];
+                    for (int c = 0; c < 9; ++c) acc[c] += s_part[c][it - hb];
+                }
             }
         }
     }
-    __syncthreads();  // the last round's partials read: s_part becomes the entry sums
+    __syncthreads();  // every item read: the geo / col / pix buffer holds the entry sums
     if (kStamp && tid == 0) st[4] = tstamp();
+    float(*s_sum)[kT] = reinterpret_cast<float(*)[kT]>(s_buf);
     if (tid < kend) {
 #pragma unroll
-        for (int c = 0; c < 9; ++c) s_part[c][tid] = acc[c];
+        for (int c = 0; c < 9; ++c) s_sum[c][tid] = acc[c];
     }
     __syncthreads();
     // 16 lanes per entry, 9 of them add one float each into the splat's
     // 64-byte gradient record: one memory request per (splat, tile)
     for (int q = tid; q < kend * 16; q += kT) {
         const int e2 = q >> 4, c = q & 15;
-        if (c < 9) unsafeAtomicAdd(A.grad + (size_t)__float_as_int(s_ext[e2].y) * 16 + c, s_part[c][e2]);
+        if (c < 9) unsafeAtomicAdd(A.grad + (size_t)__float_as_int(s_ext[e2].y) * 16 + c, s_sum[c][e2]);
     }
     if (kStamp && tid == 0) st[5] = tstamp();
 }
