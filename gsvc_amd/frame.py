@@ -20,7 +20,7 @@ from .adan import Adan
 from .project_gaussians_2d import project_gaussians_2d
 from .rasterize_sum import rasterize_gaussians_sum
 from .render import render_frame_sum
-from .train import LOSS_KIND, train_step_sum
+from .train import LOSS_KIND, BoundStep
 
 
 def loss_fn(pred, target, loss_type="L2", lambda_value=0.7):
@@ -76,6 +76,7 @@ class GaussianVideoFrame(nn.Module):
         # whole train_iter as one fused call (gsvc_amd/train.py) where it applies
         self.fused_train = kwargs.get("fused_train", str(self.device).startswith("cuda"))
         self.fused_steps = 0
+        self._bound_step = None
         self.update_optimizer()
         self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=20000, gamma=0.5)
 
@@ -247,9 +248,15 @@ class GaussianVideoFrame(nn.Module):
         gt = gt_image.detach()
         if gt.dtype != torch.float32 or not gt.is_contiguous():
             gt = gt.float().contiguous()
-        losses = train_step_sum(self._xyz.data, self._cholesky.data, self._features_dc.data,
-                                self.rgb_W.data, rgbw_train, self.cholesky_bound, self.background,
-                                gt, self.H, self.W, self.loss_type, state, hparams, flags)
+        # the step bound to these tensors: pointers built once, rebuilt when any
+        # parameter, state tensor or constant object changes
+        bound = (self._xyz, self._cholesky, self._features_dc, self.rgb_W, self.cholesky_bound,
+                 self.background, *state)
+        bs = self._bound_step
+        if bs is None or bs.rgbw_train != int(rgbw_train) or not bs.matches(bound):
+            bs = self._bound_step = BoundStep(*bound[:4], rgbw_train, *bound[4:6], self.H, self.W,
+                                              self.loss_type, state)
+        losses = bs(gt, hparams, flags)
         loss = losses[LOSS_KIND[self.loss_type]]
         psnr = 10 * math.log10(1.0 / float(losses[0]))
         # the step ran (keeps StepLR's call-order check quiet; the scheduler may

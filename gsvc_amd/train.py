@@ -30,16 +30,21 @@ class _TrainWorkspace:
         self.hw = None
         self.dirty = True
         self.frame = 0
+        self.shape = None
 
 
 _workspaces = {}
+_raw_stream = torch._C._cuda_getCurrentRawStream  # current stream handle, no Stream object
 
 
 def _workspace(dev: torch.device, n: int, H: int, W: int) -> _TrainWorkspace:
-    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    key = (dev.index, _raw_stream(dev.index))
     ws = _workspaces.get(key)
     if ws is None:
         ws = _workspaces[key] = _TrainWorkspace()
+    if ws.shape == (n, H, W) and not ws.dirty:
+        return ws
+    ws.shape = (n, H, W)
     need = L.size("gsvc_train_step_workspace_bytes", n, H, W)
     if ws.buf is None or ws.buf.numel() < need:
         ws.buf = torch.empty((need,), dtype=torch.uint8, device=dev)
@@ -64,6 +69,60 @@ def _f32_ptr(t: Optional[Tensor], name: str, numel: int) -> int:
     if t.numel() != numel:
         raise ValueError(f"{name} must have {numel} elements, got {t.numel()}")
     return t.data_ptr()
+
+
+class BoundStep:
+    """A fused training step bound to fixed tensors (parameters, Adan state,
+    constants): pointers and the ctypes state array are built once, so a call
+    costs one C call plus the loss tensor.  The owner rebuilds it when any
+    bound tensor object changes (``matches``).  Parameters are updated in place
+    through their storage (as ``p.data`` would be)."""
+
+    def __init__(self, xyz, cholesky, features, rgb_w, rgb_w_trainable, cholesky_bound,
+                 background, H, W, loss_type, adan_state):
+        n = xyz.shape[0]
+        self.tensors = (xyz, cholesky, features, rgb_w, cholesky_bound, background, *adan_state)
+        self.n, self.H, self.W = n, int(H), int(W)
+        self.dev = xyz.device
+        self.kind = LOSS_KIND[loss_type]
+        self.rgbw_train = 1 if rgb_w_trainable else 0
+        self.p = [_f32_ptr(xyz, "xyz", 2 * n), _f32_ptr(cholesky, "cholesky", 3 * n),
+                  _f32_ptr(cholesky_bound, "cholesky_bound", 3), _f32_ptr(features, "features", 3 * n),
+                  _f32_ptr(rgb_w, "rgb_w", n), _f32_ptr(background, "background", 3)]
+        self.state = (ctypes.c_void_p * 16)()
+        numels = [2 * n, 3 * n, 3 * n, n]
+        for k, t in enumerate(adan_state):
+            self.state[k] = _f32_ptr(t, "adan_state", numels[k // 4]) or None
+        self.hp = (ctypes.c_double * 10)()
+        self.fn = L.load().gsvc_train_step_sum
+
+    def matches(self, tensors) -> bool:
+        # identity, plus the parameters' storage (Module.to / ``p.data = ...``
+        # swap it under the same object)
+        return (len(tensors) == len(self.tensors)
+                and all(a is b for a, b in zip(tensors, self.tensors))
+                and all(t is None or t.data_ptr() == p
+                        for t, p in zip(tensors[:4], (self.p[0], self.p[1], self.p[3], self.p[4]))))
+
+    def __call__(self, gt: Tensor, adan_hparams, adan_flags: int) -> Tensor:
+        if not (gt.is_cuda and gt.dtype is torch.float32 and gt.is_contiguous()
+                and gt.numel() == 3 * self.H * self.W):
+            raise RuntimeError("gt must be a contiguous float32 CUDA tensor of 3*H*W elements")
+        for k, x in enumerate(adan_hparams):
+            self.hp[k] = x
+        ws = _workspace(self.dev, self.n, self.H, self.W)
+        loss = torch.empty((2,), dtype=torch.float32, device=self.dev)
+        p = self.p
+        rc = self.fn(self.n, p[0], p[1], p[2], p[3], p[4], self.rgbw_train, p[5], gt.data_ptr(),
+                     self.H, self.W, self.kind, ws.frame, self.state, self.hp, int(adan_flags),
+                     loss.data_ptr(), None, None, ws.buf_ptr, ws.buf.numel(),
+                     _raw_stream(self.dev.index))
+        if rc != 0:
+            ws.dirty = True
+            msg = L.load().gsvc_last_error().decode(errors="replace")
+            raise RuntimeError(f"gsvc_train_step_sum failed (status {rc}): {msg}")
+        ws.frame += 1
+        return loss
 
 
 def train_step_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, rgb_w: Optional[Tensor],
@@ -108,7 +167,7 @@ def train_step_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, rgb_w: Optio
     rc = L.load().gsvc_train_step_sum(
         n, p_xyz, p_chol, p_bound, p_feat, p_rgbw, 1 if rgb_w_trainable else 0, p_bg, p_gt, H, W,
         LOSS_KIND[loss_type], ws.frame, state, hp, int(adan_flags), loss.data_ptr(), p_render,
-        p_grads, ws.buf_ptr, ws.buf.numel(), torch.cuda.current_stream(dev).cuda_stream)
+        p_grads, ws.buf_ptr, ws.buf.numel(), _raw_stream(dev.index))
     if rc != 0:
         ws.dirty = True
         msg = L.load().gsvc_last_error().decode(errors="replace")
