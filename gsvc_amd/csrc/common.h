@@ -38,6 +38,16 @@ __device__ __forceinline__ int xcd_remap(int orig, int count) {
 }
 
 // v_cvt_i32_f32 semantics: truncate, saturate, NaN -> 0.
+// 16-byte write-through store (sc1: agent scope): the line leaves the XCD's L2
+// as it is written, so the end-of-kernel release has no dirty line of it to
+// write back; for data the NEXT kernel reads from other XCDs (MI355X_MICROARCH
+// "publish-large").  A vector store; never a scalar-cache one.
+__device__ __forceinline__ void store_wt(float4 *p, float4 v) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const f4 x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+}
+
 __device__ __forceinline__ int cvt_i32(float f) {
     if (f != f) return 0;
     if (f >= 2147483648.0f) return 2147483647;

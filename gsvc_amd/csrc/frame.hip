@@ -38,7 +38,7 @@ template <int K>
 __device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, int tby, int sub,
                                            float4 r0, float4 r1, float4 r2,
                                            unsigned *__restrict__ counts,
-                                           float4 *__restrict__ slab) {
+                                           float4 *__restrict__ slab, int wt) {
     unsigned x0, y0, x1, y1;
     tile_bbox(cx, cy, (float)r, tbx, tby, x0, y0, x1, y1);
     if (x1 <= x0 || y1 <= y0) return 0;
@@ -55,9 +55,15 @@ __device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, i
         for (int k = 0; k < kBatch; ++k)
             if (k < cnt && sl[k] < (unsigned)kTilePix) {
                 float4 *d = slab + ((size_t)tl[k] * kTilePix + sl[k]) * 3;
-                d[0] = r0;
-                d[1] = r1;
-                d[2] = r2;
+                if (wt) {
+                    store_wt(d, r0);
+                    store_wt(d + 1, r1);
+                    store_wt(d + 2, r2);
+                } else {
+                    d[0] = r0;
+                    d[1] = r1;
+                    d[2] = r2;
+                }
             }
         hits += cnt;
         cnt = 0;
@@ -97,7 +103,8 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
     int tby, float2 *__restrict__ xys, int *__restrict__ radii, float4 *__restrict__ rec,
     unsigned *__restrict__ counts, float4 *__restrict__ slab, int *__restrict__ m_acc,
     int *__restrict__ m_clear, float4 *__restrict__ grad_zero, long long *stamps,
-    const int *__restrict__ frame_off, int counts_stride, int m_stride, size_t slab_stride) {
+    const int *__restrict__ frame_off, int counts_stride, int m_stride, size_t slab_stride,
+    int wt) {
     __shared__ int s_hits[kProjThreads / 64];
     // batched frames (grid.y): this block's frame owns splats [begin, end)
     int begin = 0, end = n;
@@ -143,7 +150,13 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int q = sub; q < 4; q += K) {
-            if (q < 3) rec[3 * i + q] = q == 0 ? r0 : (q == 1 ? r1 : r2);
+            if (q < 3) {
+                const float4 rq = q == 0 ? r0 : (q == 1 ? r1 : r2);
+                if (wt)
+                    store_wt(rec + 3 * i + q, rq);
+                else
+                    rec[3 * i + q] = rq;
+            }
             if (q == 3) {
                 xys[i] = P.xy;
                 radii[i] = P.rad;
@@ -152,7 +165,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
         }
         if (kStamp && (threadIdx.x & 63) == 0) st[1] = proj_stamp();
         if (P.rad > 0)
-            hits = slab_insert<K>(P.xy.x, P.xy.y, P.rad, tbx, tby, sub, r0, r1, r2, counts, slab);
+            hits = slab_insert<K>(P.xy.x, P.xy.y, P.rad, tbx, tby, sub, r0, r1, r2, counts, slab, wt);
     }
     if (kStamp) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -220,6 +233,10 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
     // measured at 1080p: equal at 10k splats, 1 lane fastest at 50k)
     const int k = g_knobs[4] == 2 || g_knobs[4] == 4 || g_knobs[4] == 8 ? g_knobs[4] : 1;
     const size_t slab_stride = (size_t)3 * kTilePix * (size_t)(tbx * tby);
+    // plain record stores; A/B knob 6 = 1 writes them through (sc1): measured
+    // slower (projection 7.1 -> 9.8 us at 10k: each scattered 16-byte sc1 store
+    // is its own fabric write) and no faster for the composite's loads
+    const int wt = g_knobs[6] == 1 ? 1 : 0;
     if (frames > 1 && !frame_off) return set_error(GSVC_ERR_ARG, "frame projection: frame offsets");
     const int per = frames > 1 ? max_frame_n : n;
     if (frames > 1 && per <= 0) {
@@ -238,7 +255,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
                            chol_bound, feat, rgb_w, opac, hw, hh, tbx, tby, w.xys, w.radii,      \
                            w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero, nullptr,      \
                            frames > 1 ? frame_off : nullptr, f.counts_stride, f.m_stride,        \
-                           slab_stride);                                                         \
+                           slab_stride, wt);                                                     \
     }
         if (g_knobs[5] == 1 && g_debug_ptr) {  // diagnostic: per-wave stamps
             auto kfn = frame_project_kernel<1, true>;
@@ -247,7 +264,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
                                w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero,
                                reinterpret_cast<long long *>(g_debug_ptr),
                                frames > 1 ? frame_off : nullptr, f.counts_stride, f.m_stride,
-                               slab_stride);
+                               slab_stride, wt);
             return check_launch("frame projection");
         }
         switch (k) {

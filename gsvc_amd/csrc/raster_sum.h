@@ -15,7 +15,7 @@ struct SumFwdArgs {
     int tbx, img_w, img_h, ntiles, sparse_max, layout;
     bool vec;      // HWC: W % 4 == 0 and 16-byte aligned outputs
     bool vec_chw;  // CHW: W % 4 == 0, H*W % 4 == 0, 16-byte aligned
-    bool nt_store;  // CHW: nontemporal plane stores (gsvc_debug_set(7))
+    int store_policy;  // CHW plane stores: kStore* (gsvc_debug_set(7) selects)
     const int *m_dev;  // device num_intersects (NULL: > 0); 0 -> background
     const float *bg;
     const int *ids;

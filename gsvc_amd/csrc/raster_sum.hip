@@ -127,13 +127,39 @@ __device__ __forceinline__ bool ellipse_hits_rect(float x, float y, float a, flo
 
 typedef float v4f __attribute__((ext_vector_type(4)));
 
-// Plane stores of the render layout; ``nt``: nontemporal (streaming) stores.
-__device__ __forceinline__ void st_f4(float *p, float a, float b, float c, float d, bool nt) {
-    if (nt) {
-        const v4f v = {a, b, c, d};
-        __builtin_nontemporal_store(v, reinterpret_cast<v4f *>(p));
-    } else {
-        *reinterpret_cast<float4 *>(p) = make_float4(a, b, c, d);
+// Plane stores of the render layout, by cache policy: streaming write-through
+// (nt sc1, production: the lines leave L2 as they are written, so the
+// end-of-kernel release has ~25 MB less to write back -- composite 10.6 ->
+// 9.5 us at 1080p), plain (write-back L2), sc1, sc0 sc1, or nt alone.
+enum { kStoreNtSc1 = 0, kStorePlain = 1, kStoreSc1 = 2, kStoreSc01 = 3, kStoreNt = 4 };
+
+__device__ __forceinline__ void st_f4(float *p, float a, float b, float c, float d, int policy) {
+    const v4f v = {a, b, c, d};
+    switch (policy) {
+    case kStoreNt: __builtin_nontemporal_store(v, reinterpret_cast<v4f *>(p)); break;
+    case kStoreSc1: asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory"); break;
+    case kStoreSc01:
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+        break;
+    case kStoreNtSc1:
+        asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+        break;
+    default: *reinterpret_cast<v4f *>(p) = v; break;
+    }
+}
+
+__device__ __forceinline__ void st_f2(float *p, float a, float b, int policy) {
+    const v2f v = {a, b};
+    switch (policy) {
+    case kStoreNt: __builtin_nontemporal_store(v, reinterpret_cast<v2f *>(p)); break;
+    case kStoreSc1: asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory"); break;
+    case kStoreSc01:
+        asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+        break;
+    case kStoreNtSc1:
+        asm volatile("global_store_dwordx2 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+        break;
+    default: *reinterpret_cast<v2f *>(p) = v; break;
     }
 }
 
@@ -361,9 +387,9 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         if (pi < A.img_h) {
             const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
             float *o = A.out + (size_t)pi * (size_t)A.img_w + (size_t)pj;
-            st_f4(o, clamp01(r0), clamp01(r1), clamp01(r2), clamp01(r3), A.nt_store);
-            st_f4(o + hw, clamp01(g0), clamp01(g1), clamp01(g2), clamp01(g3), A.nt_store);
-            st_f4(o + 2 * hw, clamp01(b0), clamp01(b1), clamp01(b2), clamp01(b3), A.nt_store);
+            st_f4(o, clamp01(r0), clamp01(r1), clamp01(r2), clamp01(r3), A.store_policy);
+            st_f4(o + hw, clamp01(g0), clamp01(g1), clamp01(g2), clamp01(g3), A.store_policy);
+            st_f4(o + 2 * hw, clamp01(b0), clamp01(b1), clamp01(b2), clamp01(b3), A.store_policy);
             if (A.final_idx)
                 *reinterpret_cast<int4 *>(A.final_idx + (o - A.out)) = make_int4(l0, l1, l2, l3);
         }
@@ -499,17 +525,9 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
         if (pi < A.img_h) {
             const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
             float *o = A.out + (size_t)pi * (size_t)A.img_w + (size_t)pj;
-            if (A.nt_store) {
-                __builtin_nontemporal_store((v2f){clamp01(ar.x), clamp01(ar.y)}, reinterpret_cast<v2f *>(o));
-                __builtin_nontemporal_store((v2f){clamp01(ag.x), clamp01(ag.y)},
-                                            reinterpret_cast<v2f *>(o + hw));
-                __builtin_nontemporal_store((v2f){clamp01(ab.x), clamp01(ab.y)},
-                                            reinterpret_cast<v2f *>(o + 2 * hw));
-            } else {
-                *reinterpret_cast<float2 *>(o) = make_float2(clamp01(ar.x), clamp01(ar.y));
-                *reinterpret_cast<float2 *>(o + hw) = make_float2(clamp01(ag.x), clamp01(ag.y));
-                *reinterpret_cast<float2 *>(o + 2 * hw) = make_float2(clamp01(ab.x), clamp01(ab.y));
-            }
+            st_f2(o, clamp01(ar.x), clamp01(ar.y), A.store_policy);
+            st_f2(o + hw, clamp01(ag.x), clamp01(ag.y), A.store_policy);
+            st_f2(o + 2 * hw, clamp01(ab.x), clamp01(ab.y), A.store_policy);
             if (A.final_idx) *reinterpret_cast<int2 *>(A.final_idx + (o - A.out)) = make_int2(l0, l1);
         }
         return;
@@ -796,7 +814,7 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
     A.vec = (A.img_w % 4 == 0) && (((uintptr_t)A.out & 15) == 0) &&
             (((uintptr_t)A.final_idx & 15) == 0) && (((uintptr_t)A.final_Ts & 15) == 0);
     A.vec_chw = A.vec && (((size_t)A.img_w * (size_t)A.img_h) % 4 == 0);
-    A.nt_store = g_knobs[7] == 0;  // streaming stores unless disabled (A/B knob 7)
+    A.store_policy = g_knobs[7];  // kStoreNtSc1 unless an A/B run selects another (knob 7)
     const int ntiles = A.ntiles;
     int mode = g_knobs[0];
     if (mode == 0)
