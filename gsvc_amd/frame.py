@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import msssim
 from .adan import Adan
 from .project_gaussians_2d import project_gaussians_2d
 from .rasterize_sum import rasterize_gaussians_sum
@@ -24,8 +25,11 @@ from .train import LOSS_KIND, BoundStep
 
 
 def loss_fn(pred, target, loss_type="L2", lambda_value=0.7):
-    """utils.py:21-41 for the losses that need no pytorch_msssim (absent here;
-    the SSIM variants are parity-unpinned and not provided)."""
+    """utils.py:21-41.  The SSIM terms are gsvc_amd.msssim (pytorch_msssim's
+    ssim / ms_ssim on the gfx950 kernels, CUDA tensors only); as in the
+    reference they need 4-d inputs, so train_iter's squeezed [3,H,W] images
+    raise for them there (GaussianSplats_Represent.py:194) and pre_train_iter's
+    NCHW ones (:213) work."""
     target = target.detach()
     pred = pred.float()
     target = target.float()
@@ -33,9 +37,24 @@ def loss_fn(pred, target, loss_type="L2", lambda_value=0.7):
         return F.mse_loss(pred, target)
     if loss_type == "L1":
         return F.l1_loss(pred, target)
+    if loss_type == "SSIM":
+        return 1 - msssim.ssim(pred, target, data_range=1, size_average=True)
+    if loss_type == "Fusion1":
+        return lambda_value * F.mse_loss(pred, target) + (1 - lambda_value) * (
+            1 - msssim.ssim(pred, target, data_range=1, size_average=True))
+    if loss_type == "Fusion2":
+        return lambda_value * F.l1_loss(pred, target) + (1 - lambda_value) * (
+            1 - msssim.ssim(pred, target, data_range=1, size_average=True))
     if loss_type == "Fusion3":
         return lambda_value * F.mse_loss(pred, target) + (1 - lambda_value) * F.l1_loss(pred, target)
-    raise NotImplementedError(f"loss_type {loss_type!r} needs pytorch_msssim (not available)")
+    if loss_type == "Fusion4":
+        return lambda_value * F.l1_loss(pred, target) + (1 - lambda_value) * (
+            1 - msssim.ms_ssim(pred, target, data_range=1, size_average=True))
+    if loss_type == "Fusion_hinerv":
+        return lambda_value * F.l1_loss(pred, target) + (1 - lambda_value) * (
+            1 - msssim.ms_ssim(pred, target, data_range=1, size_average=True, win_size=5))
+    # the reference falls through to `return loss` with loss unassigned
+    raise UnboundLocalError(f"loss_fn: unknown loss_type {loss_type!r}")
 
 
 class GaussianVideoFrame(nn.Module):
@@ -284,6 +303,40 @@ class GaussianVideoFrame(nn.Module):
             self.adaptive_control(iter)
         elif iter % self.densification_interval == 0 and self.isremoval:
             self.removal_control(iter)
+        self.optimizer.step()
+        self.optimizer.zero_grad(set_to_none=True)
+        self.scheduler.step()
+        return loss, psnr
+
+    def train_iter_trace(self, gt_image, iter):
+        """GaussianSplats_Represent.py:175-188: train_iter returning the render."""
+        render_pkg = self.forward()
+        image = render_pkg["render"]
+        loss = loss_fn(image.squeeze(0), gt_image.squeeze(0), self.loss_type, lambda_value=0)
+        loss.backward()
+        if (iter == 1 or iter % self.densification_interval == 0) and self.isdensity:
+            self.adaptive_control(iter)
+        elif iter % self.densification_interval == 0 and self.isremoval:
+            self.removal_control(iter)
+        self.optimizer.step()
+        self.optimizer.zero_grad(set_to_none=True)
+        self.scheduler.step()
+        return image
+
+    def pre_train_iter(self, gt_image):
+        """GaussianSplats_Represent.py:210-222 (the K-frame detector's step): no
+        pruning or densification, the loss on the NCHW images with lambda 0.7.
+        L2 / L1 take the fused step (lambda does not enter them)."""
+        rgbw_train = self._fused_train_params(gt_image)
+        if rgbw_train is not None:
+            return self._train_iter_fused(gt_image, rgbw_train)
+        render_pkg = self.forward()
+        image = render_pkg["render"]
+        loss = loss_fn(image, gt_image, self.loss_type, lambda_value=0.7)
+        loss.backward()
+        with torch.no_grad():
+            mse_loss = F.mse_loss(image, gt_image)
+            psnr = 10 * math.log10(1.0 / mse_loss.item())
         self.optimizer.step()
         self.optimizer.zero_grad(set_to_none=True)
         self.scheduler.step()

@@ -26,8 +26,9 @@ detect_outliers_mean_diff :214-229) that runs on the MI355X path:
         --iterations 300 --loss_type L2
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m gsvc_amd.video -d Beauty.yuv ...
 
-MS-SSIM needs pytorch_msssim (not installed): reported as NaN (parity
-unpinned).
+The per-frame MS-SSIM is gsvc_amd.msssim.ms_ssim (pytorch_msssim's algorithm
+on the gfx950 kernels; parity unpinned against the package, DESIGN.md §2);
+frames whose smaller side is <= 160 (where ms_ssim asserts) report NaN.
 """
 from __future__ import annotations
 
@@ -44,6 +45,7 @@ import torch
 import torch.nn.functional as F
 
 from .frame import GaussianVideoFrame
+from .msssim import ms_ssim
 from .shard import aggregate_video_metrics, forced_k_frames, shard_gops
 
 # ---------------------------------------------------------------------------
@@ -182,7 +184,7 @@ class FrameTrainer:
         self.model.train()
         loss = None
         for it in range(1, int(self.iterations) + 1):
-            loss, _ = self.model.train_iter(self.gt_image, it)
+            loss, _ = self.model.pre_train_iter(self.gt_image)
         return self._filtered(), float(loss)
 
     def train(self):
@@ -210,6 +212,12 @@ class FrameTrainer:
             out = self.model()["render"]
             mse = F.mse_loss(out.float(), self.gt_image.float())
             psnr = 10 * math.log10(1.0 / float(mse))
+            # :145; ms_ssim needs a smaller side > 160 (the reference asserts):
+            # smaller frames report NaN
+            ms = float("nan")
+            if min(self.H, self.W) > 160 and self.device.type == "cuda":
+                ms = float(ms_ssim(out.float(), self.gt_image.float(), data_range=1,
+                                   size_average=True))
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
             t1 = time.time()
@@ -218,7 +226,7 @@ class FrameTrainer:
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
             eval_time = (time.time() - t1) / 100
-        return dict(psnr=psnr, ms_ssim=float("nan"), training_time=train_time,
+        return dict(psnr=psnr, ms_ssim=ms, training_time=train_time,
                     eval_time=eval_time, eval_fps=1.0 / eval_time,
                     num_gaussians=int(self.model._xyz.shape[0]), loss=float(loss.detach()),
                     iterations=it, model=self._filtered())

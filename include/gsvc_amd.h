@@ -346,6 +346,27 @@ int gsvc_rasterize_backward(
  * OpenCV's COLOR_YUV2RGB_I420 fixed-point BT.601 arithmetic.  H, W even. */
 int gsvc_i420_to_rgb(const unsigned char *yuv, int height, int width, float *out, void *stream);
 
+/* ---- SSIM / MS-SSIM (the loss_fn SSIM variants, utils.py:29-40, and the
+ * per-frame MS-SSIM metric, train_video_Represent.py:145), restating
+ * pytorch_msssim's ssim() / ms_ssim() (_ssim, gaussian_filter, avg-pool
+ * pyramid).  X, Y: [batch*channels][H][W] fp32 device planes.  levels = 1:
+ * ssim(); levels > 1: ms_ssim() with `weights` (host, levels values).
+ * flags: bit0 size_average (out[1]; else out[batch] = mean over channels),
+ * bit1 nonnegative_ssim (levels = 1).  C1 = (K1 data_range)^2, C2 = (K2 data_range)^2.
+ * The forward leaves in `ws` what the backward needs (pooled levels, upstream
+ * factors): pass the same workspace to the backward.  win_size odd, <= 11. */
+size_t gsvc_ssim_workspace_bytes(int planes, int height, int width, int win_size, int levels);
+int gsvc_ssim_forward(int batch, int channels, int height, int width, const float *X,
+                      const float *Y, int win_size, float win_sigma, float C1, float C2,
+                      int levels, const double *weights, int flags, float *out, void *ws,
+                      size_t ws_bytes, void *stream);
+/* d(out)/dX and/or d(out)/dY (either may be NULL) times grad_out (device,
+ * out's shape). */
+int gsvc_ssim_backward(int batch, int channels, int height, int width, const float *X,
+                       const float *Y, int win_size, float win_sigma, float C1, float C2,
+                       int levels, int flags, const float *grad_out, float *dX, float *dY,
+                       void *ws, size_t ws_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -270,3 +270,83 @@ def i420_to_rgb(yuv: np.ndarray, h: int, w: int) -> np.ndarray:
     b = (y + half + CUB * U) >> SH
     rgb = np.clip(np.stack([r, g, b]), 0, 255).astype(np.float32)
     return (rgb / np.float32(255.0)).astype(np.float32)
+
+
+# ---------------------------------------------------------------- SSIM / MS-SSIM
+# pytorch_msssim's published algorithm (ssim, ms_ssim, _ssim, gaussian_filter,
+# _fspecial_gauss_1d), the package GSVC calls at utils.py:29-40 and
+# train_video_Represent.py:145.  It is unpinned (requirements.txt:5) and not
+# installed here, so this float64 restatement is the checker: parity unpinned
+# against the package itself.
+
+def gauss_window(size: int, sigma: float) -> np.ndarray:
+    """_fspecial_gauss_1d: exp(-(c^2) / (2 sigma^2)) at c = t - size//2, normalised."""
+    c = np.arange(size, dtype=F64) - size // 2
+    g = np.exp(-(c ** 2) / (2 * sigma ** 2))
+    return g / g.sum()
+
+
+def _filter(x: np.ndarray, g: np.ndarray) -> np.ndarray:
+    """gaussian_filter: valid correlation along H, then W; a dimension shorter
+    than the window is left unfiltered.  x: [..., H, W]."""
+    k = g.shape[0]
+    out = x
+    for axis in (-2, -1):
+        if out.shape[axis] >= k:
+            win = np.lib.stride_tricks.sliding_window_view(out, k, axis=axis)
+            out = win @ g
+    return out
+
+
+def _ssim_terms(X, Y, g, C1, C2):
+    mu1, mu2 = _filter(X, g), _filter(Y, g)
+    s1 = _filter(X * X, g) - mu1 * mu1
+    s2 = _filter(Y * Y, g) - mu2 * mu2
+    s12 = _filter(X * Y, g) - mu1 * mu2
+    cs_map = (2 * s12 + C2) / (s1 + s2 + C2)
+    ssim_map = ((2 * mu1 * mu2 + C1) / (mu1 * mu1 + mu2 * mu2 + C1)) * cs_map
+    return ssim_map.mean(axis=(-2, -1)), cs_map.mean(axis=(-2, -1))  # [B, C]
+
+
+def ssim(X, Y, data_range=255.0, size_average=True, win_size=11, win_sigma=1.5,
+         K=(0.01, 0.03), nonnegative_ssim=False):
+    """X, Y: [B, C, H, W] -> scalar (size_average) or [B]."""
+    X = np.asarray(X, F64)
+    Y = np.asarray(Y, F64)
+    C1, C2 = (K[0] * data_range) ** 2, (K[1] * data_range) ** 2
+    s, _ = _ssim_terms(X, Y, gauss_window(win_size, win_sigma), C1, C2)
+    if nonnegative_ssim:
+        s = np.maximum(s, 0.0)
+    return s.mean() if size_average else s.mean(axis=1)
+
+
+def avg_pool2(x: np.ndarray) -> np.ndarray:
+    """F.avg_pool2d(kernel 2, stride 2, padding (H % 2, W % 2)), pads counted."""
+    H, W = x.shape[-2:]
+    ph, pw = H % 2, W % 2
+    xp = np.pad(x, [(0, 0)] * (x.ndim - 2) + [(ph, ph), (pw, pw)])
+    Ho, Wo = (H + 2 * ph - 2) // 2 + 1, (W + 2 * pw - 2) // 2 + 1
+    xp = xp[..., :2 * Ho, :2 * Wo]
+    return (xp[..., 0::2, 0::2] + xp[..., 0::2, 1::2] + xp[..., 1::2, 0::2] +
+            xp[..., 1::2, 1::2]) / 4.0
+
+
+MS_SSIM_WEIGHTS = (0.0448, 0.2856, 0.3001, 0.2363, 0.1333)
+
+
+def ms_ssim(X, Y, data_range=255.0, size_average=True, win_size=11, win_sigma=1.5,
+            weights=None, K=(0.01, 0.03)):
+    X = np.asarray(X, F64)
+    Y = np.asarray(Y, F64)
+    w = np.asarray(MS_SSIM_WEIGHTS if weights is None else weights, F64)
+    C1, C2 = (K[0] * data_range) ** 2, (K[1] * data_range) ** 2
+    g = gauss_window(win_size, win_sigma)
+    mcs = []
+    for i in range(len(w)):
+        s, cs = _ssim_terms(X, Y, g, C1, C2)
+        if i < len(w) - 1:
+            mcs.append(np.maximum(cs, 0.0))
+            X, Y = avg_pool2(X), avg_pool2(Y)
+    stack = np.stack(mcs + [np.maximum(s, 0.0)], axis=0)  # [levels, B, C]
+    val = np.prod(stack ** w[:, None, None], axis=0)
+    return val.mean() if size_average else val.mean(axis=1)
