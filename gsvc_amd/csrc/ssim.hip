@@ -19,16 +19,23 @@
 //   counted), prod_i relu(cs_i)^w_i (i < 4) * relu(ssim_4)^w_4.
 //
 // Layout: planes [P = B*C][H][W] fp32.  Every level is one LDS-tiled launch
-// over (W tiles, H tiles, planes): the 5 windowed moments of a 16x64 output
-// tile from a 26x74 input tile (vertical pass, then horizontal), per-block
-// partial sums of ssim_map and cs (reduced in double, in a fixed order, by
-// ssim_reduce_kernel, then ssim_combine_kernel forms the values and the
-// per-plane upstream factors the backward needs -- nothing goes to the host).
-// Backward (w.r.t. X; w.r.t. Y by symmetry with X and Y swapped): per level
-//   dX = w^T*g_mu1 + 2 X (w^T*g_E11) + Y (w^T*g_E12)
-// with the per-output coefficients g recomputed in LDS from a (16+20)x(64+20)
-// input tile, plus the coarser level's gradient through the average pool.
-// HBM: forward 8 B per pixel and level, backward 12 B (+4 B per coarse pixel).
+// over (W tiles, H tiles, planes) of ssim_moments_kernel: the 5 windowed
+// moments of a 16x64 output tile from its 26x74 input region (every load
+// issued before the first LDS store; vertical pass over 4-row runs, horizontal
+// over 4-column runs read as conflict-free ds_read_b128), then per-block sums
+// of ssim_map and cs, reduced in double in a fixed order (ssim_reduce_kernel);
+// ssim_combine_kernel forms the values and the per-plane upstream factors the
+// backward needs -- nothing goes to the host.
+// Backward (w.r.t. X; w.r.t. Y by symmetry with X and Y swapped), per level
+// from the coarsest: ssim_moments_kernel<true> writes the per-output
+// coefficients (g_mu1, g_E11, g_E12) as 3 maps, ssim_grad_kernel applies the
+// transposed filter,
+//   dX = w^T*g_mu1 + 2 X (w^T*g_E11) + Y (w^T*g_E12),
+// and adds the coarser level's gradient through the average pool.
+// 1080p x 3: forward 82 us (SSIM) / 162 us (MS-SSIM), forward + backward
+// 250 / 444 us (tools/ssimbench.py; torch conv2d restatement: 3.9 / 6.9 ms
+// and 6.6 / 11.7 ms).  The level-0 moments launch is latency/LDS-issue bound
+// (73 us for 50 MB of input).
 #include "common.h"
 
 namespace gsvc {
@@ -43,88 +50,198 @@ struct SsimWin {
     int kv, kh;
 };
 
-// ---------------------------------------------------------------- forward
+// ---------------------------------------------------------------- moments
 
-__global__ __launch_bounds__(256) void ssim_fwd_kernel(const float *__restrict__ X,
-                                                       const float *__restrict__ Y, int H, int W,
-                                                       int Ho, int Wo, SsimWin w, float C1,
-                                                       float C2, float2 *__restrict__ partial) {
-    constexpr int kInH = kSsimTH + kSsimMaxWin - 1, kInW = kSsimTW + kSsimMaxWin - 1;
-    __shared__ float s_x[kInH][kInW], s_y[kInH][kInW];
-    __shared__ float s_v[5][kSsimTH][kInW];
+constexpr int kRegH = kSsimTH + kSsimMaxWin - 1;  // 26 input rows of a tile
+constexpr int kRegW = kSsimTW + kSsimMaxWin - 1;  // 74 input columns
+constexpr int kRowP = 76;                          // padded row of the float4-read buffers
+constexpr int kRun = 4;                            // rows / columns per thread per pass
+constexpr int kSpan = kRun + kSsimMaxWin - 1;      // 14 values a 4-run reads
+
+// Column run of a thread in the 4-column passes: 16 lanes cover one 64-column
+// row, and the lane -> run map differs by row parity so that every 16-lane
+// group of a ds_read_b128 (two rows, 76-float stride = 3 chunks of bank shift)
+// reads 16 distinct 4-bank chunks: no bank conflicts.
+__device__ __forceinline__ int run_of_lane(int tid) {
+    const int l = tid & 15;
+    if ((tid >> 4) & 1) return (l + 1) & 15;
+    return l < 4 ? l : (l < 12 ? l + 4 : l - 8);
+}
+
+// All four floats of an LDS float4 (one ds_read_b128 even when the caller
+// uses only some of them).
+__device__ __forceinline__ float4 lds_f4(const float *p) {
+    float4 f = *reinterpret_cast<const float4 *>(p);
+    asm volatile("" : "+v"(f.x), "+v"(f.y), "+v"(f.z), "+v"(f.w));
+    return f;
+}
+
+// Per output of the plane: the SSIM terms at one window position.
+struct SsimTerms {
+    float mu1, mu2, B1, B2, l, cs;
+};
+__device__ __forceinline__ SsimTerms ssim_terms(const float m[5], float C1, float C2) {
+    SsimTerms T;
+    const float mu1_sq = m[0] * m[0], mu2_sq = m[1] * m[1], mu12 = m[0] * m[1];
+    const float s1 = m[2] - mu1_sq, s2 = m[3] - mu2_sq, s12 = m[4] - mu12;
+    T.mu1 = m[0];
+    T.mu2 = m[1];
+    T.B1 = (mu1_sq + mu2_sq) + C1;
+    T.B2 = (s1 + s2) + C2;
+    T.cs = (2.0f * s12 + C2) / T.B2;            // cs_map
+    T.l = (2.0f * mu12 + C1) / T.B1;            // ssim_map = l * cs
+    return T;
+}
+
+// One 16x64 output tile of a plane: the 5 windowed moments (vertical pass over
+// 4-row runs, horizontal pass over 4-column runs read as float4s), then
+//   kCoef = false: the tile's sums of ssim_map and cs -> partial[plane][tile];
+//   kCoef = true : the backward coefficients of every output,
+//     g_mu1 = us (dl/dmu1 cs + l dcs/dmu1) + uc dcs/dmu1,
+//     g_E11 = (us l + uc) dcs/dE11,  g_E12 = (us l + uc) dcs/dE12,
+//     with us, uc = the plane's upstream factors times the output gradient,
+//   -> coef[plane][3][Ho][Wo].
+template <bool kCoef>
+__global__ __launch_bounds__(256) void ssim_moments_kernel(
+    const float *__restrict__ X, const float *__restrict__ Y, int H, int W, int Ho, int Wo,
+    SsimWin w, float C1, float C2, float2 *__restrict__ partial, const float2 *__restrict__ fac,
+    const float *__restrict__ gout, int gdiv, float *__restrict__ coef) {
+    __shared__ float s_x[kRegH][kRegW], s_y[kRegH][kRegW];
+    __shared__ __attribute__((aligned(16))) float s_v[5][kSsimTH][kRowP];
     __shared__ float2 s_red[4];
     const int tid = threadIdx.x;
     const int plane = blockIdx.z;
     const int r0 = blockIdx.y * kSsimTH, c0 = blockIdx.x * kSsimTW;
     const size_t hw = (size_t)H * (size_t)W;
     const float *x = X + plane * hw, *y = Y + plane * hw;
-    const int inh = kSsimTH + w.kv - 1, inw = kSsimTW + w.kh - 1;
-    for (int k = tid; k < inh * inw; k += 256) {
-        const int rr = k / inw, cc = k - rr * inw;
-        const int gr = r0 + rr, gc = c0 + cc;
-        float a = 0.f, b = 0.f;
-        if (gr < H && gc < W) {
-            a = x[(size_t)gr * W + gc];
-            b = y[(size_t)gr * W + gc];
-        }
-        s_x[rr][cc] = a;
-        s_y[rr][cc] = b;
-    }
-    __syncthreads();
-    // vertical pass: the 5 moments of rows r0..r0+15 over columns of the tile
-    for (int k = tid; k < kSsimTH * inw; k += 256) {
-        const int rr = k / inw, cc = k - rr * inw;
-        float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
+    const int kv = w.kv, kh = w.kh;
+    const int inw = kSsimTW + kh - 1;
+    {  // the whole 26x74 region, every load issued before the first LDS store
+        constexpr int kN = (kRegH * kRegW + 255) / 256;
+        float a[kN], b[kN];
 #pragma unroll
-        for (int t = 0; t < kSsimMaxWin; ++t) {
-            if (t < w.kv) {
-                const float a = s_x[rr + t][cc], b = s_y[rr + t][cc], q = w.wv[t];
-                m1 = fmaf(q, a, m1);
-                m2 = fmaf(q, b, m2);
-                e11 = fmaf(q, a * a, e11);
-                e22 = fmaf(q, b * b, e22);
-                e12 = fmaf(q, a * b, e12);
+        for (int j = 0; j < kN; ++j) {
+            const int k = tid + 256 * j;
+            const int rr = k / kRegW, cc = k - rr * kRegW;
+            const int gr = r0 + rr, gc = c0 + cc;
+            a[j] = 0.f;
+            b[j] = 0.f;
+            if (k < kRegH * kRegW && gr < H && gc < W) {
+                a[j] = x[(size_t)gr * W + gc];
+                b[j] = y[(size_t)gr * W + gc];
             }
         }
-        s_v[0][rr][cc] = m1;
-        s_v[1][rr][cc] = m2;
-        s_v[2][rr][cc] = e11;
-        s_v[3][rr][cc] = e22;
-        s_v[4][rr][cc] = e12;
-    }
-    __syncthreads();
-    float acc_s = 0.f, acc_c = 0.f;
 #pragma unroll
-    for (int j = 0; j < kSsimTH * kSsimTW / 256; ++j) {
-        const int k = tid + 256 * j;
-        const int rr = k / kSsimTW, cc = k - rr * kSsimTW;
-        if (r0 + rr >= Ho || c0 + cc >= Wo) continue;
-        float m[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int t = 0; t < kSsimMaxWin; ++t) {
-            if (t < w.kh) {
-#pragma unroll
-                for (int q = 0; q < 5; ++q) m[q] = fmaf(w.wh[t], s_v[q][rr][cc + t], m[q]);
+        for (int j = 0; j < kN; ++j) {
+            const int k = tid + 256 * j;
+            if (k < kRegH * kRegW) {
+                const int rr = k / kRegW, cc = k - rr * kRegW;
+                s_x[rr][cc] = a[j];
+                s_y[rr][cc] = b[j];
             }
         }
-        const float mu1_sq = m[0] * m[0], mu2_sq = m[1] * m[1], mu12 = m[0] * m[1];
-        const float s1 = m[2] - mu1_sq, s2 = m[3] - mu2_sq, s12 = m[4] - mu12;
-        const float cs = (2.0f * s12 + C2) / ((s1 + s2) + C2);
-        const float ss = ((2.0f * mu12 + C1) / ((mu1_sq + mu2_sq) + C1)) * cs;
-        acc_s += ss;
-        acc_c += cs;
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        acc_s += __shfl_xor(acc_s, off, 64);
-        acc_c += __shfl_xor(acc_c, off, 64);
-    }
-    if ((tid & 63) == 0) s_red[tid >> 6] = make_float2(acc_s, acc_c);
     __syncthreads();
-    if (tid == 0) {
-        const float2 a = s_red[0], b = s_red[1], c = s_red[2], d = s_red[3];
-        partial[((size_t)plane * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] =
-            make_float2((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y));
+    {  // vertical: lane = column, wave = a run of 4 rows
+        const int tx = tid & 63, rb = (tid >> 6) * kRun;
+        for (int cc = tx; cc < inw; cc += 64) {
+            float a[kSpan], b[kSpan];
+#pragma unroll
+            for (int j = 0; j < kSpan; ++j) {
+                if (j < kRun + kv - 1) {
+                    a[j] = s_x[rb + j][cc];
+                    b[j] = s_y[rb + j][cc];
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < kRun; ++r) {
+                float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
+#pragma unroll
+                for (int t = 0; t < kSsimMaxWin; ++t) {
+                    if (t < kv) {
+                        const float av = a[r + t], bv = b[r + t], q = w.wv[t];
+                        m1 = fmaf(q, av, m1);
+                        m2 = fmaf(q, bv, m2);
+                        e11 = fmaf(q, av * av, e11);
+                        e22 = fmaf(q, bv * bv, e22);
+                        e12 = fmaf(q, av * bv, e12);
+                    }
+                }
+                s_v[0][rb + r][cc] = m1;
+                s_v[1][rb + r][cc] = m2;
+                s_v[2][rb + r][cc] = e11;
+                s_v[3][rb + r][cc] = e22;
+                s_v[4][rb + r][cc] = e12;
+            }
+        }
+    }
+    __syncthreads();
+    // horizontal: a thread owns 4 consecutive outputs of one row
+    const int rr = tid >> 4, cb = run_of_lane(tid) * kRun;
+    float m[kRun][5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float4 f = lds_f4(&s_v[q][rr][cb + 4 * j]);
+            v[4 * j] = f.x;
+            v[4 * j + 1] = f.y;
+            v[4 * j + 2] = f.z;
+            v[4 * j + 3] = f.w;
+        }
+#pragma unroll
+        for (int c = 0; c < kRun; ++c) {
+            float acc = 0.f;
+#pragma unroll
+            for (int t = 0; t < kSsimMaxWin; ++t)
+                if (t < kh) acc = fmaf(w.wh[t], v[c + t], acc);
+            m[c][q] = acc;
+        }
+    }
+    const int orow = r0 + rr;
+    if (!kCoef) {
+        float acc_s = 0.f, acc_c = 0.f;
+#pragma unroll
+        for (int c = 0; c < kRun; ++c) {
+            if (orow < Ho && c0 + cb + c < Wo) {
+                const SsimTerms T = ssim_terms(m[c], C1, C2);
+                acc_s += T.l * T.cs;
+                acc_c += T.cs;
+            }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            acc_s += __shfl_xor(acc_s, off, 64);
+            acc_c += __shfl_xor(acc_c, off, 64);
+        }
+        if ((tid & 63) == 0) s_red[tid >> 6] = make_float2(acc_s, acc_c);
+        __syncthreads();
+        if (tid == 0) {
+            const float2 a = s_red[0], b = s_red[1], c = s_red[2], d = s_red[3];
+            partial[((size_t)plane * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] =
+                make_float2((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y));
+        }
+    } else {
+        const float g = gout[gdiv > 0 ? plane / gdiv : 0];
+        const float2 f = fac[plane];
+        const float us = f.x * g, uc = f.y * g;
+        const size_t ohw = (size_t)Ho * (size_t)Wo;
+        float *co = coef + (size_t)plane * 3 * ohw;
+#pragma unroll
+        for (int c = 0; c < kRun; ++c) {
+            const int ocol = c0 + cb + c;
+            if (orow < Ho && ocol < Wo) {
+                const SsimTerms T = ssim_terms(m[c], C1, C2);
+                const float dl_dm1 = (2.0f * T.mu2 - 2.0f * T.mu1 * T.l) / T.B1;
+                const float dcs_dm1 = (2.0f * T.mu1 * T.cs - 2.0f * T.mu2) / T.B2;
+                const float k_cs = us * T.l + uc;  // d loss / d cs through both routes
+                const size_t o = (size_t)orow * Wo + ocol;
+                co[o] = us * (dl_dm1 * T.cs) + k_cs * dcs_dm1;
+                co[ohw + o] = k_cs * (-T.cs / T.B2);
+                co[2 * ohw + o] = k_cs * (2.0f / T.B2);
+            }
+        }
     }
 }
 
@@ -193,53 +310,54 @@ __global__ __launch_bounds__(256) void ssim_reduce_kernel(const float2 *__restri
 // Values (out[1] when size_average, else out[B]) and per-(level, plane)
 // upstream factors {d value / d ssim_map pixel, d value / d cs pixel} per unit
 // of the caller's output gradient.  flags: bit0 size_average, bit1
-// nonnegative_ssim (single level).  One thread: planes are few (B*C).
-__global__ void ssim_combine_kernel(const double2 *__restrict__ stats, SsimLevels L, int batch,
-                                    int channels, int flags, float *__restrict__ out,
-                                    float2 *__restrict__ fac) {
-    if (threadIdx.x != 0) return;
+// nonnegative_ssim (single level).  A thread per plane forms its value in fp32
+// as the package does (relu, ** weights, product); thread 0 then takes the
+// means over planes in double, in plane order.
+__global__ __launch_bounds__(256) void ssim_combine_kernel(const double2 *__restrict__ stats,
+                                                           SsimLevels L, int batch, int channels,
+                                                           int flags, float *__restrict__ out,
+                                                           float2 *__restrict__ fac,
+                                                           float *__restrict__ vals) {
     const int planes = batch * channels;
     const bool avg = flags & 1, nonneg = flags & 2;
-    const double scale = avg ? 1.0 / (double)planes : 1.0 / (double)channels;
+    const float scale = avg ? 1.0f / (float)planes : 1.0f / (float)channels;
+    for (int p = threadIdx.x; p < planes; p += blockDim.x) {
+        float val;
+        if (L.n == 1) {
+            const float s = (float)stats[p].x;
+            val = (nonneg && s < 0.0f) ? 0.0f : s;
+            const float d = (nonneg && s <= 0.0f) ? 0.0f : scale;
+            fac[p] = make_float2(d / ((float)L.Ho[0] * (float)L.Wo[0]), 0.0f);
+        } else {
+            float term[kSsimMaxLevels], base[kSsimMaxLevels];
+            val = 1.0f;
+            for (int l = 0; l < L.n; ++l) {
+                const float raw = (float)(l < L.n - 1 ? stats[(size_t)l * planes + p].y
+                                                      : stats[(size_t)l * planes + p].x);
+                base[l] = raw > 0.0f ? raw : 0.0f;  // relu
+                term[l] = powf(base[l], L.weight[l]);
+                val *= term[l];
+            }
+            for (int l = 0; l < L.n; ++l) {
+                float d = 0.0f;
+                if (base[l] > 0.0f) {  // relu'(0) = 0
+                    float others = 1.0f;
+                    for (int j = 0; j < L.n; ++j)
+                        if (j != l) others *= term[j];
+                    d = scale * L.weight[l] * powf(base[l], L.weight[l] - 1.0f) * others;
+                }
+                const float f = d / ((float)L.Ho[l] * (float)L.Wo[l]);
+                fac[(size_t)l * planes + p] = l < L.n - 1 ? make_float2(0.0f, f) : make_float2(f, 0.0f);
+            }
+        }
+        vals[p] = val;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
     double total = 0.0;
     for (int b = 0; b < batch; ++b) {
         double sum_b = 0.0;
-        for (int c = 0; c < channels; ++c) {
-            const int p = b * channels + c;
-            double val;
-            if (L.n == 1) {
-                const double s = stats[p].x;
-                val = (nonneg && s < 0.0) ? 0.0 : s;
-                const double d = (nonneg && s <= 0.0) ? 0.0 : scale;
-                const double cnt = (double)L.Ho[0] * (double)L.Wo[0];
-                fac[p] = make_float2((float)(d / cnt), 0.0f);
-            } else {
-                double term[kSsimMaxLevels], base[kSsimMaxLevels];
-                val = 1.0;
-                for (int l = 0; l < L.n; ++l) {
-                    const double raw = l < L.n - 1 ? stats[(size_t)l * planes + p].y
-                                                   : stats[(size_t)l * planes + p].x;
-                    base[l] = raw > 0.0 ? raw : 0.0;  // relu
-                    term[l] = pow(base[l], (double)L.weight[l]);
-                    val *= term[l];
-                }
-                for (int l = 0; l < L.n; ++l) {
-                    double d = 0.0;
-                    if (base[l] > 0.0) {
-                        double others = 1.0;
-                        for (int j = 0; j < L.n; ++j)
-                            if (j != l) others *= term[j];
-                        d = scale * (double)L.weight[l] * pow(base[l], (double)L.weight[l] - 1.0) *
-                            others;
-                    }
-                    const double cnt = (double)L.Ho[l] * (double)L.Wo[l];
-                    const float f = (float)(d / cnt);
-                    fac[(size_t)l * planes + p] =
-                        l < L.n - 1 ? make_float2(0.0f, f) : make_float2(f, 0.0f);
-                }
-            }
-            sum_b += val;
-        }
+        for (int c = 0; c < channels; ++c) sum_b += (double)vals[b * channels + c];
         if (!avg) out[b] = (float)(sum_b / (double)channels);
         total += sum_b;
     }
@@ -248,145 +366,113 @@ __global__ void ssim_combine_kernel(const double2 *__restrict__ stats, SsimLevel
 
 // ---------------------------------------------------------------- backward
 
-constexpr int kBInH = kSsimTH + 2 * kSsimMaxWin - 2;   // 36 input rows
-constexpr int kBInW = kSsimTW + 2 * kSsimMaxWin - 2;   // 84 input columns
-constexpr int kBCoH = kSsimTH + kSsimMaxWin - 1;       // 26 coefficient rows
-constexpr int kBCoW = kSsimTW + kSsimMaxWin - 1;       // 74 coefficient columns
-
-__global__ __launch_bounds__(256) void ssim_bwd_kernel(
-    const float *__restrict__ X, const float *__restrict__ Y, int H, int W, int Ho, int Wo,
-    SsimWin w, float C1, float C2, const float2 *__restrict__ fac, const float *__restrict__ gout,
-    int gdiv, const float *__restrict__ dcoarse, int Hc, int Wc, int pr, int pc,
-    float *__restrict__ dX) {
-    // phase buffers: inputs [2][36][84] then coefficients [3][26][74];
-    // vertical moments [5][26][84] then transposed partials [3][16][74]
-    __shared__ float s_a[2 * kBInH * kBInW];
-    __shared__ float s_b[5 * kBCoH * kBInW];
+// Input gradient of one 16x64 tile of a plane from the coefficient maps:
+//   dX = w^T * g_mu1 + 2 X (w^T * g_E11) + Y (w^T * g_E12)
+// (transposed separable filter: vertical 4-row runs, horizontal 4-column runs),
+// plus the coarser level's gradient through the 2x2 average pool (1/4 each).
+__global__ __launch_bounds__(256) void ssim_grad_kernel(
+    const float *__restrict__ coef, int Ho, int Wo, const float *__restrict__ X,
+    const float *__restrict__ Y, int H, int W, SsimWin w, const float *__restrict__ dcoarse,
+    int Hc, int Wc, int pr, int pc, float *__restrict__ dX) {
+    __shared__ float s_co[3][kRegH][kRegW];
+    __shared__ __attribute__((aligned(16))) float s_t[3][kSsimTH][kRowP];
     const int tid = threadIdx.x;
     const int plane = blockIdx.z;
     const int r0 = blockIdx.y * kSsimTH, c0 = blockIdx.x * kSsimTW;
-    const size_t hw = (size_t)H * (size_t)W;
-    const float *x = X + plane * hw, *y = Y + plane * hw;
     const int kv = w.kv, kh = w.kh;
     const int ir0 = r0 - (kv - 1), ic0 = c0 - (kh - 1);
-    const int inh = kSsimTH + 2 * (kv - 1), inw = kSsimTW + 2 * (kh - 1);
     const int coh = kSsimTH + kv - 1, cow = kSsimTW + kh - 1;
-    const float g = gout[gdiv > 0 ? plane / gdiv : 0];
-    const float2 f = fac[plane];
-    const float us = f.x * g, uc = f.y * g;
-    float *in_x = s_a, *in_y = s_a + kBInH * kBInW;  // [36][84] each
-    for (int k = tid; k < inh * inw; k += 256) {
-        const int rr = k / inw, cc = k - rr * inw;
-        const int gr = ir0 + rr, gc = ic0 + cc;
-        float a = 0.f, b = 0.f;
-        if (gr >= 0 && gr < H && gc >= 0 && gc < W) {
-            a = x[(size_t)gr * W + gc];
-            b = y[(size_t)gr * W + gc];
-        }
-        in_x[rr * kBInW + cc] = a;
-        in_y[rr * kBInW + cc] = b;
-    }
-    __syncthreads();
-    // vertical moments at coefficient rows, all input columns
-    for (int k = tid; k < coh * inw; k += 256) {
-        const int rr = k / inw, cc = k - rr * inw;
-        float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
+    const size_t ohw = (size_t)Ho * (size_t)Wo;
+    const float *co = coef + (size_t)plane * 3 * ohw;
+    {  // the 26x74 coefficient region, every load issued before the first LDS store
+        constexpr int kN = (kRegH * kRegW + 255) / 256;
+        float a[kN], b[kN], c[kN];
 #pragma unroll
-        for (int t = 0; t < kSsimMaxWin; ++t) {
-            if (t < kv) {
-                const float a = in_x[(rr + t) * kBInW + cc], b = in_y[(rr + t) * kBInW + cc];
-                const float q = w.wv[t];
-                m1 = fmaf(q, a, m1);
-                m2 = fmaf(q, b, m2);
-                e11 = fmaf(q, a * a, e11);
-                e22 = fmaf(q, b * b, e22);
-                e12 = fmaf(q, a * b, e12);
+        for (int j = 0; j < kN; ++j) {
+            const int k = tid + 256 * j;
+            const int rr = k / kRegW, cc = k - rr * kRegW;
+            const int p_r = ir0 + rr, p_c = ic0 + cc;
+            a[j] = 0.f;
+            b[j] = 0.f;
+            c[j] = 0.f;
+            if (k < kRegH * kRegW && rr < coh && cc < cow && p_r >= 0 && p_r < Ho && p_c >= 0 &&
+                p_c < Wo) {
+                const size_t o = (size_t)p_r * Wo + p_c;
+                a[j] = co[o];
+                b[j] = co[ohw + o];
+                c[j] = co[2 * ohw + o];
             }
         }
-        const int o = rr * kBInW + cc;
-        s_b[o] = m1;
-        s_b[kBCoH * kBInW + o] = m2;
-        s_b[2 * kBCoH * kBInW + o] = e11;
-        s_b[3 * kBCoH * kBInW + o] = e22;
-        s_b[4 * kBCoH * kBInW + o] = e12;
+#pragma unroll
+        for (int j = 0; j < kN; ++j) {
+            const int k = tid + 256 * j;
+            if (k < kRegH * kRegW) {
+                const int rr = k / kRegW, cc = k - rr * kRegW;
+                s_co[0][rr][cc] = a[j];
+                s_co[1][rr][cc] = b[j];
+                s_co[2][rr][cc] = c[j];
+            }
+        }
     }
     __syncthreads();
-    // coefficients at every output p of the region (zero outside [0,Ho)x[0,Wo))
-    float *co = s_a;  // [3][26][74]
-    for (int k = tid; k < coh * cow; k += 256) {
-        const int rr = k / cow, cc = k - rr * cow;
-        const int pr_ = ir0 + rr, pc_ = ic0 + cc;
-        float ga = 0.f, gb = 0.f, gc = 0.f;
-        if (pr_ >= 0 && pr_ < Ho && pc_ >= 0 && pc_ < Wo) {
-            float m[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    {  // transposed vertical: row rb + r gathers coefficient rows rb + r + kv-1-t
+        const int tx = tid & 63, rb = (tid >> 6) * kRun;
+        for (int cc = tx; cc < cow; cc += 64) {
 #pragma unroll
-            for (int t = 0; t < kSsimMaxWin; ++t) {
-                if (t < kh) {
+            for (int q = 0; q < 3; ++q) {
+                float v[kSpan];
 #pragma unroll
-                    for (int q = 0; q < 5; ++q)
-                        m[q] = fmaf(w.wh[t], s_b[q * kBCoH * kBInW + rr * kBInW + cc + t], m[q]);
+                for (int j = 0; j < kSpan; ++j)
+                    if (j < kRun + kv - 1) v[j] = s_co[q][rb + j][cc];
+#pragma unroll
+                for (int r = 0; r < kRun; ++r) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int t = 0; t < kSsimMaxWin; ++t)
+                        if (t < kv) acc = fmaf(w.wv[t], v[r + kv - 1 - t], acc);
+                    s_t[q][rb + r][cc] = acc;
                 }
             }
-            const float mu1_sq = m[0] * m[0], mu2_sq = m[1] * m[1], mu12 = m[0] * m[1];
-            const float s1 = m[2] - mu1_sq, s2 = m[3] - mu2_sq, s12 = m[4] - mu12;
-            const float B1 = (mu1_sq + mu2_sq) + C1, B2 = (s1 + s2) + C2;
-            const float l = (2.0f * mu12 + C1) / B1;
-            const float cs = (2.0f * s12 + C2) / B2;
-            const float dl_dm1 = (2.0f * m[1] - 2.0f * m[0] * l) / B1;
-            const float dcs_dm1 = (2.0f * m[0] * cs - 2.0f * m[1]) / B2;
-            const float k_cs = us * l + uc;  // d loss / d cs through both routes
-            ga = us * (dl_dm1 * cs) + k_cs * dcs_dm1;
-            gb = k_cs * (-cs / B2);
-            gc = k_cs * (2.0f / B2);
         }
-        co[rr * kBCoW + cc] = ga;
-        co[kBCoH * kBCoW + rr * kBCoW + cc] = gb;
-        co[2 * kBCoH * kBCoW + rr * kBCoW + cc] = gc;
     }
     __syncthreads();
-    // transposed vertical: tile rows x coefficient columns
-    float *tv = s_b;  // [3][16][74]
-    for (int k = tid; k < kSsimTH * cow; k += 256) {
-        const int rr = k / cow, cc = k - rr * cow;
-        float a = 0.f, b = 0.f, c = 0.f;
+    const int rr = tid >> 4, cb = run_of_lane(tid) * kRun;
+    float G[3][kRun];
 #pragma unroll
-        for (int t = 0; t < kSsimMaxWin; ++t) {
-            if (t < kv) {
-                const int src = (rr + kv - 1 - t) * kBCoW + cc;
-                const float q = w.wv[t];
-                a = fmaf(q, co[src], a);
-                b = fmaf(q, co[kBCoH * kBCoW + src], b);
-                c = fmaf(q, co[2 * kBCoH * kBCoW + src], c);
-            }
+    for (int q = 0; q < 3; ++q) {
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float4 f = lds_f4(&s_t[q][rr][cb + 4 * j]);
+            v[4 * j] = f.x;
+            v[4 * j + 1] = f.y;
+            v[4 * j + 2] = f.z;
+            v[4 * j + 3] = f.w;
         }
-        tv[rr * kBCoW + cc] = a;
-        tv[kSsimTH * kBCoW + rr * kBCoW + cc] = b;
-        tv[2 * kSsimTH * kBCoW + rr * kBCoW + cc] = c;
+#pragma unroll
+        for (int c = 0; c < kRun; ++c) {
+            float acc = 0.f;
+#pragma unroll
+            for (int t = 0; t < kSsimMaxWin; ++t)
+                if (t < kh) acc = fmaf(w.wh[t], v[c + kh - 1 - t], acc);
+            G[q][c] = acc;
+        }
     }
-    __syncthreads();
+    const int qr = r0 + rr;
+    if (qr >= H) return;
+    const size_t hw = (size_t)H * (size_t)W;
+    const float *x = X + plane * hw, *y = Y + plane * hw;
     float *dx = dX + plane * hw;
     const float *dc = dcoarse ? dcoarse + (size_t)plane * Hc * Wc : nullptr;
+    const int orow = (qr + pr) >> 1;
 #pragma unroll
-    for (int j = 0; j < kSsimTH * kSsimTW / 256; ++j) {
-        const int k = tid + 256 * j;
-        const int rr = k / kSsimTW, cc = k - rr * kSsimTW;
-        const int qr = r0 + rr, qc = c0 + cc;
-        if (qr >= H || qc >= W) continue;
-        float a = 0.f, b = 0.f, c = 0.f;
-#pragma unroll
-        for (int t = 0; t < kSsimMaxWin; ++t) {
-            if (t < kh) {
-                const int src = rr * kBCoW + cc + kh - 1 - t;
-                const float q = w.wh[t];
-                a = fmaf(q, tv[src], a);
-                b = fmaf(q, tv[kSsimTH * kBCoW + src], b);
-                c = fmaf(q, tv[2 * kSsimTH * kBCoW + src], c);
-            }
-        }
+    for (int c = 0; c < kRun; ++c) {
+        const int qc = c0 + cb + c;
+        if (qc >= W) break;
         const size_t qi = (size_t)qr * W + qc;
-        float v = a + 2.0f * x[qi] * b + y[qi] * c;
+        float v = G[0][c] + 2.0f * x[qi] * G[1][c] + y[qi] * G[2][c];
         if (dc) {
-            const int orow = (qr + pr) >> 1, ocol = (qc + pc) >> 1;
+            const int ocol = (qc + pc) >> 1;
             if (orow < Hc && ocol < Wc) v += 0.25f * dc[(size_t)orow * Wc + ocol];
         }
         dx[qi] = v;
@@ -406,7 +492,7 @@ struct SsimPlan {
     // workspace
     size_t pyr_off[kSsimMaxLevels];  // floats: X_l at pyr_off[l], Y_l right after (l >= 1)
     size_t dx_off[kSsimMaxLevels];   // floats: dX_l (l >= 1)
-    size_t part_off, stats_off, fac_off, bytes;
+    size_t part_off, coef_off, stats_off, fac_off, vals_off, bytes;
 };
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -460,10 +546,14 @@ int make_plan(int planes, int H, int W, int win_size, float sigma, int levels,
     }
     P.part_off = off;
     off += align256(sizeof(float2) * (size_t)part);
+    P.coef_off = off;  // the backward's coefficient maps, [P][3][Ho][Wo] of level 0
+    off += align256(sizeof(float) * 3 * (size_t)planes * P.L.Ho[0] * P.L.Wo[0]);
     P.stats_off = off;
     off += align256(sizeof(double2) * (size_t)levels * planes);
     P.fac_off = off;
     off += align256(sizeof(float2) * (size_t)levels * planes);
+    P.vals_off = off;
+    off += align256(sizeof(float) * (size_t)planes);
     P.bytes = off;
     return 0;
 }
@@ -512,14 +602,17 @@ extern "C" int gsvc_ssim_forward(int batch, int channels, int height, int width,
                                P.pc[l - 1], planes);
         }
         const dim3 grid(ceil_div(P.L.Wo[l], kSsimTW), ceil_div(P.L.Ho[l], kSsimTH), planes);
-        hipLaunchKernelGGL(ssim_fwd_kernel, grid, dim3(256), 0, s, xl, yl, P.H[l], P.W[l],
-                           P.L.Ho[l], P.L.Wo[l], P.win[l], C1, C2, part + P.L.part_off[l]);
+        auto kfn = ssim_moments_kernel<false>;
+        hipLaunchKernelGGL(kfn, grid, dim3(256), 0, s, xl, yl, P.H[l], P.W[l], P.L.Ho[l],
+                           P.L.Wo[l], P.win[l], C1, C2, part + P.L.part_off[l], nullptr, nullptr,
+                           0, nullptr);
     }
     double2 *stats = reinterpret_cast<double2 *>(w + P.stats_off);
     hipLaunchKernelGGL(ssim_reduce_kernel, dim3(planes, levels), dim3(256), 0, s, part, P.L,
                        planes, stats);
-    hipLaunchKernelGGL(ssim_combine_kernel, dim3(1), dim3(64), 0, s, stats, P.L, batch, channels,
-                       flags, out, reinterpret_cast<float2 *>(w + P.fac_off));
+    hipLaunchKernelGGL(ssim_combine_kernel, dim3(1), dim3(256), 0, s, stats, P.L, batch, channels,
+                       flags, out, reinterpret_cast<float2 *>(w + P.fac_off),
+                       reinterpret_cast<float *>(w + P.vals_off));
     return check_launch("ssim forward");
 }
 
@@ -549,11 +642,17 @@ extern "C" int gsvc_ssim_backward(int batch, int channels, int height, int width
             }
             float *dst = l == 0 ? dst0 : reinterpret_cast<float *>(w) + P.dx_off[l];
             const float *dc = l + 1 < levels ? reinterpret_cast<float *>(w) + P.dx_off[l + 1] : nullptr;
-            const dim3 grid(ceil_div(P.W[l], kSsimTW), ceil_div(P.H[l], kSsimTH), planes);
-            hipLaunchKernelGGL(ssim_bwd_kernel, grid, dim3(256), 0, s, xl, yl, P.H[l], P.W[l],
-                               P.L.Ho[l], P.L.Wo[l], P.win[l], C1, C2, fac + (size_t)l * planes,
-                               grad_out, gdiv, dc, l + 1 < levels ? P.H[l + 1] : 0,
-                               l + 1 < levels ? P.W[l + 1] : 0, P.pr[l], P.pc[l], dst);
+            float *coef = reinterpret_cast<float *>(w + P.coef_off);
+            const dim3 ogrid(ceil_div(P.L.Wo[l], kSsimTW), ceil_div(P.L.Ho[l], kSsimTH), planes);
+            auto kfn = ssim_moments_kernel<true>;
+            hipLaunchKernelGGL(kfn, ogrid, dim3(256), 0, s, xl, yl, P.H[l], P.W[l], P.L.Ho[l],
+                               P.L.Wo[l], P.win[l], C1, C2, nullptr, fac + (size_t)l * planes,
+                               grad_out, gdiv, coef);
+            const dim3 igrid(ceil_div(P.W[l], kSsimTW), ceil_div(P.H[l], kSsimTH), planes);
+            hipLaunchKernelGGL(ssim_grad_kernel, igrid, dim3(256), 0, s, coef, P.L.Ho[l], P.L.Wo[l],
+                               xl, yl, P.H[l], P.W[l], P.win[l], dc,
+                               l + 1 < levels ? P.H[l + 1] : 0, l + 1 < levels ? P.W[l + 1] : 0,
+                               P.pr[l], P.pc[l], dst);
         }
     }
     return check_launch("ssim backward");
