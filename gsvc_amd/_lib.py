@@ -59,8 +59,9 @@ _SIGS = {
     "gsvc_i420_to_rgb": [_P, _I, _I, _P, _P],
     "gsvc_ssim_workspace_bytes": [_I, _I, _I, _I, _I],
     "gsvc_ssim_forward": [_I, _I, _I, _I, _P, _P, _I, _F, _F, _F, _I, _P, _I, _P, _P, _SZ, _P],
+    "gsvc_ssim_backward_scratch_bytes": [_I, _I, _I, _I, _I],
     "gsvc_ssim_backward": [_I, _I, _I, _I, _P, _P, _I, _F, _F, _F, _I, _I, _P, _P, _P, _P, _SZ,
-                           _P],
+                           _P, _SZ, _P],
     "gsvc_render_frames_workspace_bytes": [_I, _I, _U, _U],
     "gsvc_render_frames_zeroed_bytes": [_I, _U, _U],
     "gsvc_render_frames_sum": [_I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _U, _U, _I, _I, _P, _P,
@@ -87,6 +88,7 @@ _RESTYPE = {
     "gsvc_render_frames_workspace_bytes": _SZ,
     "gsvc_render_frames_zeroed_bytes": _SZ,
     "gsvc_ssim_workspace_bytes": _SZ,
+    "gsvc_ssim_backward_scratch_bytes": _SZ,
 }
 
 ABI_VERSION = 1

@@ -178,7 +178,8 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
     if (threadIdx.x == 0) {
         int tot = 0;
 #pragma unroll
-        for (int k = 0; k < kProjThreads / 64; ++k) tot += s_hits[k];
+        for (int k = 0; k < kProjThreads / 64; ++k)
+            if (k < (int)(blockDim.x >> 6)) tot += s_hits[k];
         if (tot) atomicAdd(m_acc, tot);
     }
     if (kStamp) {
@@ -247,11 +248,13 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
         return check_launch("frame projection");
     }
     if (per > 0) {
-        const dim3 grid(ceil_div(per, kProjThreads / k), frames > 1 ? frames : 1);
+        // workgroup size: 256 unless A/B knob 1 picks 64 or 128
+        const int bs = g_knobs[1] == 64 || g_knobs[1] == 128 ? g_knobs[1] : kProjThreads;
+        const dim3 grid(ceil_div(per, bs / k), frames > 1 ? frames : 1);
 #define GSVC_FRAME_PROJECT(K)                                                                    \
     {                                                                                            \
         auto kfn = frame_project_kernel<K, false>;                                               \
-        hipLaunchKernelGGL(kfn, grid, dim3(kProjThreads), 0, s, n, xyz, xyz_tanh, chol,          \
+        hipLaunchKernelGGL(kfn, grid, dim3(bs), 0, s, n, xyz, xyz_tanh, chol,          \
                            chol_bound, feat, rgb_w, opac, hw, hh, tbx, tby, w.xys, w.radii,      \
                            w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero, nullptr,      \
                            frames > 1 ? frame_off : nullptr, f.counts_stride, f.m_stride,        \
@@ -259,7 +262,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
     }
         if (g_knobs[5] == 1 && g_debug_ptr) {  // diagnostic: per-wave stamps
             auto kfn = frame_project_kernel<1, true>;
-            hipLaunchKernelGGL(kfn, grid, dim3(kProjThreads), 0, s, n, xyz, xyz_tanh, chol,
+            hipLaunchKernelGGL(kfn, grid, dim3(bs), 0, s, n, xyz, xyz_tanh, chol,
                                chol_bound, feat, rgb_w, opac, hw, hh, tbx, tby, w.xys, w.radii,
                                w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero,
                                reinterpret_cast<long long *>(g_debug_ptr),

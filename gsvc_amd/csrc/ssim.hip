@@ -491,8 +491,11 @@ struct SsimPlan {
     SsimLevels L;
     // workspace
     size_t pyr_off[kSsimMaxLevels];  // floats: X_l at pyr_off[l], Y_l right after (l >= 1)
-    size_t dx_off[kSsimMaxLevels];   // floats: dX_l (l >= 1)
-    size_t part_off, coef_off, stats_off, fac_off, vals_off, bytes;
+    // forward workspace (kept for the backward): pyramid, partials, stats, factors
+    size_t part_off, stats_off, fac_off, vals_off, bytes;
+    // backward scratch: the coefficient maps of level 0's size, dX_l (l >= 1)
+    size_t dx_off[kSsimMaxLevels];   // floats
+    size_t coef_off, scratch_bytes;
 };
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -513,7 +516,7 @@ int make_plan(int planes, int H, int W, int win_size, float sigma, int levels,
     for (int t = 0; t < win_size; ++t) g[t] /= sum;
     P.levels = levels;
     P.L.n = levels;
-    size_t off = 0;  // bytes
+    size_t off = 0, soff = 0;  // bytes: workspace, scratch
     int h = H, w = W;
     long long part = 0;
     for (int l = 0; l < levels; ++l) {
@@ -535,8 +538,8 @@ int make_plan(int planes, int H, int W, int win_size, float sigma, int levels,
         if (l >= 1) {
             P.pyr_off[l] = off / sizeof(float);
             off += align256(sizeof(float) * 2 * (size_t)planes * h * w);
-            P.dx_off[l] = off / sizeof(float);
-            off += align256(sizeof(float) * (size_t)planes * h * w);
+            P.dx_off[l] = soff / sizeof(float);
+            soff += align256(sizeof(float) * (size_t)planes * h * w);
         }
         P.pr[l] = h % 2;
         P.pc[l] = w % 2;
@@ -546,8 +549,9 @@ int make_plan(int planes, int H, int W, int win_size, float sigma, int levels,
     }
     P.part_off = off;
     off += align256(sizeof(float2) * (size_t)part);
-    P.coef_off = off;  // the backward's coefficient maps, [P][3][Ho][Wo] of level 0
-    off += align256(sizeof(float) * 3 * (size_t)planes * P.L.Ho[0] * P.L.Wo[0]);
+    P.coef_off = soff;  // [P][3][Ho][Wo] of level 0
+    soff += align256(sizeof(float) * 3 * (size_t)planes * P.L.Ho[0] * P.L.Wo[0]);
+    P.scratch_bytes = soff;
     P.stats_off = off;
     off += align256(sizeof(double2) * (size_t)levels * planes);
     P.fac_off = off;
@@ -574,6 +578,13 @@ extern "C" size_t gsvc_ssim_workspace_bytes(int planes, int height, int width, i
     SsimPlan P;
     if (make_plan(planes, height, width, win_size, 1.5f, levels, nullptr, P) != 0) return 0;
     return P.bytes;
+}
+
+extern "C" size_t gsvc_ssim_backward_scratch_bytes(int planes, int height, int width,
+                                                   int win_size, int levels) {
+    SsimPlan P;
+    if (make_plan(planes, height, width, win_size, 1.5f, levels, nullptr, P) != 0) return 0;
+    return P.scratch_bytes;
 }
 
 extern "C" int gsvc_ssim_forward(int batch, int channels, int height, int width, const float *X,
@@ -619,14 +630,18 @@ extern "C" int gsvc_ssim_forward(int batch, int channels, int height, int width,
 extern "C" int gsvc_ssim_backward(int batch, int channels, int height, int width, const float *X,
                                   const float *Y, int win_size, float win_sigma, float C1,
                                   float C2, int levels, int flags, const float *grad_out,
-                                  float *dX, float *dY, void *ws, size_t ws_bytes, void *stream) {
+                                  float *dX, float *dY, void *ws, size_t ws_bytes, void *scratch,
+                                  size_t scratch_bytes, void *stream) {
     const int planes = batch * channels;
     SsimPlan P;
     if (int rc = make_plan(planes, height, width, win_size, win_sigma, levels, nullptr, P)) return rc;
-    if (!X || !Y || !grad_out || !ws) return set_error(GSVC_ERR_ARG, "ssim: missing buffer");
-    if (ws_bytes < P.bytes) return set_error(GSVC_ERR_WORKSPACE, "ssim: workspace too small");
+    if (!X || !Y || !grad_out || !ws || !scratch)
+        return set_error(GSVC_ERR_ARG, "ssim: missing buffer");
+    if (ws_bytes < P.bytes || scratch_bytes < P.scratch_bytes)
+        return set_error(GSVC_ERR_WORKSPACE, "ssim: workspace or scratch too small");
     hipStream_t s = (hipStream_t)stream;
     char *w = (char *)ws;
+    float *sc = reinterpret_cast<float *>(scratch);
     const float2 *fac = reinterpret_cast<const float2 *>(w + P.fac_off);
     const int gdiv = (flags & 1) ? 0 : channels;
     for (int side = 0; side < 2; ++side) {
@@ -640,9 +655,9 @@ extern "C" int gsvc_ssim_backward(int batch, int channels, int height, int width
                 xl = yl;
                 yl = t;
             }
-            float *dst = l == 0 ? dst0 : reinterpret_cast<float *>(w) + P.dx_off[l];
-            const float *dc = l + 1 < levels ? reinterpret_cast<float *>(w) + P.dx_off[l + 1] : nullptr;
-            float *coef = reinterpret_cast<float *>(w + P.coef_off);
+            float *dst = l == 0 ? dst0 : sc + P.dx_off[l];
+            const float *dc = l + 1 < levels ? sc + P.dx_off[l + 1] : nullptr;
+            float *coef = sc + P.coef_off / sizeof(float);
             const dim3 ogrid(ceil_div(P.L.Wo[l], kSsimTW), ceil_div(P.L.Ho[l], kSsimTH), planes);
             auto kfn = ssim_moments_kernel<true>;
             hipLaunchKernelGGL(kfn, ogrid, dim3(256), 0, s, xl, yl, P.H[l], P.W[l], P.L.Ho[l],

@@ -89,10 +89,13 @@ class _SsimFn(torch.autograd.Function):
         dX = torch.empty_like(Xc) if need_x else None
         dY = torch.empty_like(Yc) if need_y else None
         if need_x or need_y:
+            sc_bytes = L.size("gsvc_ssim_backward_scratch_bytes", B * C, H, W, win_size, levels)
+            scratch = torch.empty((sc_bytes,), dtype=torch.uint8, device=Xc.device)
             L.call("gsvc_ssim_backward", B, C, H, W, Xc.data_ptr(), Yc.data_ptr(), win_size,
                    win_sigma, C1, C2, levels, flags, g.data_ptr(),
                    dX.data_ptr() if need_x else None, dY.data_ptr() if need_y else None,
-                   ws.data_ptr(), ws.numel(), _raw_stream(Xc.device.index))
+                   ws.data_ptr(), ws.numel(), scratch.data_ptr(), sc_bytes,
+                   _raw_stream(Xc.device.index))
         if dX is not None:
             dX = dX.to(ctx.dtypes[0])
         if dY is not None:

@@ -361,11 +361,16 @@ int gsvc_ssim_forward(int batch, int channels, int height, int width, const floa
                       int levels, const double *weights, int flags, float *out, void *ws,
                       size_t ws_bytes, void *stream);
 /* d(out)/dX and/or d(out)/dY (either may be NULL) times grad_out (device,
- * out's shape). */
+ * out's shape).  `ws`: the forward's workspace; `scratch`: a temporary of
+ * gsvc_ssim_backward_scratch_bytes (the coefficient maps and coarse-level
+ * gradients; free after the call). */
+size_t gsvc_ssim_backward_scratch_bytes(int planes, int height, int width, int win_size,
+                                        int levels);
 int gsvc_ssim_backward(int batch, int channels, int height, int width, const float *X,
                        const float *Y, int win_size, float win_sigma, float C1, float C2,
                        int levels, int flags, const float *grad_out, float *dX, float *dY,
-                       void *ws, size_t ws_bytes, void *stream);
+                       void *ws, size_t ws_bytes, void *scratch, size_t scratch_bytes,
+                       void *stream);
 
 #ifdef __cplusplus
 }
