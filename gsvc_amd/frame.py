@@ -277,13 +277,15 @@ class GaussianVideoFrame(nn.Module):
                                               self.loss_type, state)
         losses = bs(gt, hparams, flags)
         loss = losses[LOSS_KIND[self.loss_type]]
-        psnr = 10 * math.log10(1.0 / float(losses[0]))
         # the step ran (keeps StepLR's call-order check quiet; the scheduler may
-        # hold the optimizer from before update_optimizer, as in the reference)
+        # hold the optimizer from before update_optimizer, as in the reference).
+        # The scheduler only sets the next iteration's lr, so it steps while the
+        # kernels run, before the PSNR read-back waits for them.
         opt._opt_called = True
         self.scheduler.optimizer._opt_called = True
         self.fused_steps += 1
         self.scheduler.step()
+        psnr = 10 * math.log10(1.0 / float(losses[0]))
         return loss, psnr
 
     def train_iter(self, gt_image, iter):
