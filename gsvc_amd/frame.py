@@ -151,11 +151,14 @@ class GaussianVideoFrame(nn.Module):
             self.optimizer = Adan(self.parameters(), lr=self.lr, fused=self.fused_adan)
 
     def _keep(self, keep):
+        # p[keep] for each parameter (GaussianSplats_Represent.py:122-125), with
+        # the mask's indices found once (one device->host count, not four)
         with torch.no_grad():
-            self._xyz = nn.Parameter(self._xyz[keep])
-            self._cholesky = nn.Parameter(self._cholesky[keep])
-            self._features_dc = nn.Parameter(self._features_dc[keep])
-            self.rgb_W = nn.Parameter(self.rgb_W[keep])
+            idx = keep.nonzero().squeeze(1)
+            self._xyz = nn.Parameter(self._xyz.index_select(0, idx))
+            self._cholesky = nn.Parameter(self._cholesky.index_select(0, idx))
+            self._features_dc = nn.Parameter(self._features_dc.index_select(0, idx))
+            self.rgb_W = nn.Parameter(self.rgb_W.index_select(0, idx))
 
     def _remove_lowest(self, sorted_indices, remove_count):
         keep = torch.ones(self._xyz.shape[0], dtype=torch.bool, device=self._xyz.device)
@@ -212,6 +215,25 @@ class GaussianVideoFrame(nn.Module):
             if remove_count > 0:
                 self._remove_lowest(sorted_indices, remove_count)
             self.update_optimizer()
+
+    def _control_replaces_params(self, iter):
+        """Whether train_iter's prune / densify at this iteration replaces the
+        parameters (adaptive_control / removal_control below): densify at
+        iteration 1, pruning inside their windows, and the final prune when it
+        removes anything.  Not the final update_optimizer alone, whose new
+        optimizer still steps on this iteration's gradients."""
+        final_remove = self._xyz.shape[0] - int(self.max_num_points * (1 - self.removal_rate)) > 0
+        if (iter == 1 or iter % self.densification_interval == 0) and self.isdensity:
+            if iter == 1:
+                return int(self.max_num_points * self.removal_rate) > 0
+            if iter < 500 or iter > 1000:
+                return False
+            return iter < 1000 or final_remove
+        if iter % self.densification_interval == 0 and self.isremoval:
+            if iter > 4000:
+                return False
+            return iter < 4000 or final_remove
+        return False
 
     def _fused_train_params(self, gt_image):
         """(rgb_W trainable?) when this iteration can run as one fused step
@@ -294,6 +316,22 @@ class GaussianVideoFrame(nn.Module):
         rgbw_train = None if controls else self._fused_train_params(gt_image)
         if rgbw_train is not None:
             return self._train_iter_fused(gt_image, rgbw_train)
+        if controls and self.fused_train and self._control_replaces_params(iter):
+            # the gradients of this iteration would be dropped unused: the
+            # control swaps in new Parameters (no .grad), so Adan only advances
+            # its step count.  Forward only (the same image bits and loss).
+            with torch.no_grad():
+                image = self.forward()["render"]
+                loss = loss_fn(image.squeeze(0), gt_image.squeeze(0), self.loss_type, lambda_value=0)
+                psnr = 10 * math.log10(1.0 / F.mse_loss(image, gt_image).item())
+            if (iter == 1 or iter % self.densification_interval == 0) and self.isdensity:
+                self.adaptive_control(iter)
+            else:
+                self.removal_control(iter)
+            self.optimizer.step()
+            self.optimizer.zero_grad(set_to_none=True)
+            self.scheduler.step()
+            return loss, psnr
         render_pkg = self.forward()
         image = render_pkg["render"]
         loss = loss_fn(image.squeeze(0), gt_image.squeeze(0), self.loss_type, lambda_value=0)

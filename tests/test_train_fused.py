@@ -197,3 +197,42 @@ def test_densify_iterations_interleave(cuda):
     for k, v in a.state_dict().items():
         np.testing.assert_allclose(v.cpu().numpy(), b.state_dict()[k].cpu().numpy(), rtol=0,
                                    atol=2e-5, err_msg=k)
+
+
+@pytest.mark.parametrize("mode,it", [("removal", 400), ("removal", 4000), ("removal", 4100),
+                                     ("densify", 1), ("densify", 600), ("densify", 1000),
+                                     ("densify", 300)])
+def test_control_iterations_match_op_path(cuda, mode, it):
+    """A prune / densify iteration (removal_control / adaptive_control) of the
+    fused model -- forward only when the control swaps in new Parameters --
+    leaves the same parameters, loss, PSNR, Adan step count and lr as the
+    op-by-op iteration (forward + backward + control + step); the next
+    (fused vs op-by-op) iteration then agrees too."""
+    from gsvc_amd.frame import synthetic_gt
+    H, W, n = 96, 128, 1500
+    gt = synthetic_gt(H, W, 3, cuda)
+    kw = dict(isremoval=mode == "removal", isdensity=mode == "densify", densification_interval=100,
+              max_num_points=n, removal_rate=0.1)
+    a = _model(H, W, n, cuda, seed=21, fused_train=True, **kw)
+    b = _model(H, W, n, cuda, seed=21, fused_train=False, **kw)
+    b.load_state_dict(a.state_dict())
+    for m in (a, b):  # one ordinary step first, so Adan has state to lose or keep
+        m.train_iter(gt, 2)
+    outs = []
+    for m in (a, b):
+        torch.manual_seed(5)
+        loss, psnr = m.train_iter(gt, it)
+        outs.append((float(loss), psnr))
+    assert outs[0][0] == outs[1][0] and outs[0][1] == outs[1][1]
+    assert a._xyz.shape == b._xyz.shape
+    for k, v in a.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), b.state_dict()[k].cpu().numpy(), rtol=0,
+                                   atol=2e-5, err_msg=k)
+    assert a.optimizer.param_groups[0]["step"] == b.optimizer.param_groups[0]["step"]
+    assert a.optimizer.param_groups[0]["lr"] == b.optimizer.param_groups[0]["lr"]
+    la, _ = a.train_iter(gt, it + 1)
+    lb, _ = b.train_iter(gt, it + 1)
+    np.testing.assert_allclose(float(la), float(lb), rtol=1e-5)
+    for k, v in a.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), b.state_dict()[k].cpu().numpy(), rtol=0,
+                                   atol=2e-5, err_msg=k)
