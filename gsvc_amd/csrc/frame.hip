@@ -50,12 +50,12 @@ __device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, i
         unsigned sl[kBatch];
 #pragma unroll
         for (int k = 0; k < kBatch; ++k)
-            if (k < cnt) sl[k] = atomicAdd(counts + tl[k], 1u);
+            if (k < cnt) sl[k] = (wt & 4) ? (unsigned)(tl[k] & 127) : atomicAdd(counts + tl[k], 1u);
 #pragma unroll
         for (int k = 0; k < kBatch; ++k)
-            if (k < cnt && sl[k] < (unsigned)kTilePix) {
+            if (k < cnt && sl[k] < (unsigned)kTilePix && !(wt & 2)) {
                 float4 *d = slab + ((size_t)tl[k] * kTilePix + sl[k]) * 3;
-                if (wt) {
+                if (wt & 1) {
                     store_wt(d, r0);
                     store_wt(d + 1, r1);
                     store_wt(d + 2, r2);
@@ -68,6 +68,9 @@ __device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, i
         hits += cnt;
         cnt = 0;
     };
+    // (wt & 6: timing-only A/B of gsvc_debug_set(2, v): 1 drops the record
+    // stores, 2 replaces the slot atomics by a fixed slot -- images are wrong;
+    // v = 4 (wt & 8) keeps one 32-bit atomic per tile instead of the pairs)
     unsigned y = y0 + (unsigned)sub / bw, x = x0 + (unsigned)sub % bw;
     while (y < y1) {
         tl[cnt < kBatch ? cnt : 0] = y * (unsigned)tbx + x;
@@ -76,6 +79,73 @@ __device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, i
         while (x >= x1) {
             x -= bw;
             ++y;
+        }
+    }
+    if (cnt) flush();
+    return hits;
+}
+
+// K = 1 insertion: the lane walks its bbox row by row; two horizontally
+// adjacent tiles whose counters share an aligned 8-byte word take ONE 64-bit
+// atomic adding 1 to both halves (a 32-bit count never carries into its
+// neighbour), so a splat k tiles wide costs ~k/2 + 1 slot atomics per row.
+// The memory-side atomic rate is what bounds the projection at high M
+// (trained-like 1080p / 50k splats: 794k insertions).
+__device__ __forceinline__ int slab_insert_pairs(float cx, float cy, int r, int tbx, int tby,
+                                                 float4 r0, float4 r1, float4 r2,
+                                                 unsigned *__restrict__ counts,
+                                                 float4 *__restrict__ slab, int wt) {
+    unsigned x0, y0, x1, y1;
+    tile_bbox(cx, cy, (float)r, tbx, tby, x0, y0, x1, y1);
+    if (x1 <= x0 || y1 <= y0) return 0;
+    constexpr int kBatch = 8;
+    const unsigned base_par = (unsigned)(reinterpret_cast<uintptr_t>(counts) >> 2) & 1u;
+    unsigned op[kBatch];  // tile << 1 | paired
+    int cnt = 0, hits = 0;
+    auto put = [&](unsigned t, unsigned sl) {
+        if (sl < (unsigned)kTilePix && !(wt & 2)) {
+            float4 *d = slab + ((size_t)t * kTilePix + sl) * 3;
+            d[0] = r0;
+            d[1] = r1;
+            d[2] = r2;
+        }
+    };
+    auto flush = [&]() {
+        unsigned lo[kBatch], hi[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            if (k < cnt) {
+                const unsigned t = op[k] >> 1;
+                if (op[k] & 1u) {
+                    const unsigned long long old = atomicAdd(
+                        reinterpret_cast<unsigned long long *>(counts + t), 0x100000001ull);
+                    lo[k] = (unsigned)old;
+                    hi[k] = (unsigned)(old >> 32);
+                } else {
+                    lo[k] = atomicAdd(counts + t, 1u);
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            if (k < cnt) {
+                const unsigned t = op[k] >> 1;
+                put(t, lo[k]);
+                if (op[k] & 1u) put(t + 1, hi[k]);
+                hits += 1 + (int)(op[k] & 1u);
+            }
+        }
+        cnt = 0;
+    };
+    const bool wide = x1 - x0 >= 3;  // narrow rows: single atomics (measured faster at 10k)
+    for (unsigned y = y0; y < y1; ++y) {
+        unsigned x = x0;
+        while (x < x1) {
+            const unsigned t = y * (unsigned)tbx + x;
+            const unsigned pair = (wide && x + 1 < x1 && ((t + base_par) & 1u) == 0) ? 1u : 0u;
+            op[cnt < kBatch ? cnt : 0] = (t << 1) | pair;
+            x += 1 + pair;
+            if (++cnt == kBatch) flush();
         }
     }
     if (cnt) flush();
@@ -152,7 +222,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
         for (int q = sub; q < 4; q += K) {
             if (q < 3) {
                 const float4 rq = q == 0 ? r0 : (q == 1 ? r1 : r2);
-                if (wt)
+                if (wt & 1)
                     store_wt(rec + 3 * i + q, rq);
                 else
                     rec[3 * i + q] = rq;
@@ -164,8 +234,14 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
             if (grad_zero) grad_zero[4 * i + q] = z;
         }
         if (kStamp && (threadIdx.x & 63) == 0) st[1] = proj_stamp();
-        if (P.rad > 0)
-            hits = slab_insert<K>(P.xy.x, P.xy.y, P.rad, tbx, tby, sub, r0, r1, r2, counts, slab, wt);
+        if (P.rad > 0) {
+            if (K == 1 && !(wt & 9))  // paired atomics unless write-through / A/B knob 2 = 4
+                hits = slab_insert_pairs(P.xy.x, P.xy.y, P.rad, tbx, tby, r0, r1, r2, counts,
+                                         slab, wt);
+            else
+                hits = slab_insert<K>(P.xy.x, P.xy.y, P.rad, tbx, tby, sub, r0, r1, r2, counts,
+                                      slab, wt);
+        }
     }
     if (kStamp) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -237,7 +313,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
     // plain record stores; A/B knob 6 = 1 writes them through (sc1): measured
     // slower (projection 7.1 -> 9.8 us at 10k: each scattered 16-byte sc1 store
     // is its own fabric write) and no faster for the composite's loads
-    const int wt = g_knobs[6] == 1 ? 1 : 0;
+    const int wt = (g_knobs[6] == 1 ? 1 : 0) | ((g_knobs[2] & 7) << 1);
     if (frames > 1 && !frame_off) return set_error(GSVC_ERR_ARG, "frame projection: frame offsets");
     const int per = frames > 1 ? max_frame_n : n;
     if (frames > 1 && per <= 0) {

@@ -63,14 +63,17 @@ def main():
             if kv:
                 lib.gsvc_debug_set(kv[0], kv[1])
 
+            hint = [0]  # the density hint render.py passes: M of an earlier frame
+
             def frame():
                 L.call("gsvc_render_frame_sum", n, L.ptr(xyz), 1, L.ptr(chol), L.ptr(bound),
-                       L.ptr(feat), None, None, L.ptr(bg), H, W, counter[0], 0, L.ptr(meta),
+                       L.ptr(feat), None, None, L.ptr(bg), H, W, counter[0], hint[0], L.ptr(meta),
                        L.ptr(ws), ws_bytes, L.ptr(out), L.stream(dev))
                 counter[0] += 1
 
             frame()
             torch.cuda.synchronize()
+            hint[0] = int(meta[0])
             gr = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gr):
                 for _ in range(args.iters):
