@@ -57,13 +57,13 @@ __device__ __forceinline__ float clamp_unit(float x) {
 
 // The pixels of the 16x16 tile at (tx0, ty0) at whose centres splat (x, y,
 // conic a b c, opacity o) can reach alpha >= 1/255, as a rectangle of tile
-// coordinates packed {x0, x1, y0, y1} (4 bits each, inclusive); 0xffffffff
+// coordinates packed {x0, x1, y0, y1} (4 bits each, inclusive); kNoRect
 // when provably none.  alpha >= 1/255 needs sigma <= ln(255 o), i.e.
 // d^T C d <= 2 ln(255 o), an ellipse with half-extents sqrt(2 ln(255 o) c / det)
 // and sqrt(2 ln(255 o) a / det); the margins (0.1 % + 0.01 px) dwarf fp32
 // rounding (the banded forward's test, raster_sum.hip ellipse_hits_rect).  A
 // culled (entry, pixel) pair contributes nothing in the reference either.
-constexpr unsigned kNoRect = 0xffffffffu;
+constexpr unsigned kNoRect = 0x000fu;  // x0 = 15 > x1 = 0: empty (fits the 16-bit LDS slot)
 constexpr unsigned kFullRect = 0xf0f0u;  // x 0..15, y 0..15
 
 __device__ __forceinline__ unsigned ellipse_rect(float x, float y, float a, float b, float c,
@@ -125,16 +125,18 @@ __device__ __forceinline__ long long tstamp() {
     return t;
 }
 
+// 8 workgroups per CU: <= 64 VGPRs (launch bound: 8 waves per SIMD) and
+// <= 20 KB of LDS (16-bit rectangles and item offsets).
 template <bool kStamp>
-__global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
+__global__ __launch_bounds__(256, 8) void train_tile_kernel(TrainTileArgs A) {
     // LDS: geo / col / pix, reused as the 9 x 256 gradient reduction buffer
-    // once the backward loop is done (16.5 KB per workgroup)
+    // once the backward loop is done
     __shared__ float4 s_buf[3 * kT];
     __shared__ float2 s_ext[kT];     // b, id bits
-    __shared__ unsigned s_rect[kT];  // pixels of the tile the entry can reach (ellipse_rect)
+    __shared__ unsigned short s_rect[kT];  // pixels of the tile the entry can reach (ellipse_rect)
     constexpr int kHalf = kT / 2;
     __shared__ float s_part[9][kHalf];  // backward: partial gradients of half a round of items
-    __shared__ int s_off[kT + 1];    // backward: first work item of each entry
+    __shared__ unsigned short s_off[kT + 1];  // backward: first work item of each entry (<= 8192)
     __shared__ int s_cnt[4];
     __shared__ float s_err[2][4];
     float4 *s_geo = s_buf;           // x, y, a/2, b
@@ -200,7 +202,7 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
         s_geo[rank] = r0;
         s_col[rank] = r1;
         s_ext[rank] = make_float2(r2.x, r2.y);
-        s_rect[rank] = ellipse_rect(r0.x, r0.y, r2.z, r0.w, r2.w, r1.y, tx0, ty0);
+        s_rect[rank] = (unsigned short)ellipse_rect(r0.x, r0.y, r2.z, r0.w, r2.w, r1.y, tx0, ty0);
     }
     __syncthreads();
     if (kStamp && tid == 0) st[1] = tstamp();
@@ -303,8 +305,8 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
     int wave_off = 0;
     for (int q = 0; q < w; ++q) wave_off += s_cnt[q];
     const int total = (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
-    if (tid < kend) s_off[tid] = wave_off + incl - items;
-    if (tid == 0) s_off[kend] = total;
+    if (tid < kend) s_off[tid] = (unsigned short)(wave_off + incl - items);
+    if (tid == 0) s_off[kend] = (unsigned short)total;
     if (kStamp && tid == 0) st[3] = tstamp();
     float acc[9];
 #pragma unroll
@@ -320,7 +322,7 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
             int lo = 0, hi = kend - 1;
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
-                if (s_off[mid] <= item) lo = mid;
+                if ((int)s_off[mid] <= item) lo = mid;
                 else hi = mid - 1;
             }
             const int e = lo;
@@ -328,7 +330,7 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
             const int rx0 = (int)(rc & 15u), rw = (int)((rc >> 4) & 15u) - rx0 + 1;
             const int ry0 = (int)((rc >> 8) & 15u);
             const int area = rw * ((int)((rc >> 12) & 15u) - ry0 + 1);
-            const int q0 = (item - s_off[e]) * kRun;
+            const int q0 = (item - (int)s_off[e]) * kRun;
             int yy = q0 / rw, xx = q0 - yy * rw;
             const float4 G = s_geo[e];
             const float4 C = s_col[e];
@@ -376,7 +378,7 @@ __global__ __launch_bounds__(256) void train_tile_kernel(TrainTileArgs A) {
             }
             __syncthreads();
             if (tid < kend) {
-                const int i0 = max(s_off[tid], hb), i1 = min(s_off[tid + 1], hb + kHalf);
+                const int i0 = max((int)s_off[tid], hb), i1 = min((int)s_off[tid + 1], hb + kHalf);
                 for (int it = i0; it < i1; ++it) {
 #pragma unroll
                     for (int c = 0; c < 9; ++c) acc[c] += s_part[c][it - hb];
