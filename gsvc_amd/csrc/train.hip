@@ -138,6 +138,8 @@ __global__ __launch_bounds__(256, 8) void train_tile_kernel(TrainTileArgs A) {
     __shared__ float s_part[9][kHalf];  // backward: partial gradients of half a round of items
     __shared__ unsigned short s_off[kT + 1];  // backward: first work item of each entry (<= 8192)
     __shared__ int s_cnt[4];
+    __shared__ int s_tot[4];         // backward: per-wave item totals (s_cnt still holds
+                                     // the last-entry maxima other waves may be reading)
     __shared__ float s_err[2][4];
     float4 *s_geo = s_buf;           // x, y, a/2, b
     float4 *s_col = s_buf + kT;      // c/2, opacity, r, g
@@ -300,11 +302,11 @@ __global__ __launch_bounds__(256, 8) void train_tile_kernel(TrainTileArgs A) {
         const int u = __shfl_up(incl, off, 64);
         if (lane >= off) incl += u;
     }
-    if (lane == 63) s_cnt[w] = incl;
+    if (lane == 63) s_tot[w] = incl;
     __syncthreads();
     int wave_off = 0;
-    for (int q = 0; q < w; ++q) wave_off += s_cnt[q];
-    const int total = (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
+    for (int q = 0; q < w; ++q) wave_off += s_tot[q];
+    const int total = (s_tot[0] + s_tot[1]) + (s_tot[2] + s_tot[3]);
     if (tid < kend) s_off[tid] = (unsigned short)(wave_off + incl - items);
     if (tid == 0) s_off[kend] = (unsigned short)total;
     if (kStamp && tid == 0) st[3] = tstamp();
