@@ -23,8 +23,8 @@
 //       the step reads gt once;
 //   train_splat_kernel  one lane per splat: projection VJP (the reference's
 //       doubled L cross term), activation VJPs and the Adan update of every
-//       parameter element; block 0 sums the tiles' errors in a fixed order
-//       into the loss.
+//       parameter element; an extra last workgroup sums the tiles' errors in
+//       a fixed order into the loss.
 #include "adan.h"
 #include "frame.h"
 
@@ -423,8 +423,9 @@ struct TrainSplatArgs {
 };
 
 __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
-    if (blockIdx.x == 0) {
-        // the loss: tiles' error sums in a fixed order, in double
+    if (blockIdx.x == gridDim.x - 1) {
+        // the last workgroup (no splats): the loss, the tiles' error sums in a
+        // fixed order, in double
         __shared__ double s_l[2][4];
         double s2 = 0.0, s1 = 0.0;
         for (int t0 = threadIdx.x; t0 < A.ntiles; t0 += 8 * 256) {
@@ -669,7 +670,8 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     P.grads_out = grads_out;
     P.err = w.err;
     P.loss = loss;
-    const int blocks = num_points > 0 ? ceil_div(num_points, 256) : 1;
+    // one extra (last) workgroup sums the loss, off the splat workgroups' path
+    const int blocks = (num_points > 0 ? ceil_div(num_points, 256) : 0) + 1;
     hipLaunchKernelGGL(train_splat_kernel, dim3(blocks), dim3(256), 0, s, P);
     return check_launch("train_step_sum: splats");
 }
