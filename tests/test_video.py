@@ -175,3 +175,16 @@ def test_video_driver_end_to_end(cuda, tmp_path):
                         "gmodels_state_dict.pth", weights_only=True)
     assert sorted(models) == [f"frame_{i}" for i in range(1, 7)]
     assert set(models["frame_2"]) == {"_xyz", "_cholesky", "_features_dc"}
+
+
+@pytest.mark.gpu
+def test_video_driver_reports_ms_ssim(cuda, tmp_path):
+    """Frames larger than ms_ssim's 160-pixel minimum get the per-frame MS-SSIM
+    of train_video_Represent.py:145 (gsvc_amd.msssim): finite, in (0, 1], and
+    equal to a direct ms_ssim of the final render."""
+    from gsvc_amd import video as V
+    res = V.main(["--synthetic", "2", "--height", "176", "--width", "200", "--num_points", "400",
+                  "--iterations", "200", "--k_frames", "1", "--root", str(tmp_path)])
+    ms = [r["ms_ssim"] for r in res["frames"]]
+    assert all(np.isfinite(ms)) and all(0.0 < m <= 1.0 for m in ms)
+    assert res["average"]["ms_ssim"] == pytest.approx(float(np.mean(ms)), rel=1e-6)
