@@ -13,13 +13,30 @@ inline int tiles_of(unsigned h, unsigned w) {
     return ceil_div((int)w, kTile) * ceil_div((int)h, kTile);
 }
 
+// Per frame, the slab region is a dense head [T][kHeadSlots][3] float4 (the
+// first slots of every tile: what the consumers load with the count -- 3 MB
+// at 1080p, so a batch of frames touches few pages for them) followed by the
+// body [T][256][3] (slots from kHeadSlots on, at their slot index).
+constexpr int kHeadSlots = 8;
+__host__ __device__ inline size_t slab_frame_f4(int ntiles) {
+    return (size_t)3 * (kHeadSlots + kTilePix) * (size_t)ntiles;
+}
+// Record of slot s of tile t in a frame's slab region.
+__host__ __device__ inline float4 *slab_rec(float4 *slab, int ntiles, int tile, int s) {
+    return s < kHeadSlots ? slab + ((size_t)tile * kHeadSlots + s) * 3
+                          : slab + (size_t)3 * kHeadSlots * ntiles + ((size_t)tile * kTilePix + s) * 3;
+}
+__host__ __device__ inline const float4 *slab_rec(const float4 *slab, int ntiles, int tile, int s) {
+    return slab_rec(const_cast<float4 *>(slab), ntiles, tile, s);
+}
+
 // Workspace of F frame models rendered together (base NULL: sizes only).  The
 // first ``zeroed`` bytes (counts and M slots) must be zero before the first
 // call; every call leaves them zero.
 struct FrameWs {
     unsigned *counts;  // [F][2][T]: per frame, this call's and the next call's
     int *m_slots;      // [F][2]
-    float4 *slab;      // [F][T][256][3] splat records
+    float4 *slab;      // [F] x (head [T][kHeadSlots][3] + body [T][256][3]) splat records
     float2 *xys;       // [N] (N = splats of all F frames)
     int *radii;        // [N]
     float4 *rec;       // [N][3] splat records

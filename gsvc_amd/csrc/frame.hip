@@ -42,6 +42,7 @@ __device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, i
     unsigned x0, y0, x1, y1;
     tile_bbox(cx, cy, (float)r, tbx, tby, x0, y0, x1, y1);
     if (x1 <= x0 || y1 <= y0) return 0;
+    const int ntiles = tbx * tby;
     const unsigned bw = x1 - x0;
     constexpr int kBatch = 8;
     unsigned tl[kBatch];
@@ -54,7 +55,7 @@ __device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, i
 #pragma unroll
         for (int k = 0; k < kBatch; ++k)
             if (k < cnt && sl[k] < (unsigned)kTilePix && !(wt & 2)) {
-                float4 *d = slab + ((size_t)tl[k] * kTilePix + sl[k]) * 3;
+                float4 *d = slab_rec(slab, ntiles, (int)tl[k], (int)sl[k]);
                 if (wt & 1) {
                     store_wt(d, r0);
                     store_wt(d + 1, r1);
@@ -104,7 +105,7 @@ __device__ __forceinline__ int slab_insert_pairs(float cx, float cy, int r, int 
     int cnt = 0, hits = 0;
     auto put = [&](unsigned t, unsigned sl) {
         if (sl < (unsigned)kTilePix && !(wt & 2)) {
-            float4 *d = slab + ((size_t)t * kTilePix + sl) * 3;
+            float4 *d = slab_rec(slab, tbx * tby, (int)t, (int)sl);
             d[0] = r0;
             d[1] = r1;
             d[2] = r2;
@@ -279,7 +280,7 @@ FrameWs frame_ws(char *base, int n, int ntiles, int frames) {
     w.counts = (unsigned *)take(sizeof(unsigned) * 2 * nt * nf + 2 * nf * sizeof(int));
     w.m_slots = (int *)(w.counts + 2 * nt * nf);
     w.zeroed = sizeof(unsigned) * 2 * nt * nf + 2 * nf * sizeof(int);
-    w.slab = (float4 *)take(sizeof(float4) * 3 * kTilePix * nt * nf);
+    w.slab = (float4 *)take(sizeof(float4) * slab_frame_f4((int)nt) * nf);
     w.xys = (float2 *)take(sizeof(float2) * nn);
     w.radii = (int *)take(sizeof(int) * nn);
     w.rec = (float4 *)take(sizeof(float4) * 3 * nn);
@@ -309,7 +310,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
     // lanes per splat: 1 unless gsvc_debug_set(4, k) picks 2, 4 or 8 (A/B knob;
     // measured at 1080p: equal at 10k splats, 1 lane fastest at 50k)
     const int k = g_knobs[4] == 2 || g_knobs[4] == 4 || g_knobs[4] == 8 ? g_knobs[4] : 1;
-    const size_t slab_stride = (size_t)3 * kTilePix * (size_t)(tbx * tby);
+    const size_t slab_stride = slab_frame_f4(tbx * tby);
     // plain record stores; A/B knob 6 = 1 writes them through (sc1): measured
     // slower (projection 7.1 -> 9.8 us at 10k: each scattered 16-byte sc1 store
     // is its own fabric write) and no faster for the composite's loads
@@ -417,7 +418,7 @@ static int render_frames(int frames, const int *frame_off_host, const int *frame
         A.frame_off = frame_off_dev;
         A.counts_stride = f.counts_stride;
         A.m_stride = f.m_stride;
-        A.slab_stride = (size_t)3 * kTilePix * (size_t)ntiles;
+        A.slab_stride = slab_frame_f4(ntiles);
         A.out_stride = (size_t)3 * img_width * img_height;
     }
     return sum_forward_launch(A, density_hint, s);

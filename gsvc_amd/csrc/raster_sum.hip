@@ -36,12 +36,13 @@
 // per entry (shuffles + LDS), then one 64-byte-aligned 9-float record per
 // (splat, tile) is added with 9 lanes of one atomic instruction (one memory
 // request per entry instead of the reference's 9 per warp).
+#include "frame.h"
 #include "raster_sum.h"
 
 namespace gsvc {
 
 constexpr int kChunk = 64;
-constexpr int kSpecSlots = 8;  // slab records loaded with the count (frame path)
+constexpr int kSpecSlots = kHeadSlots;  // slab records loaded with the count (frame path)
 constexpr int kSlice = kTilePix * 3 / 4;  // float4s of LDS per wave (3 KB)
 
 // Forward kernel modes.  Production: the launcher picks kModeSparse (one wave
@@ -214,9 +215,11 @@ constexpr int kSortWords = 512;
 // slab record (stride 12 floats).
 struct SegIds {
     const int *ids;
-    const float4 *recs;
+    const float4 *recs;  // slab body (slots >= kHeadSlots at their index) ...
+    const float4 *head;  // ... and the tile's head slots
     __device__ __forceinline__ int operator[](int j) const {
-        return recs ? __float_as_int(recs[3 * j + 2].y) : ids[j];
+        if (!recs) return ids[j];
+        return __float_as_int(j < kHeadSlots ? head[3 * j + 2].y : recs[3 * j + 2].y);
     }
 };
 
@@ -342,7 +345,7 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
             // <= 64 slab records in fill order: staged at their rank by id
             float4 geo = spec0, col = spec1, bx = spec2;
             if (lane >= kSpecSlots && lane < cnt) {
-                geo = seg_rec[3 * lane];
+                geo = seg_rec[3 * lane];  // body slots (lanes >= kSpecSlots = kHeadSlots)
                 col = seg_rec[3 * lane + 1];
                 bx = seg_rec[3 * lane + 2];
             }
@@ -467,7 +470,7 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
                 geo = spec0;
                 col = spec1;
                 if (lane >= kSpecSlots) {
-                    geo = seg_rec[3 * j];
+                    geo = seg_rec[3 * j];  // body slots (j >= kSpecSlots = kHeadSlots)
                     col = seg_rec[3 * j + 1];
                     bx = seg_rec[3 * j + 2];
                 }
@@ -601,12 +604,14 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         // this frame's count, and the first kSpecSlots records loaded in the
         // same round trip (speculatively: most tiles have that few)
         const int lane = threadIdx.x & 63;
-        const float4 *recs = A.slab + (size_t)tile * kTilePix * 3;
+        // slots >= kHeadSlots at their index from recs; the first ones in the head
+        const float4 *recs = slab_rec(A.slab, A.ntiles, tile, kHeadSlots) - 3 * kHeadSlots;
         n_all = (int)__builtin_amdgcn_readfirstlane(A.slab_counts[tile]);
         if (lane < kSpecSlots) {
-            spec0 = recs[3 * lane];
-            spec1 = recs[3 * lane + 1];
-            spec2 = recs[3 * lane + 2];
+            const float4 *h = slab_rec(A.slab, A.ntiles, tile, lane);
+            spec0 = h[0];
+            spec1 = h[1];
+            spec2 = h[2];
         }
         if (threadIdx.x == 0) {
             A.slab_counts_clear[tile] = 0u;  // the next frame's counts
@@ -618,13 +623,15 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         range = make_int2(0, n_all);
         seg.ids = nullptr;
         seg.recs = recs;
-        if (n_all <= kChunk) seg_rec = recs;
+        seg.head = slab_rec(A.slab, A.ntiles, tile, 0);
+        if (n_all <= kChunk) seg_rec = recs;  // slots past the head, at their index
     } else {
         range = A.bins[tile];
         n_all = range.y - range.x;
         n_all = n_all < 0 ? 0 : n_all;
         seg.ids = A.ids + range.x;
         seg.recs = nullptr;
+        seg.head = nullptr;
     }
     int n = n_all > kTilePix ? kTilePix : n_all;
     // rasterize_sum.py:121-127: a frame without intersections is the background

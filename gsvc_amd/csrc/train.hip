@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256, 8) void train_tile_kernel(TrainTileArgs A) {
     constexpr int kSpec = 32;
     float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
     if (tid < kSpec) {
-        const float4 *r = A.slab + ((size_t)tile * kT + tid) * 3;
+        const float4 *r = slab_rec(A.slab, A.ntiles, tile, tid);
         r0 = r[0];
         r1 = r[1];
         r2 = r[2];
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256, 8) void train_tile_kernel(TrainTileArgs A) {
     if (n_all <= kT) {
         int id = 0x7fffffff;
         if (tid >= kSpec && tid < n_all) {
-            const float4 *r = A.slab + ((size_t)tile * kT + tid) * 3;
+            const float4 *r = slab_rec(A.slab, A.ntiles, tile, tid);
             r0 = r[0];
             r1 = r[1];
             r2 = r[2];

@@ -256,7 +256,9 @@ def test_tanh_matches_torch(cuda):
     assert out.shape == (1, 3, 16, 16)
     from gsvc_amd.render import _workspaces
     fw = _workspaces[(0, torch.cuda.current_stream().cuda_stream)]
-    off = 256 + 256 * 48  # counts + M slots (256-aligned), one tile's 256-record slab
+    # counts + M slots (256-aligned), then one tile's slab region: the 8-record
+    # head and the 256-record body (frame.h slab_frame_f4), 256-aligned
+    off = 256 + ((8 + 256) * 48 + 255) // 256 * 256
     xys = fw.buf[off: off + 8 * n].view(torch.float32).view(n, 2)
     assert torch.equal(xys, ref)
 
