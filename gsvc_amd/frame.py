@@ -20,7 +20,7 @@ from . import msssim
 from .adan import Adan
 from .project_gaussians_2d import project_gaussians_2d
 from .rasterize_sum import rasterize_gaussians_sum
-from .render import render_frame_sum
+from .render import BoundRender, render_frame_sum
 from .train import LOSS_KIND, BoundStep
 
 
@@ -96,6 +96,7 @@ class GaussianVideoFrame(nn.Module):
         self.fused_train = kwargs.get("fused_train", str(self.device).startswith("cuda"))
         self.fused_steps = 0
         self._bound_step = None
+        self._bound_render = None
         self.update_optimizer()
         self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=20000, gamma=0.5)
 
@@ -128,10 +129,21 @@ class GaussianVideoFrame(nn.Module):
             # inference: same image from the sync-free path with the clamp +
             # NCHW epilogue fused into the rasterizer (gsvc_amd/render.py)
             # (activations fused into the frame kernel: tanh, + bound, * rgb_W)
-            return {"render": render_frame_sum(self._xyz, self._cholesky, self._features_dc,
-                                               self.H, self.W, self.background, xyz_tanh=True,
-                                               cholesky_bound=self.cholesky_bound,
-                                               rgb_w=self.rgb_W)}
+            bound = (self._xyz, self._cholesky, self._features_dc, self.background,
+                     self.cholesky_bound, self.rgb_W)
+            br = self._bound_render
+            if br is None or not br.matches(bound):
+                try:
+                    br = self._bound_render = BoundRender(
+                        self._xyz, self._cholesky, self._features_dc, self.H, self.W,
+                        self.background, cholesky_bound=self.cholesky_bound, rgb_w=self.rgb_W)
+                except ValueError:  # non-contiguous / non-fp32 tensors: the general call
+                    self._bound_render = None
+                    return {"render": render_frame_sum(
+                        self._xyz, self._cholesky, self._features_dc, self.H, self.W,
+                        self.background, xyz_tanh=True, cholesky_bound=self.cholesky_bound,
+                        rgb_w=self.rgb_W)}
+            return {"render": br()}
         # reference: torch.ones(N, 1).to(device) per call; same values
         _opacity = self._ones_opacity()
         self.xys, depths, self.radii, conics, num_tiles_hit = project_gaussians_2d(

@@ -103,6 +103,48 @@ def _render_frame_fn():
     return _render_fn
 
 
+class BoundRender:
+    """render_frame_sum bound to one frame model's tensors: the pointer checks
+    are done once, so a call costs the workspace lookup, the output
+    allocation and the C call.  The owner rebuilds it when a bound tensor
+    object or its storage changes (``matches``)."""
+
+    def __init__(self, xyz, cholesky, features, img_height, img_width, background,
+                 cholesky_bound=None, rgb_w=None):
+        n = xyz.shape[0]
+        self.tensors = (xyz, cholesky, features, background, cholesky_bound, rgb_w)
+        self.H, self.W, self.n = int(img_height), int(img_width), n
+        self.dev = xyz.device
+        keep = []
+        self.p = (_ptr_f32(xyz, "xyz", 2 * n, keep), _ptr_f32(cholesky, "cholesky", 3 * n, keep),
+                  _ptr_f32(features, "features", 3 * n, keep),
+                  _ptr_f32(background, "background", 3, keep),
+                  _ptr_f32(cholesky_bound, "cholesky_bound", 3, keep), _ptr_f32(rgb_w, "rgb_w", n, keep))
+        if keep:  # a converted copy would go stale: bind only tensors used in place
+            raise ValueError("BoundRender needs contiguous float32 CUDA tensors")
+        self.fn = _render_frame_fn()
+
+    def matches(self, tensors) -> bool:
+        return (len(tensors) == len(self.tensors)
+                and all(a is b for a, b in zip(tensors, self.tensors))
+                and all(t is None or t.data_ptr() == p for t, p in zip(tensors, self.p)))
+
+    def __call__(self) -> Tensor:
+        H, W, n = self.H, self.W, self.n
+        fw = _workspace(self.dev, n, H, W)
+        out = torch.empty((1, 3, H, W), dtype=_F32, device=self.dev)
+        p = self.p
+        rc = self.fn(n, p[0], 1, p[1], p[4], p[2], p[5], 0, p[3], H, W, fw.frame, fw.hint.value,
+                     fw.meta_ptr, fw.buf_ptr, fw.buf.numel(), out.data_ptr(), fw.stream)
+        if rc != 0:
+            fw.dirty = True
+            msg = L.load().gsvc_last_error().decode(errors="replace")
+            raise RuntimeError(f"gsvc_render_frame_sum failed (status {rc}): {msg}")
+        fw.frame += 1
+        fw.hint.update(fw.meta)
+        return out
+
+
 def render_frame_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, img_height: int,
                      img_width: int, background: Tensor, xyz_tanh: bool = True,
                      cholesky_bound: Optional[Tensor] = None, rgb_w: Optional[Tensor] = None,
