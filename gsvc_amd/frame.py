@@ -97,6 +97,7 @@ class GaussianVideoFrame(nn.Module):
         self.fused_steps = 0
         self._bound_step = None
         self._bound_render = None
+        self._fused_ok = None
         self.update_optimizer()
         self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=20000, gamma=0.5)
 
@@ -250,7 +251,34 @@ class GaussianVideoFrame(nn.Module):
     def _fused_train_params(self, gt_image):
         """(rgb_W trainable?) when this iteration can run as one fused step
         (train.py): L2 / L1 loss, Adan without gradient clipping, the model's
-        own parameters in one group, no gradients pending; else None."""
+        own parameters in one group, no gradients pending; else None.  The
+        configuration checks are cached against the objects they looked at
+        (optimizer, its group list, the parameters); per call only the pending
+        gradients and the target are checked."""
+        P = self._parameters
+        ps = (P.get("_xyz"), P.get("_cholesky"), P.get("_features_dc"),
+              P["rgb_W"] if "rgb_W" in P else self._buffers.get("rgb_W"))
+        opt = self.optimizer
+        c = self._fused_ok
+        if (c is not None and c[0] is opt and len(opt.param_groups) == 1
+                and c[1] is opt.param_groups[0]["params"] and all(a is b for a, b in zip(c[2], ps))
+                and c[4] == (self.fused_train, self.loss_type, opt.defaults["max_grad_norm"])):
+            for p in c[3]:
+                if (p.grad is not None or not p.requires_grad or p.dtype is not torch.float32
+                        or not p.is_contiguous()):
+                    return None
+            if gt_image.numel() != 3 * self.H * self.W or gt_image.device != ps[0].device:
+                return None
+            return c[5]
+        r = self._fused_train_params_full(gt_image)
+        self._fused_ok = None
+        if r is not None:
+            params = ps[:3] + ((ps[3],) if r else ())
+            self._fused_ok = (opt, opt.param_groups[0]["params"], ps, params,
+                              (self.fused_train, self.loss_type, opt.defaults["max_grad_norm"]), r)
+        return r
+
+    def _fused_train_params_full(self, gt_image):
         if not self.fused_train or self.loss_type not in LOSS_KIND or self.opt_type == "adam":
             return None
         if self.BLOCK_H != 16 or self.BLOCK_W != 16 or not self._xyz.is_cuda:
@@ -283,9 +311,11 @@ class GaussianVideoFrame(nn.Module):
         hparams = [b1, b2, b3, 1.0 - b1 ** step, 1.0 - b2 ** step, math.sqrt(1.0 - b3 ** step),
                    group["lr"], group["weight_decay"], group["eps"], 1.0]
         flags = 1 if group["no_prox"] else 0
+        P = self._parameters
+        xyz, chol, feat = P["_xyz"], P["_cholesky"], P["_features_dc"]
+        rgbw = P["rgb_W"] if "rgb_W" in P else self._buffers.get("rgb_W")  # a buffer when fixed
         state = []
-        for q, p in enumerate((self._xyz, self._cholesky, self._features_dc,
-                               self.rgb_W if rgbw_train else None)):
+        for q, p in enumerate((xyz, chol, feat, rgbw if rgbw_train else None)):
             if p is None:
                 state += [None] * 4
                 continue
@@ -303,8 +333,8 @@ class GaussianVideoFrame(nn.Module):
             gt = gt.float().contiguous()
         # the step bound to these tensors: pointers built once, rebuilt when any
         # parameter, state tensor or constant object changes
-        bound = (self._xyz, self._cholesky, self._features_dc, self.rgb_W, self.cholesky_bound,
-                 self.background, *state)
+        B = self._buffers
+        bound = (xyz, chol, feat, rgbw, B["cholesky_bound"], B["background"], *state)
         bs = self._bound_step
         if bs is None or bs.rgbw_train != int(rgbw_train) or not bs.matches(bound):
             bs = self._bound_step = BoundStep(*bound[:4], rgbw_train, *bound[4:6], self.H, self.W,

@@ -82,6 +82,7 @@ class BoundStep:
                  background, H, W, loss_type, adan_state):
         n = xyz.shape[0]
         self.tensors = (xyz, cholesky, features, rgb_w, cholesky_bound, background, *adan_state)
+        self.ids = tuple(map(id, self.tensors))  # the objects stay alive via self.tensors
         self.n, self.H, self.W = n, int(H), int(W)
         self.dev = xyz.device
         self.kind = LOSS_KIND[loss_type]
@@ -99,10 +100,12 @@ class BoundStep:
     def matches(self, tensors) -> bool:
         # identity, plus the parameters' storage (Module.to / ``p.data = ...``
         # swap it under the same object)
-        return (len(tensors) == len(self.tensors)
-                and all(a is b for a, b in zip(tensors, self.tensors))
-                and all(t is None or t.data_ptr() == p
-                        for t, p in zip(tensors[:4], (self.p[0], self.p[1], self.p[3], self.p[4]))))
+        if tuple(map(id, tensors)) != self.ids:
+            return False
+        p = self.p
+        return ((tensors[0].data_ptr() == p[0]) and (tensors[1].data_ptr() == p[1])
+                and (tensors[2].data_ptr() == p[3])
+                and (tensors[3] is None or tensors[3].data_ptr() == p[4]))
 
     def __call__(self, gt: Tensor, adan_hparams, adan_flags: int) -> Tensor:
         if not (gt.is_cuda and gt.dtype is torch.float32 and gt.is_contiguous()
