@@ -46,7 +46,7 @@ constexpr int kSpecSlots = kHeadSlots;  // slab records loaded with the count (f
 constexpr int kSlice = kTilePix * 3 / 4;  // float4s of LDS per wave (3 KB)
 
 // Forward kernel modes.  Production: the launcher picks kModeSparse (one wave
-// per tile) when the frame averages <= 5 entries per tile and kModeBanded
+// per tile) when the frame averages <= 8 entries per tile and kModeBanded
 // (two waves per tile) above, from the intersection count the caller already
 // holds (gsvc_rasterize_sum_forward_auto).  gsvc_debug_set(0, mode) forces a
 // mode for tools/kbench.py:
@@ -61,7 +61,7 @@ constexpr int kSlice = kTilePix * 3 / 4;  // float4s of LDS per wave (3 KB)
 // the dispatch rate of sparse tiles.
 enum { kModeAdaptive = 6, kModeSparse = 1, kModeBanded = 2, kModeStamp = 3, kModeNoBlend = 4,
        kModeNoStore = 5, kModeSparseStamp = 7 };
-constexpr int kDenseEntriesPerTile = 5;
+constexpr int kDenseEntriesPerTile = 8;  // measured crossover: 20k splats (6.1 per tile) sparse 22.1 vs banded 23.7 us, 30k (9.1) equal
 
 __device__ __forceinline__ void wave_lds_sync() {
     // a wave owns its LDS slice and LDS ops of a wave complete in order: a
