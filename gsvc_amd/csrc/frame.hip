@@ -51,10 +51,10 @@ __device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, i
         unsigned sl[kBatch];
 #pragma unroll
         for (int k = 0; k < kBatch; ++k)
-            if (k < cnt) sl[k] = (wt & 4) ? (unsigned)(tl[k] & 127) : atomicAdd(counts + tl[k], 1u);
+            if (k < cnt) sl[k] = atomicAdd(counts + tl[k], 1u);
 #pragma unroll
         for (int k = 0; k < kBatch; ++k)
-            if (k < cnt && sl[k] < (unsigned)kTilePix && !(wt & 2)) {
+            if (k < cnt && sl[k] < (unsigned)kTilePix) {
                 float4 *d = slab_rec(slab, ntiles, (int)tl[k], (int)sl[k]);
                 if (wt & 1) {
                     store_wt(d, r0);
@@ -69,9 +69,6 @@ __device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, i
         hits += cnt;
         cnt = 0;
     };
-    // (wt & 6: timing-only A/B of gsvc_debug_set(2, v): 1 drops the record
-    // stores, 2 replaces the slot atomics by a fixed slot -- images are wrong;
-    // v = 4 (wt & 8) keeps one 32-bit atomic per tile instead of the pairs)
     unsigned y = y0 + (unsigned)sub / bw, x = x0 + (unsigned)sub % bw;
     while (y < y1) {
         tl[cnt < kBatch ? cnt : 0] = y * (unsigned)tbx + x;
@@ -104,7 +101,7 @@ __device__ __forceinline__ int slab_insert_pairs(float cx, float cy, int r, int 
     unsigned op[kBatch];  // tile << 1 | paired
     int cnt = 0, hits = 0;
     auto put = [&](unsigned t, unsigned sl) {
-        if (sl < (unsigned)kTilePix && !(wt & 2)) {
+        if (sl < (unsigned)kTilePix) {
             float4 *d = slab_rec(slab, tbx * tby, (int)t, (int)sl);
             d[0] = r0;
             d[1] = r1;
@@ -236,7 +233,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
         }
         if (kStamp && (threadIdx.x & 63) == 0) st[1] = proj_stamp();
         if (P.rad > 0) {
-            if (K == 1 && !(wt & 9))  // paired atomics unless write-through / A/B knob 2 = 4
+            if (K == 1 && !(wt & 3))  // paired atomics unless write-through / A/B knob 2 = 4
                 hits = slab_insert_pairs(P.xy.x, P.xy.y, P.rad, tbx, tby, r0, r1, r2, counts,
                                          slab, wt);
             else
@@ -314,7 +311,10 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
     // plain record stores; A/B knob 6 = 1 writes them through (sc1): measured
     // slower (projection 7.1 -> 9.8 us at 10k: each scattered 16-byte sc1 store
     // is its own fabric write) and no faster for the composite's loads
-    const int wt = (g_knobs[6] == 1 ? 1 : 0) | ((g_knobs[2] & 7) << 1);
+    // bit 0: write-through record stores (A/B knob 6 = 1); bit 1: one 32-bit
+    // slot atomic per tile instead of the pairs (A/B knob 2 = 4).  Measured
+    // with the isolation runs of profiles/r01/paired_atomics/NOTES.md.
+    const int wt = (g_knobs[6] == 1 ? 1 : 0) | (g_knobs[2] == 4 ? 2 : 0);
     if (frames > 1 && !frame_off) return set_error(GSVC_ERR_ARG, "frame projection: frame offsets");
     const int per = frames > 1 ? max_frame_n : n;
     if (frames > 1 && per <= 0) {
