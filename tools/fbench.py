@@ -89,6 +89,28 @@ def main():
                 b.record()
                 torch.cuda.synchronize()
                 best = min(best, a.elapsed_time(b) * 1e3 / args.iters)
+            # the same frame as a one-frame graph replayed per step (host
+            # submits one graph per frame, as a per-call graph launch would)
+            g1 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                frame()
+            g1.replay()
+            torch.cuda.synchronize()
+            a1 = torch.cuda.Event(enable_timing=True)
+            b1 = torch.cuda.Event(enable_timing=True)
+            a1.record()
+            for _ in range(args.iters):
+                g1.replay()
+            b1.record()
+            torch.cuda.synchronize()
+            per_graph = a1.elapsed_time(b1) * 1e3 / args.iters
+            # and as plain launches (the library call per step, no graph)
+            a1.record()
+            for _ in range(args.iters):
+                frame()
+            b1.record()
+            torch.cuda.synchronize()
+            per_launch = a1.elapsed_time(b1) * 1e3 / args.iters
             same = True
             if ref is None:
                 ref = out.clone()
@@ -99,6 +121,8 @@ def main():
                 lib.gsvc_debug_set(kv[0], 0)
             print(json.dumps(dict(N=n, M=m, mode=mode, knob=kv,
                                   us_per_frame=round(best, 2), fps=round(1e6 / best, 0),
+                                  us_one_frame_graphs=round(per_graph, 2),
+                                  us_plain_launches=round(per_launch, 2),
                                   identical=same)), flush=True)
         if args.stamps:
             import numpy as np
