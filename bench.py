@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--timing", choices=["dispatch", "marker"], default="dispatch",
+                    help="composite-kernel HIP events: carried by the timed dispatch "
+                         "(hipExtLaunchKernel) or recorded around it")
     return ap.parse_args()
 
 
@@ -242,7 +245,8 @@ def main():
         torch.cuda.synchronize()
         # HIP events around every 16th composite launch of the timed region,
         # recorded by the library on the kernel's own stream
-        ops.composite_timing(True, max_launches=args.steps, every=16)
+        ops.composite_timing(True, max_launches=args.steps, every=16,
+                             dispatch=args.timing == "dispatch")
         barrier(world)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -269,10 +273,13 @@ def main():
     roof = {"kernel": "rasterize_sum_forward", "bound": "hbm", "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic, "avg_kernel_us": round(avg_ms * 1e3, 2),
-            "algorithmic_bytes_per_launch": nbytes, "shape": shape}
+            "algorithmic_bytes_per_launch": nbytes, "shape": shape,
+            "timing": ("HIP events carried by every 16th composite dispatch (hipExtLaunchKernel)"
+                       if args.timing == "dispatch" else
+                       "HIP events recorded around every 16th composite launch")}
     if trace_us:
-        # the same kernel's duration in the committed rocprofv3 kernel trace: the
-        # HIP events above include ~2-3 us of event-packet / dispatch latency
+        # the same kernel's duration in the committed rocprofv3 kernel trace
+        # (marker events around the launch add ~3 us of packet / dispatch latency)
         roof["trace_avg_kernel_us"] = round(trace_us, 2)
         roof["frac_by_trace"] = round(nbytes / (trace_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
     line = {

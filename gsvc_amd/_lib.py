@@ -30,7 +30,7 @@ _SIGS = {
     "gsvc_last_error": [],
     "gsvc_debug_set": [_I, _I],
     "gsvc_debug_set_ptr": [_P],
-    "gsvc_timing_enable": [_I, _I],
+    "gsvc_timing_enable": [_I, _I, _I],
     "gsvc_timing_collect": [_P, _I, _P],
     "gsvc_project_gaussians_2d_forward": [_I, _P, _P, _U, _U, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P],
     "gsvc_project_gaussians_2d_backward": [_I, _P, _P, _U, _U, _P, _P, _P, _P, _P, _P, _P, _P, _P],

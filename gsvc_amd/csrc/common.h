@@ -23,7 +23,9 @@ int set_error(int code, const char *fmt, ...);
 int check_launch(const char *what);
 extern int g_knobs[8];  // gsvc_debug_set(); knob 0 = sum-forward variant
 extern void *g_debug_ptr;  // gsvc_debug_set_ptr(): diagnostic output buffer
-int timing_begin(hipStream_t s);  // timing.hip: -1 when not recording
+// timing.hip: slot, or -1 when not recording; dispatch_ev[2] = the events the
+// launch must carry itself (hipExtLaunchKernel), both null otherwise
+int timing_begin(hipStream_t s, hipEvent_t *dispatch_ev);
 void timing_end(hipStream_t s, int slot);
 
 // XCD-aware block -> work-item remap.  Blocks b and b+8 share an XCD (they are

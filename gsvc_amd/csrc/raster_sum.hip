@@ -36,6 +36,8 @@
 // per entry (shuffles + LDS), then one 64-byte-aligned 9-float record per
 // (splat, tile) is added with 9 lanes of one atomic instruction (one memory
 // request per entry instead of the reference's 9 per warp).
+#include <hip/hip_ext.h>
+
 #include "frame.h"
 #include "raster_sum.h"
 
@@ -817,6 +819,17 @@ void sum_fwd_args_init(SumFwdArgs &A) {
     A.frames = 1;
 }
 
+// A timed launch carries its HIP events in the dispatch (timing.hip, how = 1);
+// every other launch is a plain one.
+template <typename K>
+static void launch_fwd(K kernel, dim3 grid, dim3 block, hipStream_t s, const hipEvent_t *tev,
+                       const SumFwdArgs &A) {
+    if (tev[0])
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, s, tev[0], tev[1], 0, A);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, 0, s, A);
+}
+
 int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
     A.vec = (A.img_w % 4 == 0) && (((uintptr_t)A.out & 15) == 0) &&
             (((uintptr_t)A.final_idx & 15) == 0) && (((uintptr_t)A.final_Ts & 15) == 0);
@@ -832,34 +845,35 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
         return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: stamp mode needs the HWC layout");
     if (A.frames > 1 && (mode == kModeStamp || mode == kModeSparseStamp))
         return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: stamp modes render one frame");
-    const int tslot = timing_begin(s);
+    hipEvent_t tev[2];
+    const int tslot = timing_begin(s, tev);
     const dim3 grid(ntiles * A.frames);
     switch (mode) {
         case kModeSparse:
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeSparse>, grid, dim3(64), 0, s, A);
+            launch_fwd(raster_sum_fwd_kernel<kModeSparse>, grid, dim3(64), s, tev, A);
             break;
         case kModeBanded:
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeBanded>, grid, dim3(128), 0, s, A);
+            launch_fwd(raster_sum_fwd_kernel<kModeBanded>, grid, dim3(128), s, tev, A);
             break;
         case kModeStamp:
             A.stamps = reinterpret_cast<long long *>(A.final_Ts);
             A.final_Ts = nullptr;
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeStamp>, grid, dim3(128), 0, s, A);
+            launch_fwd(raster_sum_fwd_kernel<kModeStamp>, grid, dim3(128), s, tev, A);
             break;
         case kModeNoBlend:
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeNoBlend>, grid, dim3(128), 0, s, A);
+            launch_fwd(raster_sum_fwd_kernel<kModeNoBlend>, grid, dim3(128), s, tev, A);
             break;
         case kModeNoStore:
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeNoStore>, grid, dim3(128), 0, s, A);
+            launch_fwd(raster_sum_fwd_kernel<kModeNoStore>, grid, dim3(128), s, tev, A);
             break;
         case kModeAdaptive:
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeAdaptive>, grid, dim3(128), 0, s, A);
+            launch_fwd(raster_sum_fwd_kernel<kModeAdaptive>, grid, dim3(128), s, tev, A);
             break;
         case kModeSparseStamp:
             if (!g_debug_ptr)
                 return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: mode 7 needs gsvc_debug_set_ptr");
             A.stamps = reinterpret_cast<long long *>(g_debug_ptr);
-            hipLaunchKernelGGL(raster_sum_fwd_kernel<kModeSparseStamp>, grid, dim3(64), 0, s, A);
+            launch_fwd(raster_sum_fwd_kernel<kModeSparseStamp>, grid, dim3(64), s, tev, A);
             break;
         default:
             return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: unknown kernel mode %d", mode);

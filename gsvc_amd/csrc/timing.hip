@@ -1,6 +1,10 @@
 // Launch timing of the composite kernel with HIP events (bench.py's roofline):
-// when enabled, every ``every``-th sum-forward launch is bracketed by two
-// events recorded on the stream it is launched on.
+// when enabled, every ``every``-th sum-forward launch is timed by two events on
+// the stream it is launched on.  Two ways (gsvc_timing_enable's ``how``):
+//   0  marker events recorded before and after the launch (hipEventRecord):
+//      includes the marker packets' latency and the kernel's dispatch, ~3 us
+//   1  the launch itself carries the events (hipExtLaunchKernel): the
+//      dispatch packet's own start / end timestamps, as rocprofv3's kernel trace
 #include <mutex>
 #include <vector>
 
@@ -10,22 +14,28 @@ namespace gsvc {
 
 static std::mutex g_tmu;
 static std::vector<hipEvent_t> g_tev;  // pairs
-static int g_tevery = 1, g_tcalls = 0, g_tused = 0;
+static int g_tevery = 1, g_tcalls = 0, g_tused = 0, g_thow = 0;
 
-int timing_begin(hipStream_t s) {
+int timing_begin(hipStream_t s, hipEvent_t *dispatch_ev) {
+    dispatch_ev[0] = dispatch_ev[1] = nullptr;
     std::lock_guard<std::mutex> lk(g_tmu);
     if (g_tev.empty()) return -1;
     if ((g_tcalls++) % g_tevery) return -1;
     if (2 * (g_tused + 1) > (int)g_tev.size()) return -1;
     const int slot = g_tused++;
-    hipEventRecord(g_tev[2 * slot], s);
+    if (g_thow == 1) {
+        dispatch_ev[0] = g_tev[2 * slot];
+        dispatch_ev[1] = g_tev[2 * slot + 1];
+    } else {
+        hipEventRecord(g_tev[2 * slot], s);
+    }
     return slot;
 }
 
 void timing_end(hipStream_t s, int slot) {
     if (slot < 0) return;
     std::lock_guard<std::mutex> lk(g_tmu);
-    hipEventRecord(g_tev[2 * slot + 1], s);
+    if (g_thow != 1) hipEventRecord(g_tev[2 * slot + 1], s);
 }
 
 static void timing_free() {
@@ -38,11 +48,13 @@ static void timing_free() {
 
 using namespace gsvc;
 
-extern "C" int gsvc_timing_enable(int max_launches, int every) {
+extern "C" int gsvc_timing_enable(int max_launches, int every, int how) {
     std::lock_guard<std::mutex> lk(g_tmu);
     timing_free();
     if (max_launches <= 0) return GSVC_OK;
+    if (how != 0 && how != 1) return set_error(GSVC_ERR_ARG, "timing_enable: how must be 0 or 1");
     g_tevery = every > 0 ? every : 1;
+    g_thow = how;
     g_tev.resize(2 * (size_t)max_launches);
     for (hipEvent_t &e : g_tev)
         if (hipEventCreate(&e) != hipSuccess) {

@@ -48,10 +48,12 @@ def enable_kernel_timing(on: bool = True, every: int = 1):
     return _kernel_events
 
 
-def composite_timing(on: bool, max_launches: int = 4096, every: int = 1):
+def composite_timing(on: bool, max_launches: int = 4096, every: int = 1, dispatch: bool = False):
     """C-side HIP-event timing of the sum-forward kernel launches (every
-    entry point, including the fused frame render); see gsvc_timing_enable."""
-    L.call("gsvc_timing_enable", int(max_launches) if on else 0, int(every))
+    entry point, including the fused frame render); see gsvc_timing_enable.
+    ``dispatch``: the timed launch carries the events itself (the kernel's own
+    start / end) instead of events recorded around it."""
+    L.call("gsvc_timing_enable", int(max_launches) if on else 0, int(every), 1 if dispatch else 0)
 
 
 def composite_times_ms(max_launches: int = 4096):

@@ -62,11 +62,14 @@ int gsvc_adan_step(int ntensors, const long long *numels, float *const *params,
                    int no_prox, double clip_global_grad_norm, void *stream);
 
 /* Launch timing of the sum-forward composite kernel (every rasterizer entry
- * point above): after gsvc_timing_enable(max, every), every every-th launch
- * is bracketed by HIP events recorded on its stream (up to max launches);
+ * point above): after gsvc_timing_enable(max, every, how), every every-th
+ * launch is timed by HIP events on its stream (up to max launches) -- how = 0:
+ * events recorded before and after the launch (includes the marker packets and
+ * the dispatch, ~3 us); how = 1: events carried by the dispatch itself
+ * (hipExtLaunchKernel: the kernel's own start / end, as a kernel trace).
  * gsvc_timing_collect waits for them and writes the durations in ms.
- * gsvc_timing_enable(0, 0) stops and frees.  Not part of the reference. */
-int gsvc_timing_enable(int max_launches, int every);
+ * gsvc_timing_enable(0, 0, 0) stops and frees.  Not part of the reference. */
+int gsvc_timing_enable(int max_launches, int every, int how);
 int gsvc_timing_collect(float *ms, int max_out, int *count);
 
 /* Tuning / A-B knob for kernel variants (tools/kbench.py).  key 0 forces the
