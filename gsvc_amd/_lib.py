@@ -32,6 +32,8 @@ _SIGS = {
     "gsvc_debug_set_ptr": [_P],
     "gsvc_timing_enable": [_I, _I, _I],
     "gsvc_timing_collect": [_P, _I, _P],
+    "gsvc_prune_workspace_bytes": [_I],
+    "gsvc_prune_lowest": [_I, _I, _P, _I, _P, _P, _P, _P, _SZ, _P],
     "gsvc_project_gaussians_2d_forward": [_I, _P, _P, _U, _U, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P],
     "gsvc_project_gaussians_2d_backward": [_I, _P, _P, _U, _U, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "gsvc_compute_cov2d_bounds": [_I, _P, _P, _P, _P],
@@ -79,6 +81,7 @@ _RESTYPE = {
     "gsvc_debug_set_ptr": None,
     "gsvc_last_error": ctypes.c_char_p,
     "gsvc_cumsum_workspace_bytes": _SZ,
+    "gsvc_prune_workspace_bytes": _SZ,
     "gsvc_sort_pairs_workspace_bytes": _SZ,
     "gsvc_bin_tiles_workspace_bytes": _SZ,
     "gsvc_bin_tiles_counted_workspace_bytes": _SZ,

@@ -20,6 +20,7 @@ from . import msssim
 from .adan import Adan
 from .project_gaussians_2d import project_gaussians_2d
 from .rasterize_sum import rasterize_gaussians_sum
+from .prune import prune_lowest
 from .render import BoundRender, render_frame_sum
 from .train import LOSS_KIND, BoundStep
 
@@ -163,20 +164,13 @@ class GaussianVideoFrame(nn.Module):
         else:
             self.optimizer = Adan(self.parameters(), lr=self.lr, fused=self.fused_adan)
 
-    def _keep(self, keep):
-        # p[keep] for each parameter (GaussianSplats_Represent.py:122-125), with
-        # the mask's indices found once (one device->host count, not four)
+    def _remove_lowest(self, remove_count):
+        # norm + torch.sort + boolean mask + p[keep] (GaussianSplats_Represent.py:
+        # 101-125, 149-166) as one radix select and compaction on the GPU
         with torch.no_grad():
-            idx = keep.nonzero().squeeze(1)
-            self._xyz = nn.Parameter(self._xyz.index_select(0, idx))
-            self._cholesky = nn.Parameter(self._cholesky.index_select(0, idx))
-            self._features_dc = nn.Parameter(self._features_dc.index_select(0, idx))
-            self.rgb_W = nn.Parameter(self.rgb_W.index_select(0, idx))
-
-    def _remove_lowest(self, sorted_indices, remove_count):
-        keep = torch.ones(self._xyz.shape[0], dtype=torch.bool, device=self._xyz.device)
-        keep[sorted_indices[:remove_count]] = False
-        self._keep(keep)
+            ps = prune_lowest(self.rgb_W, [self._xyz, self._cholesky, self._features_dc, self.rgb_W],
+                              remove_count)
+            self._xyz, self._cholesky, self._features_dc, self.rgb_W = (nn.Parameter(p) for p in ps)
 
     def _refresh_groups(self):
         for param_group in self.optimizer.param_groups:
@@ -187,16 +181,14 @@ class GaussianVideoFrame(nn.Module):
         iter_threshold_remove = 4000
         if iter > iter_threshold_remove:
             return
-        rgb_weight = torch.norm(self.rgb_W, dim=1)
-        _, sorted_indices = torch.sort(rgb_weight)
         removal_rate_per_step = self.removal_rate / int(iter_threshold_remove / self.densification_interval)
         if iter < iter_threshold_remove:
-            self._remove_lowest(sorted_indices, int(removal_rate_per_step * self.max_num_points))
+            self._remove_lowest(int(removal_rate_per_step * self.max_num_points))
             self._refresh_groups()
         elif iter == iter_threshold_remove:
             remove_count = self._xyz.shape[0] - int(self.max_num_points * (1 - self.removal_rate))
             if remove_count > 0:
-                self._remove_lowest(sorted_indices, remove_count)
+                self._remove_lowest(remove_count)
             self.update_optimizer()
 
     def adaptive_control(self, iter):
@@ -217,16 +209,14 @@ class GaussianVideoFrame(nn.Module):
                 self.rgb_W = nn.Parameter(torch.cat((self.rgb_W, new_rgb_W), dim=0))
                 self._refresh_groups()
             return
-        rgb_weight = torch.norm(self.rgb_W, dim=1)
-        _, sorted_indices = torch.sort(rgb_weight)
         if iter < iter_threshold_add + iter_threshold_remove:
             remove_count = int(densification_num / int(iter_threshold_remove / self.densification_interval))
-            self._remove_lowest(sorted_indices, remove_count)
+            self._remove_lowest(remove_count)
             self._refresh_groups()
         elif iter == iter_threshold_add + iter_threshold_remove:
             remove_count = self._xyz.shape[0] - int(self.max_num_points * (1 - self.removal_rate))
             if remove_count > 0:
-                self._remove_lowest(sorted_indices, remove_count)
+                self._remove_lowest(remove_count)
             self.update_optimizer()
 
     def _control_replaces_params(self, iter):

@@ -61,6 +61,21 @@ int gsvc_adan_step(int ntensors, const long long *numels, float *const *params,
                    double bias_correction3_sqrt, double lr, double weight_decay, double eps,
                    int no_prox, double clip_global_grad_norm, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * Pruning of a frame model (GaussianSplats_Represent.py:101-125 removal_control
+ * and :149-166 adaptive_control: norm of rgb_W, torch.sort, boolean-mask
+ * rebuild of _xyz / _cholesky / _features_dc / rgb_W).  Removes the
+ * remove_count splats of smallest ||rgb_W|| (rgb_w: fp32 [num_points, 1];
+ * equal norms leave in index order, as the GPU's stable torch.sort) and writes
+ * the kept rows, in order, of each of the ntensors fp32 [num_points, cols[t]]
+ * tensors src[t] to dst[t] ([num_points - remove_count, cols[t]]; src and dst
+ * must not overlap).  Host arrays of device pointers; no host sync.
+ * remove_count >= num_points keeps nothing and launches nothing. */
+size_t gsvc_prune_workspace_bytes(int num_points);
+int gsvc_prune_lowest(int num_points, int remove_count, const float *rgb_w, int ntensors,
+                      const int *cols, const float *const *src, float *const *dst,
+                      void *workspace, size_t workspace_bytes, void *stream);
+
 /* Launch timing of the sum-forward composite kernel (every rasterizer entry
  * point above): after gsvc_timing_enable(max, every, how), every every-th
  * launch is timed by HIP events on its stream (up to max launches) -- how = 0:

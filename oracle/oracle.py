@@ -13,6 +13,7 @@ Every function mirrors one reference operator (paths relative to
   bin_and_sort                    utils.py:121-167
   raster_sum_forward / backward   rasterize_sum.py:92-254 -> forward.cu:512-627, backward.cu:696-862
   raster_forward / backward       rasterize.py:89-253 -> forward.cu:252-374, backward.cu:138-315
+  prune_keep                      /root/reference/GaussianSplats_Represent.py:101-125, 149-166
 """
 from __future__ import annotations
 
@@ -350,3 +351,17 @@ def ms_ssim(X, Y, data_range=255.0, size_average=True, win_size=11, win_sigma=1.
     stack = np.stack(mcs + [np.maximum(s, 0.0)], axis=0)  # [levels, B, C]
     val = np.prod(stack ** w[:, None, None], axis=0)
     return val.mean() if size_average else val.mean(axis=1)
+
+
+def prune_keep(rgb_w: np.ndarray, remove_count: int) -> np.ndarray:
+    """GaussianSplats_Represent.py:101-125 / 149-166: keep mask after removing
+    the ``remove_count`` smallest ``torch.norm(rgb_W, dim=1)`` -- float32
+    sqrt(w*w) per row ([N, 1]), ordered as the GPU's stable torch.sort
+    (ties by index, NaN last; numpy's stable argsort does the same)."""
+    w = np.ascontiguousarray(rgb_w, dtype=F32).reshape(-1)
+    norms = np.sqrt(w * w).astype(F32)
+    order = np.argsort(norms, kind="stable")
+    keep = np.ones(w.shape[0], dtype=bool)
+    keep[order[:max(int(remove_count), 0)]] = False
+    return keep
+

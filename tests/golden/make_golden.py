@@ -4,7 +4,7 @@
 
 This script imports the reference Python from /root/reference (read-only) and
 is never run by the tests or on the GPU box; only its outputs (.npz data) are
-committed.  Three kinds of fixtures are produced:
+committed.  Four kinds of fixtures are produced:
 
 1. ``sum_*.npz`` / ``alpha_*.npz``: the reference's own autograd glue
    (gsplat/project_gaussians_2d.py:59-141, rasterize_sum.py:14-254,
@@ -21,6 +21,10 @@ committed.  Three kinds of fixtures are produced:
 3. ``train_iter_*.npz``: one and two ``GaussianVideo_frame.train_iter`` steps
    (GaussianSplats_Represent.py:191-207, L2 loss, Adan optimizer.py:39-362) of
    the reference model on CPU, oracle injected.
+4. ``prune_controls.npz``: ``removal_control`` / ``adaptive_control``
+   (GaussianSplats_Represent.py:98-172) of the reference model on CPU with a
+   stable torch.sort, on rgb_W with tie groups, NaN, +-0 and underflowing
+   squares (``python tests/golden/make_golden.py prune`` remakes only this).
 """
 from __future__ import annotations
 
@@ -331,7 +335,59 @@ def make_train_iter_case(name, H, W, n, seed, isremoval=False):
     print(f"{name}: losses={losses} psnrs={psnrs}")
 
 
+def make_prune_cases():
+    """removal_control / adaptive_control (GaussianSplats_Represent.py:98-172)
+    of the reference model on CPU, torch.sort made stable (the GPU's radix
+    sort; CPU torch.sort permutes ties).  rgb_W holds tie groups straddling the
+    cut (+-0.01: densified splats start at 0.01), a NaN, +-0 and values whose
+    square underflows.  Records the parameters before and after."""
+    sys.path.insert(0, REF)
+    import GaussianSplats_Represent as GR
+
+    class _StableTorch(types.ModuleType):
+        def __getattr__(self, name):
+            return getattr(torch, name)
+
+        @staticmethod
+        def sort(x, *a, **k):
+            k.setdefault("stable", True)
+            return torch.sort(x, *a, **k)
+
+    GR.torch = _StableTorch("torch_stable_sort")
+    rec = {}
+    cases = [("removal", 100, 4000, 4000), ("removal", 4000, 3800, 4000),
+             ("adaptive", 600, 4400, 4000), ("adaptive", 1000, 4100, 4000)]
+    for ci, (kind, it, n, mx) in enumerate(cases):
+        torch.manual_seed(100 + ci)
+        model = GR.GaussianVideo_frame(
+            loss_type="L2", opt_type="adan", num_points=n, max_num_points=mx,
+            densification_interval=100, iterations=10, H=32, W=32, BLOCK_H=16, BLOCK_W=16,
+            device=torch.device("cpu"), lr=1e-3, quantize=False, removal_rate=0.1,
+            isdensity=kind == "adaptive", isremoval=kind == "removal")
+        rng = np.random.default_rng(200 + ci)
+        w = rng.choice(np.array([-0.03, -0.01, 0.01, 0.02, 0.5, 1.0], np.float32), n)
+        w = w + (rng.random(n) < 0.5) * rng.normal(0, 0.2, n).astype(np.float32)
+        w[rng.choice(n, 6, replace=False)] = np.array([np.nan, 0.0, -0.0, 3e-25, 1e-25, 2e-20],
+                                                      np.float32)
+        with torch.no_grad():
+            model.rgb_W.data = torch.from_numpy(w.astype(np.float32)).reshape(n, 1)
+        for k, v in model.state_dict().items():
+            rec[f"c{ci}_in_{k}"] = _np(v).copy()
+        rec[f"c{ci}_in_rgb_W"] = _np(model.rgb_W).copy()
+        (model.removal_control if kind == "removal" else model.adaptive_control)(it)
+        rec[f"c{ci}_out_rgb_W"] = _np(model.rgb_W).copy()
+        for k, v in model.state_dict().items():
+            rec[f"c{ci}_out_{k}"] = _np(v).copy()
+        rec[f"c{ci}_meta"] = np.array([0 if kind == "removal" else 1, it, n, mx])
+        print(f"prune case {ci}: {kind} iter {it}: {n} -> {model._xyz.shape[0]}")
+    np.savez_compressed(os.path.join(OUT, "prune_controls.npz"), **rec)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "prune":
+        _import_reference()
+        make_prune_cases()
+        return
     gs = _import_reference()
     os.makedirs(OUT, exist_ok=True)
     make_ref_tests_case()
@@ -360,6 +416,7 @@ def main():
     opac = np.random.default_rng(11).uniform(0.2, 1.0, (40, 1)).astype(np.float32)
     make_alpha_case(gs, "alpha_32x48_n40", 32, 48, means, (L * 3).astype(np.float32), colors, opac, 11)
     make_train_iter_case("train_iter_64x64_n200", 64, 64, 200, 5)
+    make_prune_cases()
 
 
 if __name__ == "__main__":

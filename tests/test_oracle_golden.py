@@ -120,3 +120,25 @@ def test_oracle_backward_matches_finite_differences(oracle):
                                            r["conics"], c2, z["opacity"])
     fd = float(((out2 - r["out"]) * v_out).astype(np.float64).sum()) / 0.5
     assert abs(fd - v[2][g, 1]) < 1e-3 * max(1.0, abs(fd))
+
+
+def test_oracle_prune_matches_reference_controls(oracle):
+    """oracle.prune_keep vs the reference's removal_control / adaptive_control
+    (tests/golden/prune_controls.npz, make_golden.py prune): the kept rows of
+    every parameter, in order, for the count the reference removed.  At least
+    one case cuts through a group of equal norms, so the tie order is pinned."""
+    O = oracle
+    d = load_golden("prune_controls")
+    straddles = 0
+    for ci in range(4):
+        w = d[f"c{ci}_in_rgb_W"]
+        n = w.shape[0]
+        k = n - d[f"c{ci}_out_rgb_W"].shape[0]
+        keep = O.prune_keep(w, k)
+        for name in ("_xyz", "_cholesky", "_features_dc", "rgb_W"):
+            np.testing.assert_array_equal(d[f"c{ci}_in_{name}"][keep], d[f"c{ci}_out_{name}"])
+        norms = np.sqrt(w * w).reshape(-1)
+        cut = np.sort(norms, kind="stable")[k - 1] if k > 0 else None
+        if cut is not None and (norms == cut).sum() > 1 and (norms[~keep] == cut).sum() < (norms == cut).sum():
+            straddles += 1
+    assert straddles >= 1
