@@ -51,6 +51,27 @@ def test_argument_errors_are_reported_without_launch():
     assert b"16x16" in lib.gsvc_last_error()
 
 
+def test_prune_and_timing_argument_errors():
+    """gsvc_prune_lowest / gsvc_timing_enable check their arguments before any
+    HIP call; a prune that keeps nothing launches nothing."""
+    from gsvc_amd import _lib
+    lib = _lib.load()
+    assert lib.gsvc_prune_workspace_bytes(100000) >= 8 * 98
+    assert lib.gsvc_prune_lowest(10, -1, None, 0, None, None, None, None, 0, None) == 1
+    assert lib.gsvc_prune_lowest(10, 2, None, 9, None, None, None, None, 0, None) == 1
+    assert lib.gsvc_prune_lowest(10, 2, None, 0, None, None, None, None, 0, None) == 1
+    assert b"rgb_w" in lib.gsvc_last_error()
+    assert lib.gsvc_prune_lowest(10, 10, None, 0, None, None, None, None, 0, None) == 0
+    w = ctypes.c_void_p(16)  # never dereferenced: the workspace check fails first
+    assert lib.gsvc_prune_lowest(10, 2, w, 0, None, None, None, None, 0, None) == 2
+    assert lib.gsvc_timing_enable(4, 1, 2) == 1
+    assert b"how" in lib.gsvc_last_error()
+    assert lib.gsvc_timing_enable(0, 0, 0) == 0
+    from gsvc_amd.prune import prune_lowest
+    with pytest.raises(RuntimeError, match="CUDA"):
+        prune_lowest(torch.ones(4, 1), [torch.ones(4, 2)], 1)
+
+
 def test_single_hip_runtime_loaded():
     from gsvc_amd import _lib
     _lib.load()
