@@ -253,8 +253,11 @@ def main():
         for _ in range(args.steps):
             model()
         torch.cuda.synchronize()
-        barrier(world)
+        # each rank's clock stops at its own synchronize; the closing barrier
+        # still brackets the region, and the max over ranks (all_max below) is
+        # the job's time -- the barrier's own RCCL latency is not frame time
         elapsed = time.perf_counter() - t0
+        barrier(world)
         kt = ops.composite_times_ms(args.steps)
         ops.composite_timing(False)
     elapsed = all_max(elapsed, world, device)
