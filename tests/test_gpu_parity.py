@@ -349,3 +349,65 @@ def test_full_frame_backward_properties(cuda):
     lhs = float((out.double() * v.double()).sum())
     rhs = float((T(colors).double() * g1[2].double()).sum())
     assert abs(lhs - rhs) <= 1e-4 * max(1.0, abs(lhs))
+
+
+def _nonfinite_colours(colors, rng):
+    """inf, -inf and NaN in one channel of a few splats each."""
+    c = colors.copy()
+    n = len(c)
+    pick = rng.choice(n, 12, replace=False)
+    for j, s in enumerate(pick):
+        c[s, j % 3] = (np.inf, -np.inf, np.nan)[j % 3]
+    return c
+
+
+@pytest.mark.parametrize("name", ["sum_64x96_n300", "sum_trained_like_48x80_n200"])
+def test_raster_sum_forward_nonfinite_colours(cuda, oracle, name):
+    """The reference skips a pair whose sigma < 0 or alpha < 1/255 before it
+    touches the colour (forward.cu:600-605): an inf / NaN colour reaches only
+    the pixels where its splat is valid.  The kernel selects the updates, so
+    the non-finite footprint is the oracle's exactly (no c * 0 = NaN leaks)."""
+    from gsvc_amd import ops
+    z = load_golden(name)
+    H, W = int(z["H"]), int(z["W"])
+    tb = _tb(H, W)
+    colors = _nonfinite_colours(z["colors"], np.random.default_rng(5))
+    out, _, idx = ops.rasterize_sum_forward(
+        tb, (16, 16, 1), (W, H, 1), T(z["gaussian_ids_sorted"]), T(z["tile_bins"]),
+        T(z["xys"]), T(z["conics"]), T(colors), T(z["opacity"]), T(np.ones(3, np.float32)))
+    ref, _, ref_idx = oracle.raster_sum_forward(tb, H, W, z["gaussian_ids_sorted"], z["tile_bins"],
+                                                z["xys"], z["conics"], colors, z["opacity"])
+    g = N(out)
+    assert (~np.isfinite(ref)).any()  # the case is not vacuous
+    np.testing.assert_array_equal(np.isnan(g), np.isnan(ref))
+    np.testing.assert_array_equal(np.isposinf(g), np.isposinf(ref))
+    np.testing.assert_array_equal(np.isneginf(g), np.isneginf(ref))
+    fin = np.isfinite(ref)
+    np.testing.assert_allclose(g[fin], ref[fin], rtol=1e-6, atol=1e-5)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_render_frame_nonfinite_colours(cuda, oracle, mode):
+    """The same through the frame path (both composite variants: 1 sparse,
+    2 banded) with its fused clamp: torch.clamp keeps NaN, clamps +-inf."""
+    from gsvc_amd import _lib
+    from gsvc_amd.render import render_frame_sum
+    z = load_golden("sum_64x96_n300")
+    H, W = int(z["H"]), int(z["W"])
+    colors = _nonfinite_colours(z["colors"], np.random.default_rng(6))
+    # the fixture's means2d / L / colours as the frame inputs (no tanh, zero bound)
+    bound = torch.zeros(3, device="cuda")
+    lib = _lib.load()
+    prev = lib.gsvc_debug_set(0, mode)
+    try:
+        out = render_frame_sum(T(z["means2d"]), T(z["L"]), T(colors), H, W,
+                               torch.ones(3, device="cuda"), xyz_tanh=False, cholesky_bound=bound)
+    finally:
+        lib.gsvc_debug_set(0, prev)
+    r = oracle.render_sum(z["means2d"], z["L"], colors, np.ones((len(colors), 1), np.float32), H, W)
+    ref = np.clip(r["out"], 0, 1).transpose(2, 0, 1)[None]
+    g = N(out)
+    assert np.isnan(ref).any()
+    np.testing.assert_array_equal(np.isnan(g), np.isnan(ref))
+    fin = ~np.isnan(ref)
+    np.testing.assert_allclose(g[fin], ref[fin], rtol=1e-6, atol=1e-5)
