@@ -364,7 +364,7 @@ def _nonfinite_colours(colors, rng):
 @pytest.mark.parametrize("name", ["sum_64x96_n300", "sum_trained_like_48x80_n200"])
 def test_raster_sum_forward_nonfinite_colours(cuda, oracle, name):
     """The reference skips a pair whose sigma < 0 or alpha < 1/255 before it
-    touches the colour (forward.cu:600-605): an inf / NaN colour reaches only
+    touches the colour (forward.cu:600-609): an inf / NaN colour reaches only
     the pixels where its splat is valid.  The kernel selects the updates, so
     the non-finite footprint is the oracle's exactly (no c * 0 = NaN leaks)."""
     from gsvc_amd import ops
@@ -411,3 +411,29 @@ def test_render_frame_nonfinite_colours(cuda, oracle, mode):
     np.testing.assert_array_equal(np.isnan(g), np.isnan(ref))
     fin = ~np.isnan(ref)
     np.testing.assert_allclose(g[fin], ref[fin], rtol=1e-6, atol=1e-5)
+
+
+def test_raster_sum_backward_nonfinite_colours(cuda, oracle):
+    """Backward with inf / NaN colours: a splat's gradients turn non-finite
+    exactly where the oracle's do (valid pairs only, backward.cu:803-815);
+    the finite ones stay within the usual tolerance."""
+    from gsvc_amd import ops
+    z = load_golden("sum_64x96_n300")
+    H, W = int(z["H"]), int(z["W"])
+    tb = _tb(H, W)
+    colors = _nonfinite_colours(z["colors"], np.random.default_rng(7))
+    _, _, fidx = oracle.raster_sum_forward(tb, H, W, z["gaussian_ids_sorted"], z["tile_bins"],
+                                           z["xys"], z["conics"], colors, z["opacity"])
+    v_out = np.random.default_rng(12).standard_normal((H, W, 3)).astype(np.float32)
+    g = ops.rasterize_sum_backward(H, W, 16, 16, T(z["gaussian_ids_sorted"]), T(z["tile_bins"]),
+                                   T(z["xys"]), T(z["conics"]), T(colors), T(z["opacity"]),
+                                   T(np.ones(3, np.float32)), None, T(fidx), T(v_out), None)
+    ref = oracle.raster_sum_backward(tb, H, W, z["gaussian_ids_sorted"], z["tile_bins"], z["xys"],
+                                     z["conics"], colors, z["opacity"], fidx, v_out)
+    assert any((~np.isfinite(b)).any() for b in ref)
+    for a, b, nm in zip(g, ref, ("v_xy", "v_conic", "v_colors", "v_opacity")):
+        a = N(a)
+        np.testing.assert_array_equal(np.isnan(a), np.isnan(b), err_msg=nm)
+        np.testing.assert_array_equal(np.isinf(a), np.isinf(b), err_msg=nm)
+        fin = np.isfinite(b)
+        np.testing.assert_allclose(a[fin], b[fin], rtol=1e-4, atol=1e-4, err_msg=nm)
