@@ -68,7 +68,7 @@ def _close(a, ref, name):
 
 
 CASES = [(64, 64, 200, 1.0), (72, 120, 500, 1.0), (1080, 1920, 10000, 1.0),
-         (1080, 1920, 50000, 1.0), (256, 256, 3000, 8.0)]
+         (1080, 1920, 50000, 1.0), (256, 256, 3000, 8.0), (37, 53, 150, 1.0), (17, 33, 60, 2.0)]
 
 
 @pytest.mark.parametrize("H,W,n,chol", CASES)
