@@ -86,6 +86,7 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 // reference's per-pixel op sequence (common.h splat_sigma_h, exp_neg) on both
 // lanes of a v2f.  A pair that fails sigma >= 0 and alpha >= 1/255 keeps its
 // accumulators bit for bit (the update is selected, not added as zero).
+template <bool kIdx>
 __device__ __forceinline__ void blend_pair(float gx, float ha, float b, float bdy, float cq,
                                            float opac, float cr, float cg, float cb, v2f px,
                                            int k, v2f &ar, v2f &ag, v2f &ab, int &l0, int &l1) {
@@ -104,8 +105,10 @@ __device__ __forceinline__ void blend_pair(float gx, float ha, float b, float bd
     ar = (v2f){v0 ? nr.x : ar.x, v1 ? nr.y : ar.y};
     ag = (v2f){v0 ? ng.x : ag.x, v1 ? ng.y : ag.y};
     ab = (v2f){v0 ? nb.x : ab.x, v1 ? nb.y : ab.y};
-    l0 = v0 ? k : l0;
-    l1 = v1 ? k : l1;
+    if (kIdx) {  // final_idx is written (the autograd forward)
+        l0 = v0 ? k : l0;
+        l1 = v1 ? k : l1;
+    }
     (void)b;
 }
 
@@ -323,7 +326,7 @@ __device__ int wave_brute_tile_ids(const SumFwdArgs &A, int tile, int *s_ids) {
 }
 
 // Sparse path: one wave blends the whole 16x16 tile, 4 pixels per lane.
-template <int kMode>
+template <int kMode, bool kIdx>
 __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, int2 range, int n,
                                                float4 *s_slice, float3 init, bool ids_in_lds,
                                                const int *s_ids, const float4 *seg_rec,
@@ -378,8 +381,8 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
             const float cq = (C.x * dy) * dy;
             const float bdy = G.w * dy;
             const int k = k0 + t;
-            blend_pair(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, px01, k, ar01, ag01, ab01, l0, l1);
-            blend_pair(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, px23, k, ar23, ag23, ab23, l2, l3);
+            blend_pair<kIdx>(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, px01, k, ar01, ag01, ab01, l0, l1);
+            blend_pair<kIdx>(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, px23, k, ar23, ag23, ab23, l2, l3);
         }
         wave_lds_sync();
     }
@@ -439,7 +442,7 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
 }
 
 // Dense path: this wave blends one 8-row band, 2 pixels per lane.
-template <int kMode>
+template <int kMode, bool kIdx>
 __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int band, int2 range,
                                              int n, float4 *s_slice, float3 init, bool ids_in_lds,
                                              const int *s_ids, const float4 *seg_rec,
@@ -513,11 +516,11 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
             const float4 G = s_geo[t];
             const float4 C = s_col[t];
             const float bl = s_blu[t];
-            const int k = s_k[t];
+            const int k = kIdx ? s_k[t] : 0;
             const float dy = G.y - py;
             const float cq = (C.x * dy) * dy;
             const float bdy = G.w * dy;
-            blend_pair(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, pxv, k, ar, ag, ab, l0, l1);
+            blend_pair<kIdx>(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, pxv, k, ar, ag, ab, l0, l1);
         }
         wave_lds_sync();
     }
@@ -575,7 +578,9 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
 
 // kModeSparse launches 64-thread workgroups (one wave per tile); every other
 // mode 128-thread workgroups (two waves per tile).
-template <int kMode>
+// kIdx: final_idx is written (the autograd forward); the render paths launch
+// the kIdx = false instance, which tracks no indices.
+template <int kMode, bool kIdx>
 __global__ __launch_bounds__(kMode == kModeSparse || kMode == kModeSparseStamp ? 64 : 128, 8) void
 raster_sum_fwd_kernel(SumFwdArgs A) {
     constexpr bool kOneWave = kMode == kModeSparse || kMode == kModeSparseStamp;
@@ -654,7 +659,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
             n = (A.slab && n_all > kTilePix)
                     ? wave_brute_tile_ids(A, tile, s_ids[0])
                     : wave_sorted_tile_ids(seg, n_all, s_ids[0], reinterpret_cast<unsigned *>(s_buf[0]));
-        sum_fwd_sparse<kMode>(A, tile, range, n, s_buf[0], init, by_ids, s_ids[0], seg_rec, spec0,
+        sum_fwd_sparse<kMode, kIdx>(A, tile, range, n, s_buf[0], init, by_ids, s_ids[0], seg_rec, spec0,
                               spec1, spec2);
     } else {
         if (ty * kTile + w * 8 >= A.img_h) return;  // band below the image
@@ -662,7 +667,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
             n = (A.slab && n_all > kTilePix)
                     ? wave_brute_tile_ids(A, tile, s_ids[w])
                     : wave_sorted_tile_ids(seg, n_all, s_ids[w], reinterpret_cast<unsigned *>(s_buf[w]));
-        sum_fwd_band<kMode>(A, tile, w, range, n, s_buf[w], init, by_ids, s_ids[w], seg_rec, spec0,
+        sum_fwd_band<kMode, kIdx>(A, tile, w, range, n, s_buf[w], init, by_ids, s_ids[w], seg_rec, spec0,
                             spec1, spec2);
     }
     if (kMode == kModeStamp && (threadIdx.x & 63) == 0) {
@@ -850,30 +855,37 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
     const dim3 grid(ntiles * A.frames);
     switch (mode) {
         case kModeSparse:
-            launch_fwd(raster_sum_fwd_kernel<kModeSparse>, grid, dim3(64), s, tev, A);
+            launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeSparse, true> : raster_sum_fwd_kernel<kModeSparse, false>, grid,
+                       dim3(64), s, tev, A);
             break;
         case kModeBanded:
-            launch_fwd(raster_sum_fwd_kernel<kModeBanded>, grid, dim3(128), s, tev, A);
+            launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeBanded, true> : raster_sum_fwd_kernel<kModeBanded, false>, grid,
+                       dim3(128), s, tev, A);
             break;
         case kModeStamp:
             A.stamps = reinterpret_cast<long long *>(A.final_Ts);
             A.final_Ts = nullptr;
-            launch_fwd(raster_sum_fwd_kernel<kModeStamp>, grid, dim3(128), s, tev, A);
+            launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeStamp, true> : raster_sum_fwd_kernel<kModeStamp, false>, grid,
+                       dim3(128), s, tev, A);
             break;
         case kModeNoBlend:
-            launch_fwd(raster_sum_fwd_kernel<kModeNoBlend>, grid, dim3(128), s, tev, A);
+            launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeNoBlend, true> : raster_sum_fwd_kernel<kModeNoBlend, false>, grid,
+                       dim3(128), s, tev, A);
             break;
         case kModeNoStore:
-            launch_fwd(raster_sum_fwd_kernel<kModeNoStore>, grid, dim3(128), s, tev, A);
+            launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeNoStore, true> : raster_sum_fwd_kernel<kModeNoStore, false>, grid,
+                       dim3(128), s, tev, A);
             break;
         case kModeAdaptive:
-            launch_fwd(raster_sum_fwd_kernel<kModeAdaptive>, grid, dim3(128), s, tev, A);
+            launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeAdaptive, true> : raster_sum_fwd_kernel<kModeAdaptive, false>, grid,
+                       dim3(128), s, tev, A);
             break;
         case kModeSparseStamp:
             if (!g_debug_ptr)
                 return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: mode 7 needs gsvc_debug_set_ptr");
             A.stamps = reinterpret_cast<long long *>(g_debug_ptr);
-            launch_fwd(raster_sum_fwd_kernel<kModeSparseStamp>, grid, dim3(64), s, tev, A);
+            launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeSparseStamp, true> : raster_sum_fwd_kernel<kModeSparseStamp, false>, grid,
+                       dim3(64), s, tev, A);
             break;
         default:
             return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: unknown kernel mode %d", mode);
