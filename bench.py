@@ -3,29 +3,44 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Workload (BASELINE.json configs[1]): render one 1920x1080 frame of 10,000
-splats, i.e. ``GaussianVideoFrame.forward()`` (the restatement of GSVC's
-GaussianSplats_Represent.py:83-90: project -> bin/sort -> sum-rasterize ->
-clamp -> NCHW), the loop train_video_Represent.py:103-106 times for its FPS.
-A step is one frame.  Each rank renders its own synthetic frame (random-init
-splats, seeded per rank): frames shard across GPUs with no data-path
-collective (weak scaling); ranks only all-reduce their timings.
+Headline workload (BASELINE.json configs[2], the configuration BASELINE.md §2
+and ``north_star`` set the bar on): one ``GaussianVideoFrame.train_iter`` of a
+1920x1080 frame with 50,000 splats -- the restatement of GSVC's
+GaussianSplats_Represent.py:191-207 (forward = project -> bin -> sum-raster ->
+clamp -> NCHW, L2 loss, backward, PSNR ``.item()``, Adan step, zero_grad,
+StepLR), the loop train_video_Represent.py:85-96 runs per frame.  A step is one
+training iteration; ``value`` is training iterations per second over all
+ranks.  Each rank trains its own synthetic frame (random-init splats with the
+reference's init distributions, seeded per rank; a seeded procedural target):
+frames shard across GPUs with no data-path collective (weak scaling); ranks
+only all-reduce their timings.
+
+``python bench.py --gpus N`` with no torch.distributed environment starts N
+rank processes itself (``torch.distributed.run`` as a child process; this
+process never touches the GPU) and exits with their status.
 
 Reported beside the primary value:
-  roofline      composite kernel (rasterize_sum_forward): algorithmic bytes per
-                launch (36 N_vis + 4 M_eff + 8 T + 12 P) over its
-                average duration from HIP events on its stream, vs 8 TB/s;
-                ``traffic`` = PMC HBM bytes per launch from profiles/ (rocprofv3).
-  cpu_baseline  the CPU oracle (oracle/oracle.c, single thread) rendering the
-                same frame, timed on a bounded sample on this host.
-  secondary     BASELINE configs[2]: 1080p / 50k splats full train_iter
-                (L2 + backward + Adan) iterations/s and 50k render fps (N=1).
+  roofline      the dominant kernel of the step (train_tile_kernel): algorithmic
+                bytes per launch (12 P + 4 T + 48 M_eff + 32 M_eff +
+                12 T) over its average duration from HIP events carried by its
+                own dispatches (on its stream), vs 8 TB/s; ``traffic`` = PMC HBM
+                bytes per launch from the committed rocprofv3 passes (profiles/).
+  kernels       every kernel of the step, event-timed the same way.
+  render        configs[2]'s render: GaussianVideoFrame.forward at 50k splats,
+                frames/s and the composite kernel's roofline.
+  psnr_vs_ref   the fused trajectory against the reference's own train_iter run
+                on CPU (tests/golden/train_traj_1080p_n50k.npz, make_golden.py).
+  cpu_baseline  the CPU restatement (oracle/oracle.py train_iter_sum, C kernels,
+                1 thread) on a bounded sample of the same iteration.
+  render_10k    configs[1] (render only, 10k splats) and ``video_decode``.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -37,7 +52,7 @@ import torch  # noqa: E402
 METRIC = "1920×1080 frames/sec (render + train-iter) @ N splats; PSNR vs ref"
 H, W = 1080, 1920
 HBM_PEAK_GBS = 8000.0
-PUBLISHED_FPS = 1500.0  # BASELINE.md §1 (README.md:19; splat count unstated)
+TRAJ_FIXTURE = os.path.join(REPO, "tests", "golden", "train_traj_1080p_n50k.npz")
 
 
 def parse():
@@ -45,24 +60,55 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--splats", type=int, default=10000)
+    ap.add_argument("--splats", type=int, default=50000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--timing-launches", type=int, default=200,
+                    help="launches per kernel timed by HIP events after the timed region")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--timing", choices=["dispatch", "marker"], default="dispatch",
-                    help="composite-kernel HIP events: carried by the timed dispatch "
-                         "(hipExtLaunchKernel) or recorded around it")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: start the ranks, all-reduce, print the line (tests)")
     return ap.parse_args()
 
 
-def dist_setup():
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args) -> int:
+    """--gpus N without a torch.distributed environment: run N ranks of this
+    script under torch.distributed.run in a child process (one process per
+    GPU).  This process does not initialise the GPU and does not exec."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dry_run or args.backend != "nccl":
+            dist.init_process_group(args.backend)
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # every rank present: one all-reduce of ones
+        dev = torch.device("cpu") if args.dry_run or args.backend != "nccl" else torch.device("cuda", local)
+        t = torch.ones(1, device=dev)
+        dist.all_reduce(t)
+        if int(t.item()) != world:
+            raise SystemExit(f"bench.py: all-reduce saw {int(t.item())} ranks, expected {world}")
     return world, rank, local
 
 
@@ -81,11 +127,9 @@ def all_max(x, world, device):
     return float(t.item())
 
 
-def composite_bytes_of(means2d, L, tile_bounds):
-    """SURVEY §8d B_fwd = 36 N_vis + 4 M_eff + 8 T + 12 P for the render
-    (inference) forward of one frame: the [3,H,W] clamped image is written
-    once and no final_idx (the 16 P of the autograd forward counts its 4 B/px
-    final_idx)."""
+def frame_shape(means2d, L, tile_bounds):
+    """N_vis, M and M_eff = sum over tiles of min(count, 256) of one frame (the
+    op path's binning of the same splats), for the algorithmic byte counts."""
     from gsvc_amd import ops
     from gsvc_amd.utils import bin_and_sort_for_raster
     n = means2d.shape[0]
@@ -98,68 +142,175 @@ def composite_bytes_of(means2d, L, tile_bounds):
         else:
             m_eff = int((bins[:, 1] - bins[:, 0]).clamp(min=0, max=256).sum())
         n_vis = int((nth > 0).sum())
-    T = tile_bounds[0] * tile_bounds[1]
-    P = H * W
-    return 36 * n_vis + 4 * m_eff + 8 * T + 12 * P, dict(N_vis=n_vis, M=m, M_eff=m_eff, T=T, P=P)
+    return dict(N_vis=n_vis, M=int(m), M_eff=m_eff, T=tile_bounds[0] * tile_bounds[1], P=H * W)
 
 
-def composite_bytes(model):
-    return composite_bytes_of(model.get_xyz.detach(), model.get_cholesky_elements.detach(),
-                              model.tile_bounds)
+def composite_bytes(shape):
+    """SURVEY §8d B_fwd for the render (inference) forward: 36 N_vis + 4 M_eff +
+    8 T + 12 P (the [3,H,W] clamped image written once, no final_idx)."""
+    return 36 * shape["N_vis"] + 4 * shape["M_eff"] + 8 * shape["T"] + 12 * shape["P"]
 
 
-def load_profile(n_splats):
-    """(PMC HBM bytes per launch, rocprofv3 kernel-trace average duration in
-    us) of the composite kernel from profiles/pmc_traffic.json (written by
-    tools/gpu_bench_prof.sh from rocprofv3 runs of this same command)."""
+def train_tile_bytes(shape):
+    """Algorithmic HBM bytes of one train_tile_kernel launch:
+    gt 12 P + tile counts 4 T + the tiles' splat records 48 M_eff (read);
+    gradient sums 32 M_eff (8 floats per (splat, tile), atomics) + per-tile
+    error sums 8 T + the next frame's count reset 4 T (written)."""
+    return 12 * shape["P"] + 4 * shape["T"] + 48 * shape["M_eff"] + 32 * shape["M_eff"] + 12 * shape["T"]
+
+
+def project_bytes(shape, n):
+    """frame_project_kernel in the training step: parameters 36 N (xyz, chol,
+    features, rgb_W) read; record 48 N + xys/radii 12 N + zeroed gradient
+    record 64 N + the tiles' records 48 M + slot counters 4 M (write)."""
+    return 36 * n + 48 * n + 12 * n + 64 * n + 52 * shape["M"]
+
+
+def train_splat_bytes(n):
+    """train_splat_kernel: gradient record 64 N + record 32 N + radii 4 N +
+    parameters and Adan state (8 elements x (4 + 16 B)) read, parameters and
+    state (8 x 20 B) written per splat; the 8 T loss sum is not counted."""
+    return n * (64 + 32 + 4 + 8 * 20 + 8 * 20)
+
+
+def load_profile(key):
+    """PMC HBM bytes and kernel-trace durations per launch from
+    profiles/pmc_traffic.json (tools/prof_summary.py over the committed
+    rocprofv3 runs of this command)."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            rec = json.load(f).get(str(n_splats), {})
-        return (rec.get("rasterize_sum_forward_bytes_per_launch"),
-                rec.get("rasterize_sum_forward_trace_avg_us"))
+            return json.load(f).get(key, {})
     except (OSError, ValueError):
-        return None, None
+        return {}
+
+
+def _avg(xs):
+    return sum(xs) / len(xs) if xs else float("nan")
+
+
+def roofline(kernel, nbytes, times_ms, prof=None, prof_key=None, timing=None):
+    avg_ms = _avg(times_ms)
+    achieved = nbytes / (avg_ms * 1e-3) / 1e9
+    r = {"kernel": kernel, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+         "traffic": None, "avg_kernel_us": round(avg_ms * 1e3, 2),
+         "timed_launches": len(times_ms),
+         "algorithmic_bytes_per_launch": nbytes,
+         "timing": timing or "HIP events carried by the kernel's own dispatches (hipExtLaunchKernel)"}
+    if prof and prof_key:
+        r["traffic"] = prof.get(f"{prof_key}_bytes_per_launch")
+        tus = prof.get(f"{prof_key}_trace_avg_us")
+        if tus:
+            r["trace_avg_kernel_us"] = round(tus, 2)
+            r["frac_by_trace"] = round(nbytes / (tus * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+    return r
 
 
 def cpu_baseline(n_splats, seconds):
-    """The CPU oracle rendering the workload's frame on this host: 1 thread
-    (``value``) and every core this process may use (``all_cores``; the
-    per-tile loop of the sum rasterizer in OpenMP, the binning serial)."""
+    """The CPU restatement of the same training iteration (oracle/oracle.py
+    train_iter_sum: project + bin + sum-raster + clamp + L2 + raster and
+    projection VJPs + Adan; C kernels, numpy glue), 1 thread, timed on a
+    bounded number of iterations of the headline frame on this host."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
-    means, L, colors, opac = O.synthetic_frame(n_splats, seed=0)
-
-    def rate(threads, budget):
-        O.set_threads(threads)
-        O.render_sum(means, L, colors, opac, H, W)  # warm-up / lib build
-        t0 = time.perf_counter()
-        frames = 0
-        while True:
-            O.render_sum(means, L, colors, opac, H, W)
-            frames += 1
-            el = time.perf_counter() - t0
-            if el >= budget:
-                return frames, el
-
-    # the box's CPU share: OMP_NUM_THREADS (16 per GPU there), at most the affinity set
-    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
-    f1, e1 = rate(1, seconds)
-    fn, en = rate(cores, max(2.0, seconds / 3))
+    from gsvc_amd.frame import synthetic_gt
     O.set_threads(1)
-    return {"value": f1 / e1, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{f1} renders of one 1920x1080 / {n_splats}-splat frame "
-                      f"(project+bin+sort+sum-raster) by oracle/oracle.c, 1 thread, {e1:.1f} s",
-            "all_cores": {"value": fn / en, "cores": cores,
-                          "sample": f"{fn} renders, OpenMP per-tile rasterizer, {en:.1f} s"}}
+    g = torch.Generator().manual_seed(1000)
+    params = dict(_xyz=torch.atanh(2 * (torch.rand(n_splats, 2, generator=g) - 0.5)).numpy(),
+                  _cholesky=torch.rand(n_splats, 3, generator=g).numpy(),
+                  _features_dc=torch.rand(n_splats, 3, generator=g).numpy())
+    gt = synthetic_gt(H, W, 8, "cpu").numpy()[0]
+    state = {}
+    O.train_iter_sum(params, gt, H, W, state, 1)  # warm-up (library load, first step)
+    t0 = time.perf_counter()
+    it = 0
+    while True:
+        it += 1
+        O.train_iter_sum(params, gt, H, W, state, 1 + it)
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": it / el, "unit": "train-iters/s", "cores": 1, "kind": "port",
+            "sample": f"{it} train iterations of one 1920x1080 / {n_splats}-splat frame "
+                      "(oracle/oracle.py train_iter_sum: C project/bin/raster + VJPs, numpy "
+                      f"clamp/L2/Adan), 1 thread, {el:.1f} s"}
+
+
+def psnr_vs_ref(device):
+    """Run the reference trajectory's iterations (same seed, init, target) on
+    the fused path and compare per-iteration PSNR with the reference's CPU run."""
+    import numpy as np
+    from gsvc_amd.frame import make_frame_model, synthetic_gt
+    z = np.load(TRAJ_FIXTURE)
+    n, iters = int(z["n"]), int(z["iters"])
+    model = make_frame_model(int(z["H"]), int(z["W"]), n, device, seed=int(z["seed"]))
+    gt = synthetic_gt(int(z["H"]), int(z["W"]), int(z["gt_seed"]), "cpu").to(device)
+    ps = []
+    for it in range(1, iters + 1):
+        _, p = model.train_iter(gt, it)
+        ps.append(p)
+    ref = [float(x) for x in z["psnrs"]]
+    d = [abs(a - b) for a, b in zip(ps, ref)]
+    return {"iters": iters, "psnr": round(ps[-1], 6), "psnr_ref": round(ref[-1], 6),
+            "max_abs_diff_db": float(f"{max(d):.3g}"),
+            "fused_steps": model.fused_steps,
+            "ref": "GaussianVideo_frame.train_iter (reference Python, oracle kernels, CPU), "
+                   "tests/golden/train_traj_1080p_n50k.npz"}
+
+
+def time_channels(channels, fn, launches):
+    """HIP-event durations (ms) of every launch of ``channels`` while calling
+    ``fn`` ``launches`` times (outside the timed region)."""
+    from gsvc_amd import ops
+    for c in channels:
+        ops.channel_timing(c, True, max_launches=launches, every=1, dispatch=True)
+    for _ in range(launches):
+        fn()
+    torch.cuda.synchronize()
+    out = {c: ops.channel_times_ms(c, launches) for c in channels}
+    for c in channels:
+        ops.channel_timing(c, False)
+    return out
+
+
+def render_block(model, steps, warmup):
+    """configs[2]'s render: GaussianVideoFrame.forward() of the trained model."""
+    from gsvc_amd import ops
+    with torch.no_grad():
+        for _ in range(warmup):
+            model()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            model()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        times = time_channels(["composite", "project"], model, 200)
+    shape = frame_shape(model.get_xyz.detach(), model.get_cholesky_elements.detach(),
+                        model.tile_bounds)
+    prof = load_profile(f"render_{model._xyz.shape[0]}")
+    return {"workload": f"GaussianVideoFrame.forward, 1920x1080, {model._xyz.shape[0]} splats "
+                        "(configs[2] render): project + bin + sum-raster + clamp + NCHW",
+            "frames_per_s": round(steps / el, 1), "ms_per_frame": round(1e3 * el / steps, 4),
+            "roofline": roofline("raster_sum_fwd_kernel (composite)", composite_bytes(shape),
+                                 times["composite"], prof, "rasterize_sum_forward"),
+            "project_avg_us": round(_avg(times["project"]) * 1e3, 2), "shape": shape}
+
+
+def render_10k(device, steps=200, warmup=20):
+    """configs[1]: render one 1920x1080 frame of 10k splats."""
+    from gsvc_amd.frame import make_frame_model
+    model = make_frame_model(H, W, 10000, device, seed=1000)
+    model.eval()
+    r = render_block(model, steps, warmup)
+    r["workload"] = r["workload"].replace("(configs[2] render)", "(configs[1])")
+    return r
 
 
 def video_decode(device, frames=8, splats=10000, steps=50, warmup=5):
-    """A GOP of ``frames`` distinct 1920x1080 frame models (10k splats each,
-    the reference init distributions) rendered by ONE gsvc_render_frames_sum
-    call per step -- a video decoder's workload; the composite kernel then
-    spans frames x tiles.  Reported beside (not instead of) the single-frame
-    headline."""
+    """A GOP of ``frames`` distinct 1920x1080 frame models (10k splats each)
+    rendered by ONE gsvc_render_frames_sum call per step (a decoder's workload)."""
     from gsvc_amd import ops
     from gsvc_amd.render import render_frames_sum
     g = torch.Generator().manual_seed(4242)
@@ -172,7 +323,7 @@ def video_decode(device, frames=8, splats=10000, steps=50, warmup=5):
     for _ in range(warmup):
         render_frames_sum(xyz, chol, feat, sizes, H, W, bg, cholesky_bound=bound)
     torch.cuda.synchronize()
-    ops.composite_timing(True, max_launches=steps, every=4)
+    ops.composite_timing(True, max_launches=steps, every=1, dispatch=True)
     t0 = time.perf_counter()
     for _ in range(steps):
         render_frames_sum(xyz, chol, feat, sizes, H, W, bg, cholesky_bound=bound)
@@ -184,125 +335,117 @@ def video_decode(device, frames=8, splats=10000, steps=50, warmup=5):
     nbytes = 0
     for b in range(frames):
         sl = slice(b * splats, (b + 1) * splats)
-        nb, _ = composite_bytes_of(torch.tanh(xyz[sl]), chol[sl] + bound, tb)
-        nbytes += nb
-    avg_ms = sum(kt) / len(kt)
-    ach = nbytes / (avg_ms * 1e-3) / 1e9
+        nbytes += composite_bytes(frame_shape(torch.tanh(xyz[sl]), chol[sl] + bound, tb))
     return {"workload": f"GOP of {frames} distinct 1920x1080 frame models x {splats} splats, one "
                         "gsvc_render_frames_sum call per step",
-            "frames_per_s": frames * steps / el, "ms_per_call": 1e3 * el / steps,
-            "roofline": {"kernel": "rasterize_sum_forward (frames x tiles)", "bound": "hbm",
-                         "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "avg_kernel_us": round(avg_ms * 1e3, 2),
-                         "algorithmic_bytes_per_launch": nbytes}}
+            "frames_per_s": round(frames * steps / el, 1), "ms_per_call": round(1e3 * el / steps, 4),
+            "roofline": roofline("raster_sum_fwd_kernel (frames x tiles)", nbytes, kt)}
 
 
-def secondary(device, steps=50, warmup=10):
-    """configs[2]: 1080p / 50k splats train_iter and render (N=1 only)."""
-    from gsvc_amd.frame import make_frame_model, synthetic_gt
-    model = make_frame_model(H, W, 50000, device, seed=7)
-    gt = synthetic_gt(H, W, 8, device)
-    for it in range(1, warmup + 1):
-        model.train_iter(gt, it)
-    torch.cuda.synchronize()
+def dry_run(args, world, rank):
+    """--dry-run: the rank plumbing without a GPU (tests/test_bench_launch.py)."""
     t0 = time.perf_counter()
-    psnr = 0.0
-    for it in range(warmup + 1, warmup + steps + 1):
-        _, psnr = model.train_iter(gt, it)
-    torch.cuda.synchronize()
-    t_train = (time.perf_counter() - t0) / steps
-    with torch.no_grad():
-        for _ in range(warmup):
-            model()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            model()
-        torch.cuda.synchronize()
-        t_render = (time.perf_counter() - t0) / steps
-    return {"workload": "1920x1080, 50000 splats (BASELINE configs[2])",
-            "train_iters_per_s": 1.0 / t_train, "train_ms_per_iter": 1e3 * t_train,
-            "render_fps": 1.0 / t_render, "psnr_after_iters": psnr,
-            "train_iter": "forward + L2 + backward + PSNR .item() + Adan + zero_grad + StepLR",
-            "train_iter_path": ("fused: gsvc_train_step_sum (projection+slabs, per-tile "
-                                "forward/loss/backward, per-splat VJP+Adan)"
-                                if model.fused_steps else "op by op")}
+    x = torch.ones(1000)
+    for _ in range(args.steps):
+        x = x * 1.0001
+    elapsed = all_max(time.perf_counter() - t0, world, torch.device("cpu"))
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(world * args.steps / elapsed, 2),
+                          "unit": "train-iters/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "dry_run": True, "ranks_seen": world}), flush=True)
 
 
 def main():
     args = parse()
-    world, rank, local = dist_setup()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
+    world, rank, local = dist_setup(args)
+    if args.dry_run:
+        dry_run(args, world, rank)
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
-    from gsvc_amd import ops
-    from gsvc_amd.frame import make_frame_model
+    from gsvc_amd.frame import make_frame_model, synthetic_gt
 
+    # ---- headline: configs[2] training iterations, one frame per rank
     model = make_frame_model(H, W, args.splats, device, seed=1000 + rank)
-    model.eval()
-    with torch.no_grad():
-        for _ in range(args.warmup):
-            model()
-        torch.cuda.synchronize()
-        # HIP events around every 16th composite launch of the timed region,
-        # recorded by the library on the kernel's own stream
-        ops.composite_timing(True, max_launches=args.steps, every=16,
-                             dispatch=args.timing == "dispatch")
-        barrier(world)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            model()
-        torch.cuda.synchronize()
-        # each rank's clock stops at its own synchronize; the closing barrier
-        # still brackets the region, and the max over ranks (all_max below) is
-        # the job's time -- the barrier's own RCCL latency is not frame time
-        elapsed = time.perf_counter() - t0
-        barrier(world)
-        kt = ops.composite_times_ms(args.steps)
-        ops.composite_timing(False)
+    gt = synthetic_gt(H, W, 8 + rank, "cpu").to(device)
+    it = 0
+    psnr = float("nan")
+    for _ in range(args.warmup):
+        it += 1
+        model.train_iter(gt, it)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        it += 1
+        _, psnr = model.train_iter(gt, it)
+    torch.cuda.synchronize()
+    # each rank's clock stops at its own synchronize; the closing barrier still
+    # brackets the region and the max over ranks (all_max) is the job's time
+    elapsed = time.perf_counter() - t0
+    barrier(world)
     elapsed = all_max(elapsed, world, device)
     value = world * args.steps / elapsed
 
+    # ---- per-kernel HIP-event timing of the step, outside the timed region
+    state = {"it": it}
+
+    def one_iter():
+        state["it"] += 1
+        model.train_iter(gt, state["it"])
+
+    kt = time_channels(["train_tile", "project", "train_splat"], one_iter, args.timing_launches)
+    shape = frame_shape(model.get_xyz.detach(), model.get_cholesky_elements.detach(),
+                        model.tile_bounds)
     if rank != 0:
         if world > 1:
             import torch.distributed as dist
             dist.destroy_process_group()
         return
 
-    nbytes, shape = composite_bytes(model)
-    avg_ms = sum(kt) / len(kt)
-    achieved = nbytes / (avg_ms * 1e-3) / 1e9
-    traffic, trace_us = load_profile(args.splats)
-    roof = {"kernel": "rasterize_sum_forward", "bound": "hbm", "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic, "avg_kernel_us": round(avg_ms * 1e3, 2),
-            "algorithmic_bytes_per_launch": nbytes, "shape": shape,
-            "timing": ("HIP events carried by every 16th composite dispatch (hipExtLaunchKernel)"
-                       if args.timing == "dispatch" else
-                       "HIP events recorded around every 16th composite launch")}
-    if trace_us:
-        # the same kernel's duration in the committed rocprofv3 kernel trace
-        # (marker events around the launch add ~3 us of packet / dispatch latency)
-        roof["trace_avg_kernel_us"] = round(trace_us, 2)
-        roof["frac_by_trace"] = round(nbytes / (trace_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+    prof = load_profile(f"train_{args.splats}")
+    roof = roofline("train_tile_kernel", train_tile_bytes(shape), kt["train_tile"], prof,
+                    "train_tile")
+    kernels = {
+        "train_tile": roof,
+        "frame_project": roofline("frame_project_kernel", project_bytes(shape, args.splats),
+                                  kt["project"], prof, "frame_project"),
+        "train_splat": roofline("train_splat_kernel", train_splat_bytes(args.splats),
+                                kt["train_splat"], prof, "train_splat"),
+    }
     line = {
-        "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+        "metric": METRIC, "value": round(value, 2), "unit": "train-iters/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": round(value / PUBLISHED_FPS, 3), "dtype": "f32",
-        "data": "synthetic (random-init splats, reference init distributions)",
-        "config": {"workload": f"render 1920x1080, {args.splats} splats (BASELINE configs[1]): "
-                               "GaussianVideoFrame.forward = project + bin/sort + sum-raster + "
-                               "clamp + NCHW", "H": H, "W": W, "splats": args.splats,
-                   "parallelism": f"frames sharded over {world} rank(s), no data-path collective"},
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (random-init splats with the reference init distributions, seeded "
+                "procedural 1920x1080 target)",
+        "config": {"workload": f"BASELINE configs[2]: train_iter of one 1920x1080 frame, "
+                               f"{args.splats} splats (GaussianVideoFrame.train_iter = forward + "
+                               "L2 + backward + PSNR .item() + Adan + zero_grad + StepLR)",
+                   "H": H, "W": W, "splats": args.splats,
+                   "parallelism": f"one frame per rank, {world} rank(s), no data-path collective"},
         "roofline": roof,
+        "kernels": kernels,
+        "shape": shape,
+        "psnr_after_iters": round(psnr, 6),
+        "train_iter_path": ("fused: gsvc_train_step_sum" if model.fused_steps else "op by op"),
         "cpu_baseline": None,
     }
+    if world == 1 and not args.no_secondary:
+        line["psnr_vs_ref"] = psnr_vs_ref(device)
+        model.eval()
+        line["render"] = render_block(model, 200, 20)
+        line["render"]["vs_published_1500fps"] = round(line["render"]["frames_per_s"] / 1500.0, 2)
+        line["render_10k"] = render_10k(device)
+        line["video_decode"] = video_decode(device)
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args.splats, args.cpu_seconds)
-    if world == 1 and not args.no_secondary:
-        line["secondary"] = secondary(device)
-        line["video_decode"] = video_decode(device)
     print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

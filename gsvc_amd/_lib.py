@@ -32,6 +32,8 @@ _SIGS = {
     "gsvc_debug_set_ptr": [_P],
     "gsvc_timing_enable": [_I, _I, _I],
     "gsvc_timing_collect": [_P, _I, _P],
+    "gsvc_timing_enable_channel": [_I, _I, _I, _I],
+    "gsvc_timing_collect_channel": [_I, _P, _I, _P],
     "gsvc_prune_workspace_bytes": [_I],
     "gsvc_prune_lowest": [_I, _I, _P, _I, _P, _P, _P, _P, _SZ, _P],
     "gsvc_project_gaussians_2d_forward": [_I, _P, _P, _U, _U, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P],

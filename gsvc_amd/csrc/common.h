@@ -6,6 +6,7 @@
 // oracle (oracle/oracle.c) follows the same op sequence.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -25,8 +26,21 @@ extern int g_knobs[8];  // gsvc_debug_set(); knob 0 = sum-forward variant
 extern void *g_debug_ptr;  // gsvc_debug_set_ptr(): diagnostic output buffer
 // timing.hip: slot, or -1 when not recording; dispatch_ev[2] = the events the
 // launch must carry itself (hipExtLaunchKernel), both null otherwise
-int timing_begin(hipStream_t s, hipEvent_t *dispatch_ev);
-void timing_end(hipStream_t s, int slot);
+constexpr int kTimingComposite = 0, kTimingTrainTile = 1, kTimingProject = 2,
+              kTimingTrainSplat = 3, kTimingChannels = 4;
+int timing_begin(hipStream_t s, hipEvent_t *dispatch_ev, int channel = kTimingComposite);
+void timing_end(hipStream_t s, int slot, int channel = kTimingComposite);
+
+// A launch that carries its timing events when tev[0] is set (timing.hip,
+// how = 1), a plain launch otherwise.
+template <typename K, typename... Args>
+inline void launch_timed(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s,
+                         const hipEvent_t *tev, Args... args) {
+    if (tev[0])
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, s, tev[0], tev[1], 0, args...);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
+}
 
 // XCD-aware block -> work-item remap.  Blocks b and b+8 share an XCD (they are
 // dealt round-robin over the 8 XCDs), so give each XCD a contiguous range of

@@ -330,12 +330,14 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
         const dim3 grid(ceil_div(per, bs / k), frames > 1 ? frames : 1);
 #define GSVC_FRAME_PROJECT(K)                                                                    \
     {                                                                                            \
-        auto kfn = frame_project_kernel<K, false>;                                               \
-        hipLaunchKernelGGL(kfn, grid, dim3(bs), 0, s, n, xyz, xyz_tanh, chol,          \
-                           chol_bound, feat, rgb_w, opac, hw, hh, tbx, tby, w.xys, w.radii,      \
-                           w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero, nullptr,      \
-                           frames > 1 ? frame_off : nullptr, f.counts_stride, f.m_stride,        \
-                           slab_stride, wt);                                                     \
+        hipEvent_t tev[2];                                                                       \
+        const int tslot = timing_begin(s, tev, kTimingProject);                                  \
+        launch_timed(frame_project_kernel<K, false>, grid, dim3(bs), 0, s, tev, n, xyz,          \
+                     xyz_tanh, chol, chol_bound, feat, rgb_w, opac, hw, hh, tbx, tby, w.xys,     \
+                     w.radii, w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero,            \
+                     (long long *)nullptr, frames > 1 ? frame_off : (const int *)nullptr,        \
+                     f.counts_stride, f.m_stride, slab_stride, wt);                              \
+        timing_end(s, tslot, kTimingProject);                                                    \
     }
         if (g_knobs[5] == 1 && g_debug_ptr) {  // diagnostic: per-wave stamps
             auto kfn = frame_project_kernel<1, true>;

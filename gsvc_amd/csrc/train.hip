@@ -639,8 +639,10 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
         auto kfn = train_tile_kernel<true>;
         hipLaunchKernelGGL(kfn, dim3(ntiles), dim3(kT), 0, s, T);
     } else {
-        auto kfn = train_tile_kernel<false>;
-        hipLaunchKernelGGL(kfn, dim3(ntiles), dim3(kT), 0, s, T);
+        hipEvent_t tev[2];
+        const int tslot = timing_begin(s, tev, kTimingTrainTile);
+        launch_timed(train_tile_kernel<false>, dim3(ntiles), dim3(kT), 0, s, tev, T);
+        timing_end(s, tslot, kTimingTrainTile);
     }
     rc = check_launch("train_step_sum: tiles");
     if (rc) return rc;
@@ -672,6 +674,9 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     P.loss = loss;
     // one extra (last) workgroup sums the loss, off the splat workgroups' path
     const int blocks = (num_points > 0 ? ceil_div(num_points, 256) : 0) + 1;
-    hipLaunchKernelGGL(train_splat_kernel, dim3(blocks), dim3(256), 0, s, P);
+    hipEvent_t tev[2];
+    const int tslot = timing_begin(s, tev, kTimingTrainSplat);
+    launch_timed(train_splat_kernel, dim3(blocks), dim3(256), 0, s, tev, P);
+    timing_end(s, tslot, kTimingTrainSplat);
     return check_launch("train_step_sum: splats");
 }

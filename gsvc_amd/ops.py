@@ -64,6 +64,26 @@ def composite_times_ms(max_launches: int = 4096):
     return list(buf[: cnt.value])
 
 
+TIMING_CHANNELS = {"composite": 0, "train_tile": 1, "project": 2, "train_splat": 3}
+
+
+def channel_timing(channel: str, on: bool, max_launches: int = 4096, every: int = 1,
+                   dispatch: bool = True):
+    """HIP-event timing of one kernel's launches (gsvc_timing_enable_channel):
+    ``channel`` is one of TIMING_CHANNELS; ``dispatch`` as composite_timing."""
+    L.call("gsvc_timing_enable_channel", TIMING_CHANNELS[channel], int(max_launches) if on else 0,
+           int(every), 1 if dispatch else 0)
+
+
+def channel_times_ms(channel: str, max_launches: int = 4096):
+    import ctypes
+    buf = (ctypes.c_float * max_launches)()
+    cnt = ctypes.c_int(0)
+    L.call("gsvc_timing_collect_channel", TIMING_CHANNELS[channel], ctypes.addressof(buf),
+           max_launches, ctypes.addressof(cnt))
+    return list(buf[: cnt.value])
+
+
 def kernel_times_ms(name: str):
     """Durations in ms of the recorded launches of ``name`` (synchronizes)."""
     if not _kernel_events:

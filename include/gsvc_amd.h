@@ -86,6 +86,11 @@ int gsvc_prune_lowest(int num_points, int remove_count, const float *rgb_w, int 
  * gsvc_timing_enable(0, 0, 0) stops and frees.  Not part of the reference. */
 int gsvc_timing_enable(int max_launches, int every, int how);
 int gsvc_timing_collect(float *ms, int max_out, int *count);
+/* The same for one kernel channel: 0 the composite (as above), 1 the fused
+ * training step's tile kernel, 2 the frame projection (render and training),
+ * 3 the training step's per-splat kernel (projection VJP + Adan). */
+int gsvc_timing_enable_channel(int channel, int max_launches, int every, int how);
+int gsvc_timing_collect_channel(int channel, float *ms, int max_out, int *count);
 
 /* Tuning / A-B knob for kernel variants (tools/kbench.py).  key 0 forces the
  * sum-forward kernel mode (0 = automatic), key 3 the per-tile threshold of

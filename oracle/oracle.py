@@ -18,6 +18,7 @@ Every function mirrors one reference operator (paths relative to
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 import subprocess
 
@@ -365,3 +366,96 @@ def prune_keep(rgb_w: np.ndarray, remove_count: int) -> np.ndarray:
     keep[order[:max(int(remove_count), 0)]] = False
     return keep
 
+
+
+# ---------------------------------------------------------------- Adan + train_iter
+# The checker for the fused training step and the CPU baseline of bench.py's
+# headline (BASELINE configs[2]).  Adan: reference optimizer.py:296-362
+# (``_multi_tensor_adan``) with the bias corrections of :171-173,211, restated
+# per element in float32 numpy in the foreach op order (each foreach op rounds
+# its result to fp32; Python-float scalars enter as fp32 for fp32 tensors).
+
+def adan_scalars(step, lr=1e-3, betas=(0.98, 0.92, 0.99), eps=1e-8, weight_decay=0.0):
+    b1, b2, b3 = betas
+    return dict(b1=b1, b2=b2, b3=b3, bc1=1.0 - b1 ** step, bc2=1.0 - b2 ** step,
+                bc3_sqrt=math.sqrt(1.0 - b3 ** step), lr=lr, wd=weight_decay, eps=eps)
+
+
+def adan_step(p, grad, st, step, lr=1e-3, betas=(0.98, 0.92, 0.99), eps=1e-8, weight_decay=0.0,
+              no_prox=False, clip=1.0):
+    """One Adan update of parameter ``p`` (float32 array, updated in place) with
+    gradient ``grad`` and state dict ``st`` (exp_avg, exp_avg_sq, exp_avg_diff,
+    neg_pre_grad; created on the first call as the reference does at
+    optimizer.py:181-189).  Returns ``p``."""
+    f = np.float32
+    S = adan_scalars(step, lr, betas, eps, weight_decay)
+    g = (np.asarray(grad, F32) * f(clip)).astype(F32)
+    if not st:
+        st["exp_avg"] = np.zeros_like(p)
+        st["exp_avg_sq"] = np.zeros_like(p)
+        st["exp_avg_diff"] = np.zeros_like(p)
+    if "neg_pre_grad" not in st or step == 1:
+        st["neg_pre_grad"] = (g * f(-1.0)).astype(F32)
+    m, v, df, npg = st["exp_avg"], st["exp_avg_sq"], st["exp_avg_diff"], st["neg_pre_grad"]
+    npg += g                                                          # :313
+    m *= f(S["b1"]); m += f(1 - S["b1"]) * g                          # :315-316
+    df *= f(S["b2"]); df += f(1 - S["b2"]) * npg                      # :318-319
+    npg *= f(S["b2"]); npg += g                                       # :321-322
+    v *= f(S["b3"]); v += f(1 - S["b3"]) * (npg * npg)                # :323-324
+    den = (np.sqrt(v) / f(S["bc3_sqrt"])).astype(F32) + f(S["eps"])   # :326-328
+    step_size = f(S["lr"] / S["bc1"])
+    step_diff = f(S["lr"] * S["b2"] / S["bc2"])
+    if no_prox:
+        p *= f(1 - S["lr"] * S["wd"])
+        p += (-step_size) * (m / den)
+        p += (-step_diff) * (df / den)
+    else:
+        p += (-step_size) * (m / den)
+        p += (-step_diff) * (df / den)
+        p /= f(1 + S["lr"] * S["wd"])
+    npg[...] = -g                                                     # :361-362
+    return p
+
+
+def train_iter_sum(params, gt, H, W, state, step, lr=1e-3):
+    """GaussianVideo_frame.train_iter (GaussianSplats_Represent.py:191-207) for
+    the L2 loss, no prune / densify, on CPU: activations (:57-70), the sum-path
+    forward (render_sum), clamp, F.mse_loss against ``gt`` [3, H, W], its
+    gradient through the clamp (torch clamp passes where 0 <= out <= 1), the
+    rasterizer and projection VJPs, the activation VJPs and one Adan step of
+    _xyz, _cholesky, _features_dc (rgb_W fixed at ones).  ``params``: dict of
+    float32 arrays ``_xyz`` [N,2], ``_cholesky`` [N,3], ``_features_dc`` [N,3],
+    updated in place; ``state``: dict of per-parameter Adan state dicts.
+    Returns (loss, psnr)."""
+    xyz, chol, feat = params["_xyz"], params["_cholesky"], params["_features_dc"]
+    n = xyz.shape[0]
+    means = np.tanh(xyz).astype(F32)
+    L = (chol + np.array([0.5, 0.0, 0.5], F32)).astype(F32)
+    colors = feat.astype(F32)
+    opac = np.ones((n, 1), F32)
+    r = render_sum(means, L, colors, opac, H, W)
+    out = r["out"]
+    img = np.clip(out, 0.0, 1.0).transpose(2, 0, 1)
+    gt = np.asarray(gt, F32).reshape(3, H, W)
+    d = (img - gt).astype(F32)
+    numel = 3 * H * W
+    loss = float(np.mean(d.astype(F64) ** 2))
+    if r["m"] < 1:
+        grads = [np.zeros_like(xyz), np.zeros_like(chol), np.zeros_like(feat)]
+    else:
+        v_img = (np.float32(2.0 / numel) * d).astype(F32)
+        v_img[(img < 0.0) | (img > 1.0)] = 0.0  # (never: img is clamped; kept for the rule)
+        o_chw = out.transpose(2, 0, 1)
+        v_img[(o_chw < 0.0) | (o_chw > 1.0)] = 0.0
+        v_out = np.ascontiguousarray(v_img.transpose(1, 2, 0))
+        tb = r["tb"]
+        v_xy, v_conic, v_rgb, _ = raster_sum_backward(tb, H, W, r["gids_sorted"], r["bins"], r["xys"],
+                                                      r["conics"], colors, opac, r["final_idx"],
+                                                      v_out)
+        _, v_mean2d, v_L = project_2d_backward(L, H, W, r["radii"], r["conics"],
+                                               v_xy.astype(F32), v_conic.astype(F32))
+        d_xyz = (v_mean2d * (1.0 - means * means)).astype(F32)
+        grads = [d_xyz, v_L.astype(F32), v_rgb.astype(F32)]
+    for name, p, g in zip(("_xyz", "_cholesky", "_features_dc"), (xyz, chol, feat), grads):
+        adan_step(p, g, state.setdefault(name, {}), step, lr=lr)
+    return loss, 10.0 * math.log10(1.0 / loss)

@@ -335,6 +335,59 @@ def make_train_iter_case(name, H, W, n, seed, isremoval=False):
     print(f"{name}: losses={losses} psnrs={psnrs}")
 
 
+def synthetic_gt_np(H, W, seed):
+    """The bench's target frame (gsvc_amd/frame.py ``synthetic_gt``, CPU torch
+    ops, so the same bits on any host with this torch): a sum of 8 seeded
+    sinusoids per channel.  Restated here because this script must import the
+    reference's ``gsplat``, not the repo's; the fixture stores a checksum that
+    tests/test_train_trajectory.py compares with the repo's function."""
+    g = torch.Generator().manual_seed(int(seed))
+    yy, xx = torch.meshgrid(torch.linspace(0, 1, H), torch.linspace(0, 1, W), indexing="ij")
+    chans = []
+    for _ in range(3):
+        acc = torch.zeros(H, W)
+        for _ in range(8):
+            fx, fy, ph = (torch.rand(3, generator=g) * torch.tensor([12.0, 12.0, 6.28])).tolist()
+            acc += torch.sin(fx * xx + fy * yy + ph)
+        chans.append(0.5 + 0.5 * acc / 8)
+    return torch.stack(chans)[None].clamp(0, 1)
+
+
+def make_train_trajectory_case(name, H, W, n, seed, gt_seed, iters, keep=4096):
+    """BASELINE configs[2] at full size: ``iters`` reference
+    GaussianVideo_frame.train_iter steps (GaussianSplats_Represent.py:191-207:
+    forward, L2, backward, PSNR, Adan, StepLR) at H x W with n splats, oracle
+    injected, torch.sort stable.  Records per-iteration loss / PSNR, the
+    parameters of the first ``keep`` splats after the last step and float64
+    checksums of every parameter (the whole 50k-splat state would be 1.8 MB)."""
+    import time
+    sys.path.insert(0, REF)
+    import GaussianSplats_Represent as GR
+    torch.manual_seed(seed)
+    model = GR.GaussianVideo_frame(
+        loss_type="L2", opt_type="adan", num_points=n, max_num_points=n, densification_interval=100,
+        iterations=30000, H=H, W=W, BLOCK_H=16, BLOCK_W=16, device=torch.device("cpu"), lr=1e-3,
+        quantize=False, removal_rate=0.1, isdensity=False, isremoval=False)
+    gt = synthetic_gt_np(H, W, gt_seed)
+    losses, psnrs = [], []
+    t0 = time.time()
+    for it in range(1, iters + 1):
+        loss, psnr = model.train_iter(gt, it)
+        losses.append(float(loss.item()))
+        psnrs.append(float(psnr))
+    rec = dict(H=H, W=W, n=n, seed=seed, gt_seed=gt_seed, iters=iters,
+               gt_sum=np.float64(gt.double().sum()), gt_sq=np.float64((gt.double() ** 2).sum()),
+               losses=np.array(losses), psnrs=np.array(psnrs))
+    for k, v in model.state_dict().items():
+        a = _np(v)
+        if a.ndim == 2 and a.shape[0] == n:
+            rec["final_" + k] = a[:keep].copy()
+            rec["sum_" + k] = np.float64(a.astype(np.float64).sum())
+            rec["abssum_" + k] = np.float64(np.abs(a.astype(np.float64)).sum())
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **rec)
+    print(f"{name}: {iters} iters in {time.time() - t0:.1f} s, psnrs={[round(p, 4) for p in psnrs]}")
+
+
 def make_prune_cases():
     """removal_control / adaptive_control (GaussianSplats_Represent.py:98-172)
     of the reference model on CPU, torch.sort made stable (the GPU's radix
@@ -387,6 +440,10 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "prune":
         _import_reference()
         make_prune_cases()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "trajectory":
+        _import_reference()
+        make_train_trajectory_case("train_traj_1080p_n50k", 1080, 1920, 50000, 7, 8, 40)
         return
     gs = _import_reference()
     os.makedirs(OUT, exist_ok=True)
