@@ -22,7 +22,7 @@ int check_launch(const char *what) {
     return GSVC_OK;
 }
 
-int g_knobs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+int g_knobs[kKnobs] = {};
 void *g_debug_ptr = nullptr;
 
 }  // namespace gsvc
@@ -30,7 +30,7 @@ void *g_debug_ptr = nullptr;
 extern "C" int gsvc_abi_version(void) { return 1; }
 
 extern "C" int gsvc_debug_set(int key, int value) {
-    if (key < 0 || key >= 8) return -1;
+    if (key < 0 || key >= gsvc::kKnobs) return -1;
     const int old = gsvc::g_knobs[key];
     gsvc::g_knobs[key] = value;
     return old;

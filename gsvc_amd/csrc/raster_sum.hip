@@ -40,6 +40,7 @@
 
 #include "frame.h"
 #include "raster_sum.h"
+#include "tile_ids.h"
 
 namespace gsvc {
 
@@ -64,13 +65,6 @@ constexpr int kSlice = kTilePix * 3 / 4;  // float4s of LDS per wave (3 KB)
 enum { kModeAdaptive = 6, kModeSparse = 1, kModeBanded = 2, kModeStamp = 3, kModeNoBlend = 4,
        kModeNoStore = 5, kModeSparseStamp = 7 };
 constexpr int kDenseEntriesPerTile = 8;  // measured crossover: 20k splats (6.1 per tile) sparse 22.1 vs banded 23.7 us, 30k (9.1) equal
-
-__device__ __forceinline__ void wave_lds_sync() {
-    // a wave owns its LDS slice and LDS ops of a wave complete in order: a
-    // drain of lgkmcnt is the only fence needed (no s_barrier)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-}
 
 // Diagnostic only (kModeStamp): s_memrealtime (100 MHz) stamps per tile,
 // written to the final_Ts slot reinterpreted as int64[ntiles][4].
@@ -207,122 +201,11 @@ __device__ __forceinline__ void store_pixel(const SumFwdArgs &A, size_t p, float
     if (A.final_Ts) A.final_Ts[p] = 1.0f;
 }
 
-// The tile's splat ids in ascending order -- the first min(n_all, 256) of
-// them -- into s_ids (LDS): the segment sort of binning.hip done by the wave
-// that blends the tile, when the ids arrive in fill order (frame path).  At
-// most 64 entries: ranks by broadcast compares; more: an LDS bitmap over the
-// id range in windows of 16384 ids, emitted in order until 256 are found.
-// ``bm`` is 512 words of this wave's LDS (free until blending starts).  Ids
-// are unique within a tile, so this is the stable sort's order.
-constexpr int kSortWords = 512;
-
-// Id of slot j of a tile's segment: a plain int array, or the id lane of a
-// slab record (stride 12 floats).
-struct SegIds {
-    const int *ids;
-    const float4 *recs;  // slab body (slots >= kHeadSlots at their index) ...
-    const float4 *head;  // ... and the tile's head slots
-    __device__ __forceinline__ int operator[](int j) const {
-        if (!recs) return ids[j];
-        return __float_as_int(j < kHeadSlots ? head[3 * j + 2].y : recs[3 * j + 2].y);
-    }
-};
-
-__device__ __forceinline__ int rank_below(int v, int n) {
-    // number of lanes k < n whose value is below v (ties impossible: ids unique)
-    int rank = 0;
-    for (int k = 0; k < n; ++k) rank += (__builtin_amdgcn_readlane(v, k) < v) ? 1 : 0;
-    return rank;
-}
-
-__device__ int wave_sorted_tile_ids(SegIds ids, int n_all, int *s_ids, unsigned *bm) {
-    const int lane = threadIdx.x & 63;
-    if (n_all <= 0) return 0;
-    if (n_all <= 64) {
-        const int v = lane < n_all ? ids[lane] : 0x7fffffff;
-        const int rank = rank_below(v, n_all);
-        if (lane < n_all) s_ids[rank] = v;
-        wave_lds_sync();
-        return n_all;
-    }
-    int lo = 0x7fffffff, hi = -1;
-    for (int j = lane; j < n_all; j += 64) {
-        const int v = ids[j];
-        lo = min(lo, v);
-        hi = max(hi, v);
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        lo = min(lo, __shfl_xor(lo, off, 64));
-        hi = max(hi, __shfl_xor(hi, off, 64));
-    }
-    int written = 0;
-    for (long long base = lo; base <= hi && written < kTilePix; base += 32 * kSortWords) {
-        for (int w = lane; w < kSortWords; w += 64) bm[w] = 0u;
-        wave_lds_sync();
-        for (int j = lane; j < n_all; j += 64) {
-            const long long d = (long long)ids[j] - base;
-            if (d >= 0 && d < 32 * kSortWords) atomicOr(bm + (d >> 5), 1u << (d & 31));
-        }
-        wave_lds_sync();
-        constexpr int kPer = kSortWords / 64;  // words per lane, in order
-        unsigned wv[kPer];
-        int cnt = 0;
-#pragma unroll
-        for (int q = 0; q < kPer; ++q) {
-            wv[q] = bm[kPer * lane + q];
-            cnt += __popc(wv[q]);
-        }
-        int incl = cnt;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int u = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += u;
-        }
-        int pos = written + incl - cnt;
-#pragma unroll
-        for (int q = 0; q < kPer; ++q) {
-            unsigned bits = wv[q];
-            while (bits && pos < kTilePix) {
-                s_ids[pos++] = (int)(base + 32 * (kPer * lane + q) + (__ffs(bits) - 1));
-                bits &= bits - 1u;
-            }
-        }
-        written += __shfl(incl, 63, 64);
-        wave_lds_sync();
-    }
-    return min(written, kTilePix);
-}
-
 // A tile with more than 256 entries on the frame path (its slab kept an
-// arbitrary 256): its first 256 ids are rebuilt by testing every splat's tile
-// bbox (the binning's own tile_bbox of xys and radii) in id order, 64 at a
-// time, compacting the hits by ballot -- sorted by construction.
-__device__ int wave_brute_tile_ids(const SumFwdArgs &A, int tile, int *s_ids) {
-    const int lane = threadIdx.x & 63;
-    const unsigned ty = (unsigned)(tile / A.tbx), tx = (unsigned)(tile - (int)ty * A.tbx);
-    const int tby = (A.img_h + kTile - 1) / kTile;
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    int written = 0;
-    for (int base = A.splat_begin; base < A.num_points && written < kTilePix; base += 64) {
-        const int j = base + lane;
-        bool hit = false;
-        if (j < A.num_points) {
-            const int r = A.cull_radii[j];
-            if (r > 0) {
-                const float2 c = A.cull_xys[j];
-                unsigned x0, y0, x1, y1;
-                tile_bbox(c.x, c.y, (float)r, A.tbx, tby, x0, y0, x1, y1);
-                hit = tx >= x0 && tx < x1 && ty >= y0 && ty < y1;
-            }
-        }
-        const unsigned long long m = __ballot(hit);
-        const int pos = written + __popcll(m & lt);
-        if (hit && pos < kTilePix) s_ids[pos] = j;
-        written += __popcll(m);
-    }
-    wave_lds_sync();
-    return min(written, kTilePix);
+// arbitrary 256): its first 256 ids are rebuilt from every splat's tile bbox.
+__device__ __forceinline__ int wave_brute_tile_ids(const SumFwdArgs &A, int tile, int *s_ids) {
+    return wave_brute_ids(A.cull_xys, A.cull_radii, A.splat_begin, A.num_points, A.tbx,
+                          (A.img_h + kTile - 1) / kTile, tile, s_ids);
 }
 
 // Sparse path: one wave blends the whole 16x16 tile, 4 pixels per lane.

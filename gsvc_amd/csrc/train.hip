@@ -27,6 +27,7 @@
 //       a fixed order into the loss.
 #include "adan.h"
 #include "frame.h"
+#include "tile_ids.h"
 
 namespace gsvc {
 
@@ -75,8 +76,10 @@ __device__ __forceinline__ unsigned ellipse_rect(float x, float y, float a, floa
     const float lg = __logf(255.0f * o);
     if (lg < -0.01f) return kNoRect;  // o < e^-0.01 / 255: alpha < 1/255 everywhere
     const float S2 = 2.0f * (lg * 1.001f + 0.01f);
-    const float ex = sqrtf(S2 * c / det) * 1.001f + 0.01f;
-    const float ey = sqrtf(S2 * a / det) * 1.001f + 0.01f;
+    // hardware rcp / sqrt (~1 ulp): the 0.1 % + 0.01 px margins dwarf their error
+    const float inv_det = __builtin_amdgcn_rcpf(det);
+    const float ex = __builtin_amdgcn_sqrtf(S2 * c * inv_det) * 1.001f + 0.01f;
+    const float ey = __builtin_amdgcn_sqrtf(S2 * a * inv_det) * 1.001f + 0.01f;
     const float x0 = fmaxf(ceilf(x - ex - tx0), 0.0f), x1 = fminf(floorf(x + ex - tx0), 15.0f);
     const float y0 = fmaxf(ceilf(y - ey - ty0), 0.0f), y1 = fminf(floorf(y + ey - ty0), 15.0f);
     if (!(x0 <= x1) || !(y0 <= y1)) return kNoRect;
@@ -405,6 +408,401 @@ __global__ __launch_bounds__(256, 8) void train_tile_kernel(TrainTileArgs A) {
     if (kStamp && tid == 0) st[5] = tstamp();
 }
 
+// ---------------------------------------------------------------------------
+// Two waves per tile (production): train_tile_kernel's per-tile work in a
+// 128-thread workgroup whose waves each own one 8-row band of the tile
+// (2 pixels per lane), 9.9 KB of LDS, so 16 tiles are resident per CU (the
+// 256-thread kernel: 8).
+//   1. count + the first kWSpec slab records in the same round trip as the
+//      lanes' gt; records ranked by id and staged at their rank with their
+//      reachable rectangle (ellipse_rect).  > 64 entries: ids ranked through
+//      LDS (or rebuilt past 256 from the splats' bboxes) and records gathered
+//      64 at a time.
+//   2. forward: each wave blends only the entries whose rectangle reaches its
+//      band (a culled pair contributes nothing in the reference either), in
+//      entry order, with the render's op sequence at unit opacity (1 * e ==
+//      e: the same image bits); clamp, loss gradient, error sums; v_out planes
+//      into LDS.
+//   3. backward over work items = one row of an entry's rectangle, up to
+//      kBRun pixels (the row terms of sigma shared), laid out entry by entry
+//      over the 128 lanes; each item's 8 gradient sums go to an LDS partial
+//      slot and each entry adds its items' partials in item order
+//      (deterministic, no LDS atomics); then 8 lanes per entry add the
+//      entry's 32 bytes into the splat's gradient record (one request per
+//      (splat, tile)).
+// GSVC's opacity is ones (GaussianSplats_Represent.py:84) and the training
+// step projects with opacity 1, so the opacity gradient (record slot 8) is
+// not formed.
+constexpr int kBSpec = 32;    // slab slots loaded with the count
+constexpr int kBChunk = 64;   // entries staged at a time
+constexpr int kBRun = 8;      // pixels per backward work item (part of one rectangle row)
+constexpr int kBThreads = 128;
+
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+// raster_sum.hip blend_pair at opacity 1 (no index tracking): one splat
+// against two pixels of a row; a failing pair keeps its accumulators.
+__device__ __forceinline__ void blend2_unit(float gx, float ha, float bdy, float cq, float cr,
+                                            float cg, float cb, v2f px, v2f &ar, v2f &ag, v2f &ab) {
+    const v2f dx = gx - px;
+    const v2f q = __builtin_elementwise_fma((v2f)ha, dx, (v2f)bdy);
+    const v2f sg = __builtin_elementwise_fma(q, dx, (v2f)cq);
+    const v2f x = sg * kNegLog2e;
+    const v2f e = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+    const v2f a = {fminf(1.0f, e.x), fminf(1.0f, e.y)};
+    const bool v0 = !(sg.x < 0.0f) && !(a.x < kAlphaMin);
+    const bool v1 = !(sg.y < 0.0f) && !(a.y < kAlphaMin);
+    const v2f nr = __builtin_elementwise_fma((v2f)cr, a, ar);
+    const v2f ng = __builtin_elementwise_fma((v2f)cg, a, ag);
+    const v2f nb = __builtin_elementwise_fma((v2f)cb, a, ab);
+    ar = (v2f){v0 ? nr.x : ar.x, v1 ? nr.y : ar.y};
+    ag = (v2f){v0 ? ng.x : ag.x, v1 ? ng.y : ag.y};
+    ab = (v2f){v0 ? nb.x : ab.x, v1 ? nb.y : ab.y};
+}
+
+// Inclusive scans over one wave's 64 lanes with DPP (no LDS traffic):
+// row_shr 1, 2, 4, 8 inside each 16-lane row, then row_bcast 15 / 31 carry a
+// row's last lane into the rows above; ``id`` is the operation's identity.
+template <bool kMax>
+__device__ __forceinline__ int wave_scan_dpp(int v, int id) {
+    auto step = [&](int t) { v = kMax ? max(v, t) : v + t; };
+    step(__builtin_amdgcn_update_dpp(id, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    step(__builtin_amdgcn_update_dpp(id, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    step(__builtin_amdgcn_update_dpp(id, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    step(__builtin_amdgcn_update_dpp(id, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    step(__builtin_amdgcn_update_dpp(id, v, 0x142, 0xa, 0xf, false));  // row_bcast:15 -> rows 1, 3
+    step(__builtin_amdgcn_update_dpp(id, v, 0x143, 0xc, 0xf, false));  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
+struct BandLds {
+    float v[3][kTilePix];          // v_out planes
+    float4 geo[kBChunk];           // staged entries (rank order): x, y, a/2, b
+    float4 col[kBChunk];           //   c/2, r, g, b
+    unsigned ro[kBChunk];          //   rectangle (16 bits) | first work item << 16
+    int gid[kBChunk];              //   splat id
+    float part[8][kBThreads];      // backward: item partials; ranking / flush scratch
+    signed char own[kBThreads];    // backward: entry of the round's first items
+    int misc[8];
+};
+
+template <bool kStamp>
+__global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTileArgs A) {
+    __shared__ BandLds S;
+    const int tile = xcd_remap(blockIdx.x, A.ntiles);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    long long *st = kStamp ? A.stamps + 8 * (size_t)tile : nullptr;
+    if (kStamp && tid == 0) st[0] = tstamp();
+    const int ty = tile / A.tbx, tx = tile - ty * A.tbx;
+    const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
+    const int prow = 8 * w + (lane >> 3), pcol = (lane & 7) << 1;  // tile-local pixel pair
+    const int pi = ty * kTile + prow, pj = tx * kTile + pcol;
+    const bool row_in = pi < A.img_h;
+    const int nin = row_in ? min(2, A.img_w - pj) : 0;  // pixels of the pair inside the image
+    const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
+    const size_t pix0 = row_in ? (size_t)pi * (size_t)A.img_w + (size_t)pj : 0;
+    // the pair's targets, loaded first
+    float gt[3][2];
+    if (nin == 2 && (A.img_w & 1) == 0) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float2 v = *reinterpret_cast<const float2 *>(A.gt + c * hw + pix0);
+            gt[c][0] = v.x;
+            gt[c][1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) gt[c][q] = q < nin ? A.gt[c * hw + pix0 + q] : 0.0f;
+    }
+    // this tile's count and its first kBSpec slab records in the same round trip
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+    if (tid < kBSpec) {
+        const float4 *h = slab_rec(A.slab, A.ntiles, tile, tid);
+        r0 = h[0];
+        r1 = h[1];
+        r2 = h[2];
+    }
+    const bool empty = *A.m_dev < 1;  // rasterize_sum.py:121-127: background, no gradient
+    const int n_all = empty ? 0 : (int)__builtin_amdgcn_readfirstlane(A.counts[tile]);
+    if (tid == 0) A.counts_clear[tile] = 0u;  // the next frame's counts
+    const bool dense = n_all > kBChunk;
+    const bool brute = n_all > kTilePix;  // the slab dropped entries: ids rebuilt
+    int *s_key = reinterpret_cast<int *>(&S.part[0][0]);     // dense: key (slot / id) by rank
+    int *s_ids = reinterpret_cast<int *>(&S.part[2][0]);     // dense: slot ids (scratch)
+    int n = n_all;
+
+    // 1. the order
+    if (!dense) {
+        if (tid >= kBSpec && tid < n) {
+            const float4 *h = slab_rec(A.slab, A.ntiles, tile, tid);
+            r0 = h[0];
+            r1 = h[1];
+            r2 = h[2];
+        }
+        if (w == 0 && lane < n) {
+            const int id = __float_as_int(r2.y);
+            const int rank = rank_below(id, n);
+            S.geo[rank] = r0;
+            S.col[rank] = make_float4(r1.x, r1.z, r1.w, r2.x);
+            S.gid[rank] = id;
+            S.ro[rank] = ellipse_rect(r0.x, r0.y, 2.0f * r0.z, r0.w, 2.0f * r1.x, 1.0f, tx0, ty0);
+        }
+    } else if (brute) {
+        if (w == 0)
+            n = wave_brute_ids(A.xys, A.radii, 0, A.num_points, A.tbx,
+                               (A.img_h + kTile - 1) / kTile, tile, s_key);
+        n = min(n_all, kTilePix);  // both waves: wave_brute_ids finds >= 256 of them
+    } else {
+        for (int j = tid; j < n; j += kBThreads)
+            s_ids[j] = __float_as_int(slab_rec(A.slab, A.ntiles, tile, j)[2].y);
+        __syncthreads();
+        for (int j = tid; j < n; j += kBThreads) {
+            const int v = s_ids[j];
+            int rank = 0;
+            for (int k = 0; k < n; ++k) rank += s_ids[k] < v ? 1 : 0;
+            s_key[rank] = j;
+        }
+    }
+    __syncthreads();
+    if (kStamp && tid == 0) st[1] = tstamp();
+
+    // 2. forward: this wave's band against the entries that can reach it
+    v2f ar, ag, ab;
+    {
+        const float b0 = empty ? A.bg[0] : 0.0f, b1 = empty ? A.bg[1] : 0.0f, b2 = empty ? A.bg[2] : 0.0f;
+        ar = (v2f){b0, b0};
+        ag = (v2f){b1, b1};
+        ab = (v2f){b2, b2};
+    }
+    const float py = (float)pi;
+    const v2f px = {(float)pj, (float)(pj + 1)};
+    const int y_lo = 8 * w, y_hi = 8 * w + 7;
+    // dense: stage chunk [c0, c0 + cnt) of the order (both waves load half)
+    auto stage_chunk = [&](const int *keys, int cnt) {
+        if (tid < cnt) {
+            const int key = keys[tid];
+            const float4 *rr = brute ? A.rec + 3 * (size_t)key : slab_rec(A.slab, A.ntiles, tile, key);
+            const float4 a = rr[0], b = rr[1], c = rr[2];
+            S.geo[tid] = a;
+            S.col[tid] = make_float4(b.x, b.z, b.w, c.x);
+            S.gid[tid] = __float_as_int(c.y);
+            S.ro[tid] = ellipse_rect(a.x, a.y, 2.0f * a.z, a.w, 2.0f * b.x, 1.0f, tx0, ty0);
+        }
+    };
+    for (int c0 = 0; c0 < n; c0 += kBChunk) {
+        const int cnt = min(kBChunk, n - c0);
+        if (dense) {
+            stage_chunk(s_key + c0, cnt);
+            __syncthreads();
+        }
+        // the entries whose rectangle reaches this band, as a wave-uniform mask
+        bool keep = false;
+        if (lane < cnt) {
+            const unsigned rc = S.ro[lane];
+            keep = rc != kNoRect && (int)((rc >> 12) & 15u) >= y_lo && (int)((rc >> 8) & 15u) <= y_hi;
+        }
+        unsigned long long m = __ballot(keep);
+        while (m) {
+            const int k = __builtin_ctzll(m);
+            m &= m - 1ull;
+            const float4 G = S.geo[k];
+            const float4 C = S.col[k];
+            const float dy = G.y - py;
+            const float cq = (C.x * dy) * dy;
+            const float bdy = G.w * dy;
+            blend2_unit(G.x, G.z, bdy, cq, C.y, C.z, C.w, px, ar, ag, ab);
+        }
+        if (dense) __syncthreads();  // the next chunk overwrites the staging
+    }
+    // dense: the keys of ranks tid and tid + 128, kept in registers (the
+    // backward's partials overwrite s_key)
+    int kr0 = 0, kr1 = 0;
+    if (dense) {
+        kr0 = tid < n ? s_key[tid] : 0;
+        kr1 = tid + kBThreads < n ? s_key[tid + kBThreads] : 0;
+    }
+    if (kStamp && tid == 0) st[2] = tstamp();
+
+    // 3. clamp, loss gradient (mse_loss backward: norm * (a - b); l1: norm * sgn),
+    // clamp backward (passes where 0 <= out <= 1), error sums; v_out planes
+    {
+        const float o[3][2] = {{ar.x, ar.y}, {ag.x, ag.y}, {ab.x, ab.y}};
+        float se = 0.f, ae = 0.f;
+        float v[3][2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const bool inside = q < nin;
+            float pse = 0.f, pae = 0.f;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const float x = clamp_unit(o[c][q]);
+                const float d = x - gt[c][q];
+                pse = fmaf(d, d, pse);
+                pae += fabsf(d);
+                const float sg = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+                const float gv = A.loss_l1 ? A.norm * sg : A.norm * d;
+                v[c][q] = (inside && o[c][q] >= 0.0f && o[c][q] <= 1.0f) ? gv : 0.0f;
+            }
+            if (inside) {
+                se += pse;
+                ae += pae;
+            }
+        }
+        if (A.out) {  // optional clamped render (tests)
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                for (int q = 0; q < nin; ++q) A.out[c * hw + pix0 + q] = clamp_unit(o[c][q]);
+        }
+        const int p = prow * kTile + pcol;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) *reinterpret_cast<float2 *>(&S.v[c][p]) = make_float2(v[c][0], v[c][1]);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            se += __shfl_xor(se, off, 64);
+            ae += __shfl_xor(ae, off, 64);
+        }
+        if (lane == 0) {
+            S.misc[2 * w] = __float_as_int(se);
+            S.misc[2 * w + 1] = __float_as_int(ae);
+        }
+        __syncthreads();
+        if (tid == 0)
+            A.err[tile] = make_float2(__int_as_float(S.misc[0]) + __int_as_float(S.misc[2]),
+                                      __int_as_float(S.misc[1]) + __int_as_float(S.misc[3]));
+    }
+    if (kStamp && tid == 0) st[3] = tstamp();
+
+    // 4. backward, kBChunk entries at a time (sparse tiles: the forward's staging)
+    for (int c0 = 0; c0 < n; c0 += kBChunk) {
+        const int gn = min(kBChunk, n - c0);
+        if (dense) {
+            __syncthreads();  // misc / staging / partial readers done
+            // this chunk's keys, by rank, into the gid slots stage_chunk overwrites
+            if (tid >= c0 && tid < c0 + gn) S.gid[tid - c0] = kr0;
+            if (tid + kBThreads >= c0 && tid + kBThreads < c0 + gn) S.gid[tid + kBThreads - c0] = kr1;
+            __syncthreads();
+            stage_chunk(S.gid, gn);
+            __syncthreads();
+        }
+        // work items of entry e (wave 0, lane e): one per kBRun pixels of each rectangle row
+        int items = 0;
+        unsigned rc = kNoRect;
+        if (w == 0 && lane < gn) {
+            rc = S.ro[lane];
+            if (rc != kNoRect) {
+                const int rw = (int)((rc >> 4) & 15u) - (int)(rc & 15u) + 1;
+                const int rh = (int)((rc >> 12) & 15u) - (int)((rc >> 8) & 15u) + 1;
+                items = rh * ((rw + kBRun - 1) / kBRun);
+            }
+        }
+        const int incl = wave_scan_dpp<false>(items, 0);
+        const int off = incl - items;
+        if (w == 0) {
+            if (lane < gn) S.ro[lane] = (rc & 0xffffu) | ((unsigned)off << 16);
+            if (lane == 63) S.misc[4] = incl;
+        }
+        __syncthreads();
+        const int total = S.misc[4];
+        float acc[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc[c] = 0.0f;
+        for (int base = 0; base < total; base += kBThreads) {
+            // the entry of item base + tid: the last entry whose first item is <= it
+            S.own[tid] = -1;
+            __syncthreads();
+            if (items > 0 && off >= base && off < base + kBThreads) S.own[off - base] = (signed char)lane;
+            if (w == 0) {
+                const unsigned long long before = __ballot(lane < gn && off <= base);
+                if (lane == 0) S.misc[5] = __popcll(before) - 1;  // entry straddling into this round
+            }
+            __syncthreads();
+            int own = max((int)S.own[tid], S.misc[5]);
+            own = wave_scan_dpp<true>(own, -2147483647 - 1);
+            if (w == 1) {
+                // wave 1 continues wave 0's scan: the largest head among items base .. base+63
+                int m = (int)S.own[lane];
+#pragma unroll
+                for (int o2 = 32; o2 > 0; o2 >>= 1) m = max(m, __shfl_xor(m, o2, 64));
+                own = max(own, max(m, S.misc[5]));
+            }
+            const int item = base + tid;
+            float g[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) g[c] = 0.0f;
+            if (item < total) {
+                const float4 G = S.geo[own], C = S.col[own];
+                const unsigned ro = S.ro[own];
+                const int j = item - (int)(ro >> 16);  // item index within the entry
+                const int rx0 = (int)(ro & 15u), rx1 = (int)((ro >> 4) & 15u);
+                const int ipr = (rx1 - rx0 + kBRun) / kBRun;  // items per rectangle row (1, 2)
+                const int jr = ipr == 1 ? j : (j >> 1);
+                const int row = (int)((ro >> 8) & 15u) + jr;
+                const int cs = rx0 + kBRun * (j - jr * ipr);
+                const int ce = min(min(cs + kBRun - 1, rx1), A.img_w - 1 - (int)tx0);
+                const float pyf = ty0 + (float)row;
+                if ((int)pyf < A.img_h) {
+                    const float ex = G.x, eha = G.z, eb = G.w;
+                    const float dy = G.y - pyf;
+                    const float cq = (C.x * dy) * dy;  // splat_sigma_h's row terms
+                    const float bdy = eb * dy;
+                    const float fcdy = (2.0f * C.x) * dy;
+                    const float fa = 2.0f * eha;
+                    for (int col = cs; col <= ce; ++col) {
+                        const float pxf = tx0 + (float)col;
+                        const int pix = row * kTile + col;
+                        const float Px = S.v[0][pix], Py = S.v[1][pix], Pz = S.v[2][pix];
+                        const float dx = ex - pxf;
+                        const float sgm = fmaf(fmaf(eha, dx, bdy), dx, cq);
+                        const float vis = exp_neg(sgm);
+                        const float al = fminf(1.0f, vis);  // opacity 1
+                        if (sgm < 0.0f || al < kAlphaMin) continue;
+                        const float v_alpha = fmaf(C.w, Pz, fmaf(C.z, Py, C.y * Px));
+                        const float v_sigma = (-vis) * v_alpha;  // (-opacity * vis) * v_alpha
+                        g[5] = fmaf(al, Px, g[5]);
+                        g[6] = fmaf(al, Py, g[6]);
+                        g[7] = fmaf(al, Pz, g[7]);
+                        const float hs = 0.5f * v_sigma;
+                        const float hsdx = hs * dx;
+                        g[2] = fmaf(hsdx, dx, g[2]);
+                        g[3] = fmaf(hsdx, dy, g[3]);
+                        g[4] = fmaf(hs * dy, dy, g[4]);
+                        g[0] = fmaf(v_sigma, fmaf(fa, dx, bdy), g[0]);
+                        g[1] = fmaf(v_sigma, fmaf(eb, dx, fcdy), g[1]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 8; ++c) S.part[c][tid] = g[c];
+            __syncthreads();
+            // each entry adds its items of this round in item order
+            if (w == 0 && items > 0) {
+                const int i0 = max(off, base), i1 = min(off + items, base + kBThreads);
+                for (int it = i0; it < i1; ++it) {
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) acc[c] += S.part[c][it - base];
+                }
+            }
+            __syncthreads();  // partials read before the next round rewrites them
+        }
+        // 8 lanes per entry add the entry's sums into the splat's gradient record
+        if (w == 0 && lane < gn) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) S.part[c][lane] = acc[c];
+        }
+        __syncthreads();
+        for (int q = tid; q < gn * 8; q += kBThreads) {
+            const int e = q >> 3, c = q & 7;
+            unsafeAtomicAdd(A.grad + (size_t)S.gid[e] * 16 + c, S.part[c][e]);
+        }
+    }
+    if (kStamp && tid == 0) {
+        st[4] = tstamp();
+        st[5] = tstamp();
+    }
+}
+
 struct TrainSplatArgs {
     int n, ntiles, rgbw_train, update;
     float hw, hh;
@@ -638,10 +1036,17 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
         T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
         auto kfn = train_tile_kernel<true>;
         hipLaunchKernelGGL(kfn, dim3(ntiles), dim3(kT), 0, s, T);
+    } else if (g_knobs[5] == 3 && g_debug_ptr) {  // diagnostic: per-tile stamps, band kernel
+        T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
+        hipLaunchKernelGGL(train_tile_band_kernel<true>, dim3(ntiles), dim3(kBThreads), 0, s, T);
     } else {
+        // knob 8 = 1: the 256-thread workgroup-per-tile kernel (A/B)
         hipEvent_t tev[2];
         const int tslot = timing_begin(s, tev, kTimingTrainTile);
-        launch_timed(train_tile_kernel<false>, dim3(ntiles), dim3(kT), 0, s, tev, T);
+        if (g_knobs[8] == 1)
+            launch_timed(train_tile_kernel<false>, dim3(ntiles), dim3(kT), 0, s, tev, T);
+        else
+            launch_timed(train_tile_band_kernel<false>, dim3(ntiles), dim3(kBThreads), 0, s, tev, T);
         timing_end(s, tslot, kTimingTrainTile);
     }
     rc = check_launch("train_step_sum: tiles");

@@ -91,8 +91,6 @@ class GaussianVideoFrame(nn.Module):
         self.register_buffer("cholesky_bound", torch.tensor([0.5, 0, 0.5]).view(1, 3))
         self.lr = kwargs["lr"]
         self.opt_type = kwargs["opt_type"]
-        # the fused HIP Adan on GPU models (numerically the foreach update)
-        self.fused_adan = kwargs.get("fused_adan", str(self.device).startswith("cuda"))
         # whole train_iter as one fused call (gsvc_amd/train.py) where it applies
         self.fused_train = kwargs.get("fused_train", str(self.device).startswith("cuda"))
         self.fused_steps = 0
@@ -162,7 +160,7 @@ class GaussianVideoFrame(nn.Module):
         if self.opt_type == "adam":
             self.optimizer = torch.optim.Adam(self.parameters(), lr=self.lr)
         else:
-            self.optimizer = Adan(self.parameters(), lr=self.lr, fused=self.fused_adan)
+            self.optimizer = Adan(self.parameters(), lr=self.lr)
 
     def _remove_lowest(self, remove_count):
         # norm + torch.sort + boolean mask + p[keep] (GaussianSplats_Represent.py:
@@ -417,7 +415,7 @@ class GaussianVideoFrame(nn.Module):
 
 def make_frame_model(H, W, num_points, device, seed=None, lr=1e-3, isremoval=False,
                      isdensity=False, removal_rate=0.1, max_num_points=None,
-                     densification_interval=100, fused_adan=None, fused_train=None):
+                     densification_interval=100, fused_train=None):
     """Construct like SimpleTrainer2d does (train_video_Represent.py:51-55)."""
     if seed is not None:
         torch.manual_seed(seed)
@@ -426,7 +424,6 @@ def make_frame_model(H, W, num_points, device, seed=None, lr=1e-3, isremoval=Fal
         max_num_points=max_num_points or num_points, densification_interval=densification_interval,
         iterations=30000, H=H, W=W, BLOCK_H=16, BLOCK_W=16, device=device, lr=lr, quantize=False,
         removal_rate=removal_rate, isdensity=isdensity, isremoval=isremoval,
-        **({} if fused_adan is None else {"fused_adan": fused_adan}),
         **({} if fused_train is None else {"fused_train": fused_train})).to(device)
     return model
 

@@ -14,8 +14,9 @@ detect_outliers_mean_diff :214-229) that runs on the MI355X path:
   rank taking a contiguous frame range plus a one-frame halo;
 * the frames are split into GOPs (a K-frame and the P-frames after it, which
   start from the previous frame's model) and ranks take contiguous GOPs
-  (shard.py); K-frames are forced at the shard boundaries, which
-  K_frames.txt then records so a reference run uses the same GOPs;
+  (shard.py); when there are fewer GOPs than ranks, K-frames are forced at
+  the shard boundaries; K_frames_used.txt records the GOPs trained and a
+  missing K_frames.txt is written from detection (never overwritten);
 * each frame trains with ``GaussianVideoFrame.train_iter`` (the fused step on
   the GPU), early stopping as the reference, then PSNR and the eval FPS of
   100 renders (synchronised);
@@ -46,7 +47,7 @@ import torch.nn.functional as F
 
 from .frame import GaussianVideoFrame
 from .msssim import ms_ssim
-from .shard import aggregate_video_metrics, forced_k_frames, shard_gops
+from .shard import aggregate_video_metrics, forced_k_frames, gops, shard_gops
 
 # ---------------------------------------------------------------------------
 # frames
@@ -112,39 +113,40 @@ def synthetic_video(num_frames: int, height: int, width: int, seed: int = 0, cut
 
 
 class EarlyStopping:
-    """utils.py:188-211."""
+    """The convergence test of train_video_Represent.py:79-96 (reference
+    utils.py:188-211): stop once ``patience`` consecutive losses have failed to
+    beat the best loss so far by more than ``min_delta``; the first loss only
+    sets the best."""
 
     def __init__(self, patience=100, min_delta=0.0):
-        self.patience = patience
-        self.min_delta = min_delta
+        self.patience, self.min_delta = patience, min_delta
         self.best_loss = None
         self.counter = 0
 
-    def __call__(self, current_loss):
-        if self.best_loss is None:
-            self.best_loss = current_loss
-            return False
-        if self.best_loss - current_loss > self.min_delta:
-            self.best_loss = current_loss
-            self.counter = 0
-        else:
+    def __call__(self, current_loss) -> bool:
+        stale = self.best_loss is not None and not (self.best_loss - current_loss > self.min_delta)
+        if stale:
             self.counter += 1
-        return self.counter >= self.patience
+            return self.counter >= self.patience
+        first = self.best_loss is None
+        self.best_loss, self.counter = current_loss, 0
+        return (not first) and self.patience <= 0
 
 
 def detect_outliers_mean_diff(values, window_size=10, threshold=3):
-    """utils.py:214-229."""
-    outliers = []
-    for i in range(len(values)):
-        start_idx = max(0, i - window_size)
-        end_idx = min(len(values), i + window_size)
-        local_mean = np.mean(values[start_idx:end_idx])
-        local_std = np.std(values[start_idx:end_idx])
-        if (values[i] - local_mean) > threshold * local_std:
-            outliers.append(i)
-        elif values[i] > local_mean * threshold:
-            outliers.append(i)
-    return outliers
+    """K-frame candidates of train_video_Represent.py:348-353 (reference
+    utils.py:214-229): index i is an outlier when it exceeds the mean of its
+    window [i - window_size, i + window_size) (clipped to the sequence) by more
+    than ``threshold`` population standard deviations of that window, or is
+    more than ``threshold`` times that mean."""
+    v = np.asarray(values, dtype=np.float64)
+    n = len(v)
+    lo = np.maximum(np.arange(n) - window_size, 0)
+    hi = np.minimum(np.arange(n) + window_size, n)
+    stats = np.array([(np.mean(v[a:b]), np.std(v[a:b])) for a, b in zip(lo, hi)]).reshape(n, 2)
+    mean, std = stats[:, 0], stats[:, 1]
+    hit = ((v - mean) > threshold * std) | (v > mean * threshold)
+    return [int(i) for i in np.flatnonzero(hit)]
 
 
 # ---------------------------------------------------------------------------
@@ -242,7 +244,7 @@ def _dist():
 
 
 def detect_k_frames(frame_fn, num_frames: int, rank: int, world: int, loss_type: str, lr: float,
-                    probe_points=5000, scratch_iters=500, probe_iters=100) -> List[int]:
+                    probe_points=5000, scratch_iters=500, probe_iters=100, seed: int = 1) -> List[int]:
     """train_video_Represent.py:318-355 with frames split over ranks: rank r
     probes a contiguous range and recomputes the scratch model of the frame
     before its range (one-frame halo); the normalised loss list is gathered
@@ -252,6 +254,9 @@ def detect_k_frames(frame_fn, num_frames: int, rank: int, world: int, loss_type:
     prev = None
     for i in range(max(lo - 1, 0), hi):
         img = frame_fn(i)
+        # seeded by frame, not by rank: the halo frame's scratch model is the one
+        # its owner trains, and the list does not depend on the world size
+        torch.manual_seed(seed + i)
         k = FrameTrainer(img, i + 1, loss_type, probe_points, probe_points, scratch_iters, lr,
                          isdensity=False, isremoval=False)
         gm, loss_k = k.pre_train()
@@ -296,6 +301,8 @@ def train_video(frame_fn, num_frames: int, k_frames: Sequence[int], args, rank: 
         gmodel, npts = None, args.num_points
         for f in range(start, end):  # 1-based frame numbers
             img = frame_fn(f - 1).to(device)
+            # seeded by frame: a frame's init is the same on any number of ranks
+            torch.manual_seed(int(getattr(args, "seed", 1)) + f)
             if f == start:  # a K-frame: from scratch
                 tr = FrameTrainer(img, f, args.loss_type, args.num_points, args.num_points,
                                   args.iterations, args.lr, args.densification_interval,
@@ -362,8 +369,7 @@ def main(argv=None):
         else:
             dist.init_process_group("gloo")
     if args.seed is not None:
-        torch.manual_seed(int(args.seed) + rank)
-        np.random.seed(int(args.seed) + rank)
+        np.random.seed(int(args.seed))
 
     if args.dataset:
         size = args.width * args.height * 3 // 2
@@ -385,20 +391,29 @@ def main(argv=None):
 
     base = Path(args.root) / args.savdir / args.data_name
     kfile = base / "K_frames.txt"
+    had_kfile = kfile.exists()
     if args.k_frames == "forced":
-        k_frames = [1]
+        k_frames, source = [1], "forced"
     elif args.k_frames not in ("auto",):
-        k_frames = sorted({1} | {int(x) for x in args.k_frames.split(",") if x.strip()})
-    elif kfile.exists():
-        k_frames = [int(x) for x in kfile.read_text().split()]
+        k_frames, source = sorted({1} | {int(x) for x in args.k_frames.split(",") if x.strip()}), "list"
+    elif had_kfile:  # the reference's cache (train_video_Represent.py:312-316)
+        k_frames, source = [int(x) for x in kfile.read_text().split()], "file"
     else:
-        k_frames = detect_k_frames(frame_fn, num_frames, rank, world, args.loss_type, args.lr)
-    # forced K-frames at equal-frame shard boundaries, recorded so
-    # a reference run uses the same GOPs
-    k_frames = sorted(set(k_frames) | set(forced_k_frames(num_frames, world)))
+        k_frames, source = detect_k_frames(frame_fn, num_frames, rank, world, args.loss_type,
+                                           args.lr, seed=int(args.seed)), "detected"
+    # too few GOPs for the ranks: K-frames forced at equal-frame shard
+    # boundaries
+    if len(gops(k_frames, num_frames)) < world:
+        k_frames = sorted(set(k_frames) | set(forced_k_frames(num_frames, world)))
     if rank == 0:
         base.mkdir(parents=True, exist_ok=True)
-        kfile.write_text("".join(f"{k}\n" for k in k_frames))
+        # the GOPs this run trained; K_frames.txt (which the reference reads) is
+        # written only when it did not exist and the list came from detection,
+        # so a reference run on the same directory trains the same GOPs --
+        # never overwritten
+        (base / "K_frames_used.txt").write_text("".join(f"{k}\n" for k in k_frames))
+        if not had_kfile and source == "detected":
+            kfile.write_text("".join(f"{k}\n" for k in k_frames))
 
     t0 = time.time()
     res = train_video(frame_fn, num_frames, k_frames, args, rank, world, device)
@@ -407,8 +422,20 @@ def main(argv=None):
     out_dir.mkdir(parents=True, exist_ok=True)
     mdir = Path(args.root) / args.savdir_m / args.data_name / f"{args.model_name}_{args.iterations}_{args.num_points}"
     mdir.mkdir(parents=True, exist_ok=True)
-    torch.save(res["models"], mdir / (f"gmodels_state_dict_rank{rank}.pth" if world > 1
-                                      else "gmodels_state_dict.pth"))
+    # one gmodels_state_dict.pth keyed frame_<n> (train_video_Represent.py:379,384):
+    # rank 0 gathers every rank's frames
+    models = res["models"]
+    d = _dist()
+    if d is not None:
+        parts = [None] * world if rank == 0 else None
+        d.gather_object(models, parts, dst=0)
+        if rank == 0:
+            models = {}
+            for part in parts:
+                models.update(part)
+    if rank == 0:
+        order = sorted(models, key=lambda k: int(k.split("_")[1]))
+        torch.save({k: models[k] for k in order}, mdir / "gmodels_state_dict.pth")
     with open(out_dir / f"train_rank{rank}.jsonl", "w") as fh:
         for r in res["frames"]:
             fh.write(json.dumps(r) + "\n")

@@ -26,13 +26,14 @@ def _load_init(model, z, prefix="init_"):
 
 
 def test_adan_step_matches_reference_cpu():
-    """gsvc_amd.adan.Adan (foreach restatement) vs the reference's first Adan
-    step, on CPU: same init, same gradients."""
-    from gsvc_amd.adan import Adan
+    """The foreach Adan checker (tests/adan_checker.py, what the fused kernel
+    is held to) vs the reference's first Adan step, on CPU: same init, same
+    gradients."""
+    from adan_checker import ForeachAdan
     z = load_golden(FIX)
     names = ["_xyz", "_cholesky", "_features_dc"]
     params = [torch.nn.Parameter(torch.from_numpy(z["init_" + k].copy())) for k in names]
-    opt = Adan(params, lr=1e-3)
+    opt = ForeachAdan(params, lr=1e-3)
     for p, k in zip(params, names):
         p.grad = torch.from_numpy(z["grad_" + k].copy())
     opt.step()

@@ -26,6 +26,17 @@ from conftest import load_golden
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["band", "wg256"])
+def tile_kernel(request, cuda):
+    """The fused step's tile kernel: two 8-row band waves per tile (production)
+    or the 256-thread workgroup per tile (gsvc_debug_set(8, 1), A/B)."""
+    from gsvc_amd import _lib
+    lib = _lib.load()
+    old = lib.gsvc_debug_set(8, 1 if request.param == "wg256" else 0)
+    yield request.param
+    lib.gsvc_debug_set(8, old)
+
+
 def _model(H, W, n, dev, seed, chol_scale=1.0, **kw):
     from gsvc_amd.frame import make_frame_model
     m = make_frame_model(H, W, n, dev, seed=seed, **kw)
@@ -73,7 +84,7 @@ CASES = [(64, 64, 200, 1.0), (72, 120, 500, 1.0), (1080, 1920, 10000, 1.0),
 
 @pytest.mark.parametrize("H,W,n,chol", CASES)
 @pytest.mark.parametrize("loss_type", ["L2", "L1"])
-def test_fused_step_matches_autograd(cuda, H, W, n, chol, loss_type):
+def test_fused_step_matches_autograd(cuda, tile_kernel, H, W, n, chol, loss_type):
     from gsvc_amd.frame import synthetic_gt
     model = _model(H, W, n, cuda, seed=n + 3, chol_scale=chol, isremoval=True)
     gt = synthetic_gt(H, W, 11, cuda)
@@ -90,7 +101,7 @@ def test_fused_step_matches_autograd(cuda, H, W, n, chol, loss_type):
     _close(g[:, 8:9] * sc, grads["rgb_W"] * sc, "rgb_W")
 
 
-def test_fused_step_overfull_tiles(cuda):
+def test_fused_step_overfull_tiles(cuda, tile_kernel):
     """Tiles with more than 256 entries (the slab overflow rebuild), ids spread
     over the whole range: 1500 splats piled on one spot."""
     from gsvc_amd.frame import synthetic_gt
@@ -111,7 +122,7 @@ def test_fused_step_overfull_tiles(cuda):
     _close(g[:, 5:8] * sc, grads["_features_dc"] * sc, "_features_dc")
 
 
-def test_fused_step_empty_frame(cuda):
+def test_fused_step_empty_frame(cuda, tile_kernel):
     """Every splat degenerate (L = 0): M = 0, the image is the background and
     no gradient flows (rasterize_sum.py:121-129)."""
     from gsvc_amd.frame import synthetic_gt

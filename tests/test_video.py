@@ -137,6 +137,62 @@ def test_video_loop_world2_gops_and_allreduce():
     assert res[0][3][0][0] == 1 and res[1][3][0][0] == 7  # forced K-frame at the shard boundary
 
 
+def _kframe_worker(rank, world, port, q):
+    """detect_k_frames with a stub trainer whose losses depend on the torch RNG
+    state at construction: the K-frame list must not depend on the world size
+    (frames are seeded by index, the halo recomputes its owner's model)."""
+    import torch.distributed as dist
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, REPO)
+    try:
+        import gsvc_amd.video as V
+
+        class ProbeStub:
+            def __init__(self, image, frame_num, loss_type, num_points, max_num_points, iterations,
+                         lr, densification_interval=100, trained_model=None, isdensity=False,
+                         isremoval=True, removal_rate=0.25):
+                self.f, self.parent = frame_num, trained_model
+                self.r = float(torch.rand(1))  # the model init draw
+
+            def pre_train(self):
+                if self.parent is None:  # scratch model
+                    return {"r": self.r}, 0.1 * self.r
+                # the probe from the previous frame's model: poor across a scene cut
+                cut = 5.0 if self.f in (7, 13) else 0.0
+                return {"r": self.r}, 0.2 + 0.1 * self.r + 0.05 * self.parent["r"] + cut
+
+        V.FrameTrainer = ProbeStub
+        ks = V.detect_k_frames(lambda i: torch.zeros(1, 3, 4, 4), 20, rank, world, "L2", 1e-3, seed=3)
+        q.put((rank, ks))
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def test_kframe_detection_independent_of_world_size():
+    import queue
+    import torch.multiprocessing as mp
+    q1 = queue.Queue()
+    _kframe_worker(0, 1, 0, q1)
+    single = q1.get()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_kframe_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert 7 in single and 13 in single
+    for _, ks in res:
+        assert ks == single
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("h,w", [(2, 2), (64, 96), (1080, 1920)])
 def test_i420_kernel_matches_oracle(cuda, oracle, h, w):
@@ -168,7 +224,8 @@ def test_video_driver_end_to_end(cuda, tmp_path):
     # P-frames start from the previous frame's model: they fit better than frame 1
     assert psnr[1] > psnr[0] and psnr[4] > psnr[3]
     base = tmp_path / "result" / "Synthetic"
-    assert (base / "K_frames.txt").read_text().split() == ["1", "4"]
+    assert (base / "K_frames_used.txt").read_text().split() == ["1", "4"]
+    assert not (base / "K_frames.txt").exists()  # an explicit list never writes the cache
     line = json.loads((base / "GaussianVideo_600_300" / "train.txt").read_text().splitlines()[-1])
     assert line["frames"] == 6 and line["avg_psnr"] == pytest.approx(np.mean(psnr))
     models = torch.load(tmp_path / "models" / "Synthetic" / "GaussianVideo_600_300" /

@@ -23,6 +23,8 @@ import os
 from collections import defaultdict
 
 KERNELS = {"raster_sum_fwd_kernel": "rasterize_sum_forward",
+           "train_tile_wave_kernel": "train_tile",
+           "train_tile_band_kernel": "train_tile",
            "raster_sum_bwd_kernel": "rasterize_sum_backward",
            "train_tile_kernel": "train_tile",
            "train_splat_kernel": "train_splat",

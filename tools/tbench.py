@@ -2,7 +2,7 @@
 1920x1080 (BASELINE configs[2]: 50k splats by default), iterations/s.
 Run under ``rocprofv3 --kernel-trace --stats`` for the per-kernel split.
 
-    python tools/tbench.py [--splats 50000] [--iters 100] [--foreach-adan]
+    python tools/tbench.py [--splats 50000] [--iters 100]
 """
 from __future__ import annotations
 
@@ -23,16 +23,18 @@ def main():
     ap.add_argument("--splats", type=int, default=50000)
     ap.add_argument("--iters", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--foreach-adan", action="store_true")
     ap.add_argument("--op-by-op", action="store_true", help="disable the fused training step")
     ap.add_argument("--stamps", action="store_true",
-                    help="also stamp the fused step's tile kernel (knob 5 = 2) and print phases")
+                    help="also stamp the fused step's tile kernel and print phases")
+    ap.add_argument("--tile-kernel", choices=["band", "wg256"], default="band",
+                    help="two 8-row bands per tile (production) or the 256-thread kernel (knob 8 = 1)")
     a = ap.parse_args()
     from gsvc_amd.frame import make_frame_model, synthetic_gt
+    from gsvc_amd import _lib
+    _lib.load().gsvc_debug_set(8, 1 if a.tile_kernel == "wg256" else 0)
     dev = torch.device("cuda:0")
     H, W = 1080, 1920
     model = make_frame_model(H, W, a.splats, dev, seed=7,
-                             fused_adan=False if a.foreach_adan else None,
                              fused_train=False if a.op_by_op else None)
     gt = synthetic_gt(H, W, 8, dev)
     for it in range(1, a.warmup + 1):
@@ -52,7 +54,7 @@ def main():
         ntiles = ((W + 15) // 16) * ((H + 15) // 16)
         st = torch.zeros((ntiles, 8), dtype=torch.int64, device=dev)
         lib.gsvc_debug_set_ptr(ctypes.c_void_p(st.data_ptr()))
-        lib.gsvc_debug_set(5, 2)
+        lib.gsvc_debug_set(5, 2 if a.tile_kernel == "wg256" else 3)
         model.train_iter(gt, a.warmup + a.iters + 1)
         torch.cuda.synchronize()
         lib.gsvc_debug_set(5, 0)
@@ -61,12 +63,15 @@ def main():
         t = t[t[:, 5] > 0]
         t0 = t[:, 0].min()
         q = lambda x: [round(float(np.percentile(x, p)), 2) for p in (0, 10, 50, 90, 100)]  # noqa
-        print(json.dumps(dict(stamps="percentiles 0/10/50/90/100 (us)", tiles=int(len(t)),
-                              start=q(t[:, 0] - t0), staged=q(t[:, 1] - t[:, 0]),
-                              forward=q(t[:, 2] - t[:, 1]), scan=q(t[:, 3] - t[:, 2]),
-                              items=q(t[:, 4] - t[:, 3]), atomics=q(t[:, 5] - t[:, 4]),
-                              life=q(t[:, 5] - t[:, 0]), end=q(t[:, 5] - t0))), flush=True)
-    print(json.dumps(dict(splats=a.splats, fused_adan=model.fused_adan,
+        names = (("staged", "forward", "scan", "items", "atomics") if a.tile_kernel == "wg256" else
+                 ("ordered", "forward", "loss", "backward", "end"))
+        rec = dict(stamps="percentiles 0/10/50/90/100 (us)", kernel=a.tile_kernel,
+                   tiles=int(len(t)), start=q(t[:, 0] - t0))
+        for k, nm in enumerate(names):
+            rec[nm] = q(t[:, k + 1] - t[:, k])
+        rec.update(life=q(t[:, 5] - t[:, 0]), end=q(t[:, 5] - t0))
+        print(json.dumps(rec), flush=True)
+    print(json.dumps(dict(splats=a.splats, tile_kernel=a.tile_kernel,
                           fused_train=model.fused_steps > 0, iters_per_s=round(1 / dt, 1),
                           ms_per_iter=round(1e3 * dt, 4), psnr=round(psnr, 3))), flush=True)
 
