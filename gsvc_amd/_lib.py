@@ -30,6 +30,7 @@ _SIGS = {
     "gsvc_last_error": [],
     "gsvc_debug_set": [_I, _I],
     "gsvc_debug_set_ptr": [_P],
+    "gsvc_stream_sync": [_P],
     "gsvc_timing_enable": [_I, _I, _I],
     "gsvc_timing_collect": [_P, _I, _P],
     "gsvc_timing_enable_channel": [_I, _I, _I, _I],

@@ -39,3 +39,10 @@ extern "C" int gsvc_debug_set(int key, int value) {
 extern "C" void gsvc_debug_set_ptr(void *p) { gsvc::g_debug_ptr = p; }
 
 extern "C" const char *gsvc_last_error(void) { return gsvc::g_last_error; }
+
+extern "C" int gsvc_stream_sync(void *stream) {
+    const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+    if (e != hipSuccess)
+        return gsvc::set_error(GSVC_ERR_HIP, "stream_sync: %s", hipGetErrorString(e));
+    return GSVC_OK;
+}

@@ -327,8 +327,7 @@ class GaussianVideoFrame(nn.Module):
         if bs is None or bs.rgbw_train != int(rgbw_train) or not bs.matches(bound):
             bs = self._bound_step = BoundStep(*bound[:4], rgbw_train, *bound[4:6], self.H, self.W,
                                               self.loss_type, state)
-        losses = bs(gt, hparams, flags)
-        loss = losses[LOSS_KIND[self.loss_type]]
+        bs.launch(gt, hparams, flags)
         # the step ran (keeps StepLR's call-order check quiet; the scheduler may
         # hold the optimizer from before update_optimizer, as in the reference).
         # The scheduler only sets the next iteration's lr, so it steps while the
@@ -337,7 +336,10 @@ class GaussianVideoFrame(nn.Module):
         self.scheduler.optimizer._opt_called = True
         self.fused_steps += 1
         self.scheduler.step()
-        psnr = 10 * math.log10(1.0 / float(losses[0]))
+        mse, l1 = bs.result()  # the reference's PSNR .item(): one stream wait
+        # the loss as a host scalar tensor (callers take .item() / float() of it)
+        loss = torch.tensor(l1 if self.loss_type == "L1" else mse)
+        psnr = 10 * math.log10(1.0 / mse)
         return loss, psnr
 
     def train_iter(self, gt_image, iter):

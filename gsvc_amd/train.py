@@ -94,38 +94,50 @@ class BoundStep:
         numels = [2 * n, 3 * n, 3 * n, n]
         for k, t in enumerate(adan_state):
             self.state[k] = _f32_ptr(t, "adan_state", numels[k // 4]) or None
+        # the storage pointers ``matches`` re-checks (parameters, constants, state)
+        self.ptrs = tuple(None if t is None else t.data_ptr() for t in self.tensors)
         self.hp = (ctypes.c_double * 10)()
         self.fn = L.load().gsvc_train_step_sum
+        self.host = None
+        self.stream = None
 
     def matches(self, tensors) -> bool:
-        # identity, plus the parameters' storage (Module.to / ``p.data = ...``
-        # swap it under the same object)
+        # identity, plus every bound tensor's storage (Module.to, ``p.data = ...``,
+        # ``state[k].data = ...`` or ``set_`` swap it under the same object)
         if tuple(map(id, tensors)) != self.ids:
             return False
-        p = self.p
-        return ((tensors[0].data_ptr() == p[0]) and (tensors[1].data_ptr() == p[1])
-                and (tensors[2].data_ptr() == p[3])
-                and (tensors[3] is None or tensors[3].data_ptr() == p[4]))
+        return all((t is None and q is None) or (t is not None and t.data_ptr() == q)
+                   for t, q in zip(tensors, self.ptrs))
 
-    def __call__(self, gt: Tensor, adan_hparams, adan_flags: int) -> Tensor:
+    def launch(self, gt: Tensor, adan_hparams, adan_flags: int) -> None:
+        """Enqueue one fused step on the current stream.  The step's kernel
+        writes the losses straight into a pinned host buffer (no copy kernel,
+        no device tensor); ``result`` waits for them."""
         if not (gt.is_cuda and gt.dtype is torch.float32 and gt.is_contiguous()
                 and gt.numel() == 3 * self.H * self.W):
             raise RuntimeError("gt must be a contiguous float32 CUDA tensor of 3*H*W elements")
         for k, x in enumerate(adan_hparams):
             self.hp[k] = x
         ws = _workspace(self.dev, self.n, self.H, self.W)
-        loss = torch.empty((2,), dtype=torch.float32, device=self.dev)
+        if self.host is None:
+            self.host = torch.zeros((4,), dtype=torch.float32, pin_memory=True)
+            self.host_np = self.host.numpy()
         p = self.p
+        self.stream = _raw_stream(self.dev.index)
         rc = self.fn(self.n, p[0], p[1], p[2], p[3], p[4], self.rgbw_train, p[5], gt.data_ptr(),
                      self.H, self.W, self.kind, ws.frame, self.state, self.hp, int(adan_flags),
-                     loss.data_ptr(), None, None, ws.buf_ptr, ws.buf.numel(),
-                     _raw_stream(self.dev.index))
+                     self.host.data_ptr(), None, None, ws.buf_ptr, ws.buf.numel(), self.stream)
         if rc != 0:
             ws.dirty = True
             msg = L.load().gsvc_last_error().decode(errors="replace")
             raise RuntimeError(f"gsvc_train_step_sum failed (status {rc}): {msg}")
         ws.frame += 1
-        return loss
+
+    def result(self):
+        """(mean squared error, mean absolute error) of the last launched step:
+        waits for the stream (the reference's PSNR ``.item()``)."""
+        L.call("gsvc_stream_sync", self.stream)
+        return float(self.host_np[0]), float(self.host_np[1])
 
 
 def train_step_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, rgb_w: Optional[Tensor],

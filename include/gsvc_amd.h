@@ -97,6 +97,12 @@ int gsvc_timing_collect_channel(int channel, float *ms, int max_out, int *count)
  * mode 6; returns the previous value.  Not part of the reference interface;
  * results are identical for every value (modes 4/5 are ablations). */
 int gsvc_debug_set(int key, int value);
+
+/* hipStreamSynchronize(stream): the fused training step writes its losses
+ * into caller memory that may be pinned host memory; the caller waits with
+ * this before reading them (the reference's PSNR .item(),
+ * GaussianSplats_Represent.py:196-198).  Not part of the reference. */
+int gsvc_stream_sync(void *stream);
 /* Diagnostic device buffer for timestamp kernel variants (int64 per tile x 4). */
 void gsvc_debug_set_ptr(void *ptr);
 
@@ -277,7 +283,9 @@ int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_tanh,
  *            rasterizer; clamp(0, 1) -- the same image bits as
  *            gsvc_render_frame_sum (render_out [3,H,W], optional);
  *   loss     against gt [3,H,W]; loss[0] <- mean squared error (the PSNR's
- *            MSE), loss[1] <- mean absolute error;
+ *            MSE), loss[1] <- mean absolute error; ``loss`` may be device
+ *            memory or pinned host memory (written by the last kernel; read
+ *            it after gsvc_stream_sync);
  *   backward through clamp, rasterizer, projection (doubled L cross term,
  *            backward2d.cu:39-41) and the activations;
  *   Adan     every element of xyz [N,2], cholesky [N,3], features [N,3] and,
