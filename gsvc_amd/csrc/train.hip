@@ -23,7 +23,7 @@
 //       the step reads gt once;
 //   train_splat_kernel  one lane per splat: projection VJP (the reference's
 //       doubled L cross term), activation VJPs and the Adan update of every
-//       parameter element; an extra last workgroup sums the tiles' errors in
+//       parameter element; an extra first workgroup sums the tiles' errors in
 //       a fixed order into the loss.
 #include "adan.h"
 #include "frame.h"
@@ -820,24 +820,37 @@ struct TrainSplatArgs {
     float *loss;         // [2]: mean squared error, mean absolute error
 };
 
+// The loss workgroup's loads per round: 16 tile pairs per thread in flight, so
+// a 1080p frame (4080 pairs) is one round trip.
+constexpr int kLossBatch = 16;
+
 __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
-    if (blockIdx.x == gridDim.x - 1) {
-        // the last workgroup (no splats): the loss, the tiles' error sums in a
-        // fixed order, in double
+    if (blockIdx.x == 0) {
+        // the first workgroup (no splats): the loss, the tiles' error sums in a
+        // fixed order, in double; dispatched first so it runs beside the splats
         __shared__ double s_l[2][4];
         double s2 = 0.0, s1 = 0.0;
-        for (int t0 = threadIdx.x; t0 < A.ntiles; t0 += 8 * 256) {
-            float2 e[8];
+        const int npair = A.ntiles >> 1;
+        const float4 *e4 = reinterpret_cast<const float4 *>(A.err);
+        for (int t0 = threadIdx.x; t0 < npair; t0 += kLossBatch * 256) {
+            float4 e[kLossBatch];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {  // 8 independent loads in flight
+            for (int k = 0; k < kLossBatch; ++k) {
                 const int t = t0 + 256 * k;
-                e[k] = t < A.ntiles ? A.err[t] : make_float2(0.f, 0.f);
+                e[k] = t < npair ? e4[t] : make_float4(0.f, 0.f, 0.f, 0.f);
             }
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
+            for (int k = 0; k < kLossBatch; ++k) {
                 s2 += (double)e[k].x;
                 s1 += (double)e[k].y;
+                s2 += (double)e[k].z;
+                s1 += (double)e[k].w;
             }
+        }
+        if ((A.ntiles & 1) && threadIdx.x == 0) {
+            const float2 e = A.err[A.ntiles - 1];
+            s2 += (double)e.x;
+            s1 += (double)e.y;
         }
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
@@ -853,21 +866,45 @@ __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
             A.loss[0] = (float)(((s_l[0][0] + s_l[0][1]) + (s_l[0][2] + s_l[0][3])) * A.inv_count);
             A.loss[1] = (float)(((s_l[1][0] + s_l[1][1]) + (s_l[1][2] + s_l[1][3])) * A.inv_count);
         }
+        return;
     }
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
     if (i >= A.n) return;
+    // Every operand is loaded up front, before any arithmetic: one round trip
+    // per lane instead of three (gradient + radius -> record -> Adan state).
+    // rec is written for every splat by the projection, so its load needs no
+    // radius test; a first step's neg_pre_grad is loaded and ignored.
     const float4 g0 = A.grad[4 * i];      // v_xy.x, v_xy.y, v_conic 0, v_conic 1
     const float4 g1 = A.grad[4 * i + 1];  // v_conic 2, v_colors r g b
+    const float4 r0 = A.rec[3 * i], r2 = A.rec[3 * i + 2];
+    const int rad = A.radii[i];
+    const float c0 = A.chol[3 * i], c1 = A.chol[3 * i + 1], c2 = A.chol[3 * i + 2];
+    const float x0 = A.xyz[2 * i], x1 = A.xyz[2 * i + 1];
+    const float f0 = A.feat[3 * i], f1 = A.feat[3 * i + 1], f2 = A.feat[3 * i + 2];
+    const float w = A.rgbw ? A.rgbw[i] : 1.0f;
+    const bool upd = A.update != 0;
+    float m[9], v[9], df[9], npg[9];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+        const int q = e < 2 ? 0 : (e < 5 ? 1 : (e < 8 ? 2 : 3));
+        m[e] = v[e] = df[e] = npg[e] = 0.0f;
+        if (!upd || (q == 3 && !A.rgbw_train)) continue;
+        const size_t j = q == 0 ? 2 * (size_t)i + e : (q == 1 ? 3 * (size_t)i + (e - 2)
+                                                  : (q == 2 ? 3 * (size_t)i + (e - 5) : (size_t)i));
+        m[e] = A.state[q][0][j];
+        v[e] = A.state[q][1][j];
+        df[e] = A.state[q][2][j];
+        npg[e] = A.state[q][3][j];
+    }
     // 2D projection VJP, backward2d.cu:8-51 (the op's project2d_bwd_kernel sequence)
     float vl0 = 0.f, vl1 = 0.f, vl2 = 0.f, vmx = 0.f, vmy = 0.f;
-    float l11 = A.chol[3 * i], l21 = A.chol[3 * i + 1], l22 = A.chol[3 * i + 2];
+    float l11 = c0, l21 = c1, l22 = c2;
     if (A.chol_bound) {
         l11 = l11 + A.chol_bound[0];
         l21 = l21 + A.chol_bound[1];
         l22 = l22 + A.chol_bound[2];
     }
-    if (A.radii[i] > 0) {
-        const float4 r0 = A.rec[3 * i], r2 = A.rec[3 * i + 2];
+    if (rad > 0) {
         const float X00 = r2.z, X01 = r0.w, X10 = X01, X11 = r2.w;
         const float G00 = g0.z, G01 = g0.w, G10 = G01, G11 = g1.x;
         const float N00 = -X00, N01 = -X01, N10 = -X10, N11 = -X11;
@@ -887,14 +924,11 @@ __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
         vmy = g0.y * A.hh;
     }
     // activations (GaussianSplats_Represent.py:57-70): tanh, + bound, * rgb_W
-    const float x0 = A.xyz[2 * i], x1 = A.xyz[2 * i + 1];
     const float t0 = tanhf(x0), t1 = tanhf(x1);
     const float dx0 = vmx * (1.0f - t0 * t0), dx1 = vmy * (1.0f - t1 * t1);
-    const float w = A.rgbw ? A.rgbw[i] : 1.0f;
-    const float f0 = A.feat[3 * i], f1 = A.feat[3 * i + 1], f2 = A.feat[3 * i + 2];
     const float df0 = g1.y * w, df1 = g1.z * w, df2 = g1.w * w;
     const float dw = (g1.y * f0 + g1.z * f1) + g1.w * f2;
-    if (!A.update) {
+    if (!upd) {
         float *o = A.grads_out + 9 * (size_t)i;
         o[0] = dx0;
         o[1] = dx1;
@@ -907,38 +941,19 @@ __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
         o[8] = A.rgbw_train ? dw : 0.0f;
         return;
     }
-    // Adan on the 8 (9 with rgb_W) elements of this splat.  Every operand is
-    // loaded before the first store: the state pointers may alias as far as
-    // the compiler knows, so interleaving would serialise nine round trips.
+    // Adan on the 8 (9 with rgb_W) elements of this splat
     const float g[9] = {dx0, dx1, vl0, vl1, vl2, df0, df1, df2, dw};
-    float pv[9], m[9], v[9], df[9], npg[9];
+    const float pin[9] = {x0, x1, c0, c1, c2, f0, f1, f2, w};
 #pragma unroll
     for (int e = 0; e < 9; ++e) {
         const int q = e < 2 ? 0 : (e < 5 ? 1 : (e < 8 ? 2 : 3));
         if (q == 3 && !A.rgbw_train) continue;
+        if (A.first[q]) npg[e] = -(g[e] * A.S.clip);
+        const float pv = adan_update(A.S, pin[e], g[e], m[e], v[e], df[e], npg[e]);
         const size_t j = q == 0 ? 2 * (size_t)i + e : (q == 1 ? 3 * (size_t)i + (e - 2)
                                                   : (q == 2 ? 3 * (size_t)i + (e - 5) : (size_t)i));
         float *param = q == 0 ? A.xyz : (q == 1 ? A.chol : (q == 2 ? A.feat : A.rgbw));
-        pv[e] = param[j];
-        m[e] = A.state[q][0][j];
-        v[e] = A.state[q][1][j];
-        df[e] = A.state[q][2][j];
-        npg[e] = A.first[q] ? -(g[e] * A.S.clip) : A.state[q][3][j];
-    }
-#pragma unroll
-    for (int e = 0; e < 9; ++e) {
-        const int q = e < 2 ? 0 : (e < 5 ? 1 : (e < 8 ? 2 : 3));
-        if (q == 3 && !A.rgbw_train) continue;
-        pv[e] = adan_update(A.S, pv[e], g[e], m[e], v[e], df[e], npg[e]);
-    }
-#pragma unroll
-    for (int e = 0; e < 9; ++e) {
-        const int q = e < 2 ? 0 : (e < 5 ? 1 : (e < 8 ? 2 : 3));
-        if (q == 3 && !A.rgbw_train) continue;
-        const size_t j = q == 0 ? 2 * (size_t)i + e : (q == 1 ? 3 * (size_t)i + (e - 2)
-                                                  : (q == 2 ? 3 * (size_t)i + (e - 5) : (size_t)i));
-        float *param = q == 0 ? A.xyz : (q == 1 ? A.chol : (q == 2 ? A.feat : A.rgbw));
-        param[j] = pv[e];
+        param[j] = pv;
         A.state[q][0][j] = m[e];
         A.state[q][1][j] = v[e];
         A.state[q][2][j] = df[e];
@@ -1077,7 +1092,7 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     P.grads_out = grads_out;
     P.err = w.err;
     P.loss = loss;
-    // one extra (last) workgroup sums the loss, off the splat workgroups' path
+    // one extra (first) workgroup sums the loss, beside the splat workgroups
     const int blocks = (num_points > 0 ? ceil_div(num_points, 256) : 0) + 1;
     hipEvent_t tev[2];
     const int tslot = timing_begin(s, tev, kTimingTrainSplat);

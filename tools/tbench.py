@@ -28,10 +28,17 @@ def main():
                     help="also stamp the fused step's tile kernel and print phases")
     ap.add_argument("--tile-kernel", choices=["band", "wg256"], default="band",
                     help="two 8-row bands per tile (production) or the 256-thread kernel (knob 8 = 1)")
+    ap.add_argument("--knob", action="append", default=[],
+                    help="A/B knob K=V (gsvc_debug_set), repeatable")
+    ap.add_argument("--channels", action="store_true",
+                    help="also print HIP-event kernel averages (us) over 200 extra iterations")
     a = ap.parse_args()
     from gsvc_amd.frame import make_frame_model, synthetic_gt
     from gsvc_amd import _lib
     _lib.load().gsvc_debug_set(8, 1 if a.tile_kernel == "wg256" else 0)
+    for kv in a.knob:
+        k, v = kv.split("=")
+        _lib.load().gsvc_debug_set(int(k), int(v))
     dev = torch.device("cuda:0")
     H, W = 1080, 1920
     model = make_frame_model(H, W, a.splats, dev, seed=7,
@@ -46,6 +53,19 @@ def main():
         _, psnr = model.train_iter(gt, it)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.iters
+    chan = {}
+    if a.channels:
+        from gsvc_amd import ops
+        names = ["project", "train_tile", "train_splat"]
+        for c in names:
+            ops.channel_timing(c, True, max_launches=200, every=1, dispatch=True)
+        for it in range(200):
+            model.train_iter(gt, a.warmup + a.iters + 1 + it)
+        torch.cuda.synchronize()
+        for c in names:
+            ts = ops.channel_times_ms(c, 200)
+            chan[c] = round(1e3 * sum(ts) / max(len(ts), 1), 2)
+            ops.channel_timing(c, False)
     if a.stamps:
         import ctypes
         import numpy as np
@@ -73,7 +93,8 @@ def main():
         print(json.dumps(rec), flush=True)
     print(json.dumps(dict(splats=a.splats, tile_kernel=a.tile_kernel,
                           fused_train=model.fused_steps > 0, iters_per_s=round(1 / dt, 1),
-                          ms_per_iter=round(1e3 * dt, 4), psnr=round(psnr, 3))), flush=True)
+                          ms_per_iter=round(1e3 * dt, 4), psnr=round(psnr, 3),
+                          knobs=a.knob, kernel_us=chan)), flush=True)
 
 
 if __name__ == "__main__":
