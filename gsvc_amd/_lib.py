@@ -31,6 +31,9 @@ _SIGS = {
     "gsvc_debug_set": [_I, _I],
     "gsvc_debug_set_ptr": [_P],
     "gsvc_stream_sync": [_P],
+    "gsvc_host_alloc": [_SZ],
+    "gsvc_host_free": [_P],
+    "gsvc_wait_host_seq": [_P, _U, _P, _I],
     "gsvc_timing_enable": [_I, _I, _I],
     "gsvc_timing_collect": [_P, _I, _P],
     "gsvc_timing_enable_channel": [_I, _I, _I, _I],
@@ -59,6 +62,7 @@ _SIGS = {
     "gsvc_render_frame_sum": [_I, _P, _I, _P, _P, _P, _P, _P, _P, _U, _U, _I, _I, _P, _P, _SZ, _P,
                               _P],
     "gsvc_train_step_workspace_bytes": [_I, _U, _U],
+    "gsvc_train_step_sum_args": [_P],
     "gsvc_train_step_sum": [_I, _P, _P, _P, _P, _P, _I, _P, _P, _U, _U, _I, _I, _P, _P, _I, _P, _P,
                             _P, _P, _SZ, _P],
     "gsvc_i420_to_rgb": [_P, _I, _I, _P, _P],
@@ -82,6 +86,7 @@ _SIGS = {
 }
 _RESTYPE = {
     "gsvc_debug_set_ptr": None,
+    "gsvc_host_alloc": _P,
     "gsvc_last_error": ctypes.c_char_p,
     "gsvc_cumsum_workspace_bytes": _SZ,
     "gsvc_prune_workspace_bytes": _SZ,

@@ -1,6 +1,11 @@
 // Error reporting of the C ABI: a per-thread message for gsvc_last_error().
+#include <immintrin.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <string.h>
+
+#include <atomic>
+#include <chrono>
 
 #include "common.h"
 
@@ -44,5 +49,47 @@ extern "C" int gsvc_stream_sync(void *stream) {
     const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
     if (e != hipSuccess)
         return gsvc::set_error(GSVC_ERR_HIP, "stream_sync: %s", hipGetErrorString(e));
+    return GSVC_OK;
+}
+
+extern "C" void *gsvc_host_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocCoherent) != hipSuccess) {
+        gsvc::set_error(GSVC_ERR_HIP, "host_alloc: hipHostMalloc(%zu) failed", bytes);
+        return nullptr;
+    }
+    memset(p, 0, bytes);
+    return p;
+}
+
+extern "C" int gsvc_host_free(void *p) {
+    if (p && hipHostFree(p) != hipSuccess) return gsvc::set_error(GSVC_ERR_HIP, "host_free failed");
+    return GSVC_OK;
+}
+
+// Spin on a word of coherent host memory until a kernel has stored ``seq``
+// into it (system-scope release: everything the kernel stored before it is
+// visible).  After ``spin_us`` without it, wait for the whole stream instead,
+// which also reports a failed kernel; the word must then hold ``seq``.
+extern "C" int gsvc_wait_host_seq(const unsigned *word, unsigned seq, void *stream, int spin_us) {
+    if (!word) return gsvc::set_error(GSVC_ERR_ARG, "wait_host_seq: null word");
+    const volatile unsigned *w = word;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 1;; ++it) {
+        if (*w == seq) {
+            std::atomic_thread_fence(std::memory_order_acquire);
+            return GSVC_OK;
+        }
+        _mm_pause();
+        if ((it & 255u) == 0 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us))
+            break;
+    }
+    const int rc = gsvc_stream_sync(stream);
+    if (rc) return rc;
+    if (*w != seq)
+        return gsvc::set_error(GSVC_ERR_HIP, "wait_host_seq: the stream finished without storing %u (word %u)",
+                               seq, *w);
+    std::atomic_thread_fence(std::memory_order_acquire);
     return GSVC_OK;
 }

@@ -36,7 +36,7 @@ constexpr int kT = kTilePix;  // threads = pixels = entries of one tile
 struct TrainTileArgs {
     int tbx, img_w, img_h, ntiles, num_points, loss_l1;
     float norm;  // d loss / d pixel scale: float(2 / numel) for L2, 1.0f / numel for L1
-    const float4 *slab;
+    float4 *slab;  // read; a brute tile parks its sorted ids in its own slab
     const unsigned *counts;
     unsigned *counts_clear;
     const int *m_dev;
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(256, 8) void train_tile_kernel(TrainTileArgs A) {
 // GSVC's opacity is ones (GaussianSplats_Represent.py:84) and the training
 // step projects with opacity 1, so the opacity gradient (record slot 8) is
 // not formed.
-constexpr int kBSpec = 32;    // slab slots loaded with the count
+constexpr int kBSpec = 32;    // slab slots loaded with the count (64: slower, measured)
 constexpr int kBChunk = 64;   // entries staged at a time
 constexpr int kBRun = 8;      // pixels per backward work item (part of one rectangle row)
 constexpr int kBThreads = 128;
@@ -473,6 +473,33 @@ __device__ __forceinline__ int wave_scan_dpp(int v, int id) {
     step(__builtin_amdgcn_update_dpp(id, v, 0x142, 0xa, 0xf, false));  // row_bcast:15 -> rows 1, 3
     step(__builtin_amdgcn_update_dpp(id, v, 0x143, 0xc, 0xf, false));  // row_bcast:31 -> rows 2, 3
     return v;
+}
+
+// One step of a segmented inclusive sum: lanes whose DPP source lane carries
+// the same key add its 8 sums (sources outside the row / masked rows: key -1).
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void seg_step8(float (&g)[8], int key) {
+    const int ks = __builtin_amdgcn_update_dpp(-1, key, kCtrl, kRowMask, 0xf, false);
+    const bool same = ks == key;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const float t = __int_as_float(
+            __builtin_amdgcn_update_dpp(0, __float_as_int(g[c]), kCtrl, kRowMask, 0xf, false));
+        g[c] = same ? g[c] + t : g[c];
+    }
+}
+
+// Segmented inclusive sums over one wave's 64 lanes, segments = runs of equal
+// key >= 0 (contiguous): lane i ends with the sum of its run's lanes <= i.
+// The wave_scan_dpp steps; a source lane is added only inside the run, so
+// each lane's sum covers exactly [max(run start, ...), i].
+__device__ __forceinline__ void wave_seg_sums(float (&g)[8], int key) {
+    seg_step8<0x111, 0xf>(g, key);  // row_shr:1
+    seg_step8<0x112, 0xf>(g, key);  // row_shr:2
+    seg_step8<0x114, 0xf>(g, key);  // row_shr:4
+    seg_step8<0x118, 0xf>(g, key);  // row_shr:8
+    seg_step8<0x142, 0xa>(g, key);  // row_bcast:15 -> rows 1, 3
+    seg_step8<0x143, 0xc>(g, key);  // row_bcast:31 -> rows 2, 3
 }
 
 struct BandLds {
@@ -604,24 +631,33 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             keep = rc != kNoRect && (int)((rc >> 12) & 15u) >= y_lo && (int)((rc >> 8) & 15u) <= y_hi;
         }
         unsigned long long m = __ballot(keep);
-        while (m) {
-            const int k = __builtin_ctzll(m);
-            m &= m - 1ull;
-            const float4 G = S.geo[k];
-            const float4 C = S.col[k];
-            const float dy = G.y - py;
-            const float cq = (C.x * dy) * dy;
-            const float bdy = G.w * dy;
-            blend2_unit(G.x, G.z, bdy, cq, C.y, C.z, C.w, px, ar, ag, ab);
+        if (m) {
+            do {
+                const int k = __builtin_ctzll(m);
+                m &= m - 1ull;
+                const float4 G = S.geo[k];
+                const float4 C = S.col[k];
+                const float dy = G.y - py;
+                const float cq = (C.x * dy) * dy;
+                const float bdy = G.w * dy;
+                blend2_unit(G.x, G.z, bdy, cq, C.y, C.z, C.w, px, ar, ag, ab);
+            } while (m);
         }
         if (dense) __syncthreads();  // the next chunk overwrites the staging
     }
-    // dense: the keys of ranks tid and tid + 128, kept in registers (the
-    // backward's partials overwrite s_key)
-    int kr0 = 0, kr1 = 0;
+    // dense: the keys of ranks tid and tid + 128, kept for the backward (its
+    // partials overwrite s_key)
+    // (slab slots < 256: two 16-bit halves of one register); a brute tile's
+    // keys are splat ids, parked in its own slab (whose records it never reads)
+    unsigned krp = 0u;
+    int *kpark = reinterpret_cast<int *>(slab_rec(A.slab, A.ntiles, tile, kHeadSlots));  // 248 slots, contiguous
     if (dense) {
-        kr0 = tid < n ? s_key[tid] : 0;
-        kr1 = tid + kBThreads < n ? s_key[tid + kBThreads] : 0;
+        if (!brute) {
+            krp = (unsigned)(tid < n ? s_key[tid] : 0) |
+                  ((unsigned)(tid + kBThreads < n ? s_key[tid + kBThreads] : 0) << 16);
+        } else {
+            for (int j = tid; j < n; j += kBThreads) kpark[j] = s_key[j];
+        }
     }
     if (kStamp && tid == 0) st[2] = tstamp();
 
@@ -680,8 +716,13 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
         if (dense) {
             __syncthreads();  // misc / staging / partial readers done
             // this chunk's keys, by rank, into the gid slots stage_chunk overwrites
-            if (tid >= c0 && tid < c0 + gn) S.gid[tid - c0] = kr0;
-            if (tid + kBThreads >= c0 && tid + kBThreads < c0 + gn) S.gid[tid + kBThreads - c0] = kr1;
+            if (!brute) {
+                if (tid >= c0 && tid < c0 + gn) S.gid[tid - c0] = (int)(krp & 0xffffu);
+                if (tid + kBThreads >= c0 && tid + kBThreads < c0 + gn)
+                    S.gid[tid + kBThreads - c0] = (int)(krp >> 16);
+            } else if (tid < gn) {
+                S.gid[tid] = kpark[c0 + tid];  // written by this workgroup before the forward's end
+            }
             __syncthreads();
             stage_chunk(S.gid, gn);
             __syncthreads();
@@ -773,15 +814,22 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                     }
                 }
             }
+            // per wave, segmented sums over the runs of items of one entry: the
+            // last item of an entry's run holds the run's sum (fixed tree order)
+            wave_seg_sums(g, own);
 #pragma unroll
             for (int c = 0; c < 8; ++c) S.part[c][tid] = g[c];
             __syncthreads();
-            // each entry adds its items of this round in item order
+            // each entry adds its (at most two: one per wave) run sums of this round
             if (w == 0 && items > 0) {
-                const int i0 = max(off, base), i1 = min(off + items, base + kBThreads);
-                for (int it = i0; it < i1; ++it) {
+                const int i0 = max(off, base) - base, i1 = min(off + items, base + kBThreads) - base;
+                if (i0 < i1) {
+                    if (i0 < 64 && i1 > 64) {
 #pragma unroll
-                    for (int c = 0; c < 8; ++c) acc[c] += S.part[c][it - base];
+                        for (int c = 0; c < 8; ++c) acc[c] += S.part[c][63];
+                    }
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) acc[c] += S.part[c][i1 - 1];
                 }
             }
             __syncthreads();  // partials read before the next round rewrites them
@@ -818,6 +866,7 @@ struct TrainSplatArgs {
     float *grads_out;    // update == 0: [N, 9] = d_xyz 2, d_chol 3, d_feat 3, d_rgbw 1
     const float2 *err;
     float *loss;         // [2]: mean squared error, mean absolute error
+    unsigned loss_seq;   // non-zero: stored into word 2 of ``loss`` after the losses
 };
 
 // The loss workgroup's loads per round: 16 tile pairs per thread in flight, so
@@ -865,6 +914,12 @@ __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
         if (threadIdx.x == 0) {
             A.loss[0] = (float)(((s_l[0][0] + s_l[0][1]) + (s_l[0][2] + s_l[0][3])) * A.inv_count);
             A.loss[1] = (float)(((s_l[1][0] + s_l[1][1]) + (s_l[1][2] + s_l[1][3])) * A.inv_count);
+            // coherent host memory: the host stops waiting here, while the
+            // splat workgroups still run (later work on the stream is ordered
+            // after them anyway)
+            if (A.loss_seq)
+                __hip_atomic_store(reinterpret_cast<unsigned *>(A.loss) + 2, A.loss_seq,
+                                   __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         return;
     }
@@ -1092,6 +1147,9 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     P.grads_out = grads_out;
     P.err = w.err;
     P.loss = loss;
+    // GSVC_TRAIN_LOSS_SEQ: ``loss`` is coherent host memory of 3 words; word 2
+    // receives the call's sequence number (frame_index + 1, never 0)
+    P.loss_seq = (adan_flags & GSVC_TRAIN_LOSS_SEQ) ? ((unsigned)frame_index + 1u) | 0x80000000u : 0u;
     // one extra (first) workgroup sums the loss, beside the splat workgroups
     const int blocks = (num_points > 0 ? ceil_div(num_points, 256) : 0) + 1;
     hipEvent_t tev[2];
@@ -1099,4 +1157,13 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     launch_timed(train_splat_kernel, dim3(blocks), dim3(256), 0, s, tev, P);
     timing_end(s, tslot, kTimingTrainSplat);
     return check_launch("train_step_sum: splats");
+}
+
+extern "C" int gsvc_train_step_sum_args(const gsvc_train_step_args *a) {
+    if (!a) return set_error(GSVC_ERR_ARG, "train_step_sum_args: null");
+    return gsvc_train_step_sum(a->num_points, a->xyz, a->cholesky, a->cholesky_bound, a->features,
+                               a->rgb_w, a->rgb_w_trainable, a->background, a->gt, a->img_height,
+                               a->img_width, a->loss_kind, a->frame_index, a->adan_state,
+                               a->adan_hparams, a->adan_flags, a->loss, a->render_out,
+                               a->grads_out, a->workspace, a->workspace_bytes, a->stream);
 }

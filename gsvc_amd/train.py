@@ -21,6 +21,7 @@ from torch import Tensor
 from . import _lib as L
 
 LOSS_KIND = {"L2": 0, "L1": 1}
+TRAIN_LOSS_SEQ = 0x100  # include/gsvc_amd.h GSVC_TRAIN_LOSS_SEQ
 
 
 class _TrainWorkspace:
@@ -71,11 +72,27 @@ def _f32_ptr(t: Optional[Tensor], name: str, numel: int) -> int:
     return t.data_ptr()
 
 
+class _StepArgs(ctypes.Structure):
+    """include/gsvc_amd.h gsvc_train_step_args."""
+    _fields_ = [("num_points", ctypes.c_int), ("xyz", ctypes.c_void_p),
+                ("cholesky", ctypes.c_void_p), ("cholesky_bound", ctypes.c_void_p),
+                ("features", ctypes.c_void_p), ("rgb_w", ctypes.c_void_p),
+                ("rgb_w_trainable", ctypes.c_int), ("background", ctypes.c_void_p),
+                ("gt", ctypes.c_void_p), ("img_height", ctypes.c_uint), ("img_width", ctypes.c_uint),
+                ("loss_kind", ctypes.c_int), ("frame_index", ctypes.c_int),
+                ("adan_state", ctypes.c_void_p), ("adan_hparams", ctypes.c_void_p),
+                ("adan_flags", ctypes.c_int), ("loss", ctypes.c_void_p),
+                ("render_out", ctypes.c_void_p), ("grads_out", ctypes.c_void_p),
+                ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_size_t),
+                ("stream", ctypes.c_void_p)]
+
+
 class BoundStep:
     """A fused training step bound to fixed tensors (parameters, Adan state,
-    constants): pointers and the ctypes state array are built once, so a call
-    costs one C call plus the loss tensor.  The owner rebuilds it when any
-    bound tensor object changes (``matches``).  Parameters are updated in place
+    constants): the C argument struct is built once and a call updates only
+    the target, frame, flags, hyper-parameters and stream, so a step costs
+    one single-pointer C call.  The owner rebuilds it when any bound tensor
+    object or storage changes (``matches``).  Parameters are updated in place
     through their storage (as ``p.data`` would be)."""
 
     def __init__(self, xyz, cholesky, features, rgb_w, rgb_w_trainable, cholesky_bound,
@@ -85,59 +102,92 @@ class BoundStep:
         self.ids = tuple(map(id, self.tensors))  # the objects stay alive via self.tensors
         self.n, self.H, self.W = n, int(H), int(W)
         self.dev = xyz.device
-        self.kind = LOSS_KIND[loss_type]
         self.rgbw_train = 1 if rgb_w_trainable else 0
-        self.p = [_f32_ptr(xyz, "xyz", 2 * n), _f32_ptr(cholesky, "cholesky", 3 * n),
-                  _f32_ptr(cholesky_bound, "cholesky_bound", 3), _f32_ptr(features, "features", 3 * n),
-                  _f32_ptr(rgb_w, "rgb_w", n), _f32_ptr(background, "background", 3)]
         self.state = (ctypes.c_void_p * 16)()
         numels = [2 * n, 3 * n, 3 * n, n]
         for k, t in enumerate(adan_state):
             self.state[k] = _f32_ptr(t, "adan_state", numels[k // 4]) or None
         # the storage pointers ``matches`` re-checks (parameters, constants, state)
-        self.ptrs = tuple(None if t is None else t.data_ptr() for t in self.tensors)
+        self.live = [k for k, t in enumerate(self.tensors) if t is not None]
+        self.ptrs = [self.tensors[k].data_ptr() for k in self.live]
         self.hp = (ctypes.c_double * 10)()
-        self.fn = L.load().gsvc_train_step_sum
-        self.host = None
+        a = self.args = _StepArgs()
+        a.num_points = n
+        a.xyz = _f32_ptr(xyz, "xyz", 2 * n)
+        a.cholesky = _f32_ptr(cholesky, "cholesky", 3 * n)
+        a.cholesky_bound = _f32_ptr(cholesky_bound, "cholesky_bound", 3)
+        a.features = _f32_ptr(features, "features", 3 * n)
+        a.rgb_w = _f32_ptr(rgb_w, "rgb_w", n)
+        a.rgb_w_trainable = self.rgbw_train
+        a.background = _f32_ptr(background, "background", 3)
+        a.img_height, a.img_width = self.H, self.W
+        a.loss_kind = LOSS_KIND[loss_type]
+        a.adan_state = ctypes.addressof(self.state)
+        a.adan_hparams = ctypes.addressof(self.hp)
+        self.args_ref = ctypes.byref(a)
+        self.fn = L.load().gsvc_train_step_sum_args
+        self.host = None  # coherent host words: mse, l1, sequence
+        self.seq = 0
         self.stream = None
+
+    def __del__(self):
+        if getattr(self, "host", None) is not None:
+            try:
+                L.load().gsvc_host_free(self.host)
+            except Exception:  # interpreter shutdown
+                pass
+            self.host = None
 
     def matches(self, tensors) -> bool:
         # identity, plus every bound tensor's storage (Module.to, ``p.data = ...``,
         # ``state[k].data = ...`` or ``set_`` swap it under the same object)
         if tuple(map(id, tensors)) != self.ids:
             return False
-        return all((t is None and q is None) or (t is not None and t.data_ptr() == q)
-                   for t, q in zip(tensors, self.ptrs))
+        return [tensors[k].data_ptr() for k in self.live] == self.ptrs
 
     def launch(self, gt: Tensor, adan_hparams, adan_flags: int) -> None:
-        """Enqueue one fused step on the current stream.  The step's kernel
-        writes the losses straight into a pinned host buffer (no copy kernel,
-        no device tensor); ``result`` waits for them."""
+        """Enqueue one fused step on the current stream.  The step's last
+        kernel stores the losses straight into coherent host memory, then a
+        sequence word (GSVC_TRAIN_LOSS_SEQ); ``result`` waits for that word
+        only, so the host goes on while the parameter update still runs --
+        everything later on the stream is ordered after it, as for any
+        asynchronous torch op."""
         if not (gt.is_cuda and gt.dtype is torch.float32 and gt.is_contiguous()
                 and gt.numel() == 3 * self.H * self.W):
             raise RuntimeError("gt must be a contiguous float32 CUDA tensor of 3*H*W elements")
+        hp = self.hp
         for k, x in enumerate(adan_hparams):
-            self.hp[k] = x
+            hp[k] = x
         ws = _workspace(self.dev, self.n, self.H, self.W)
+        lib = L.load()
+        a = self.args
         if self.host is None:
-            self.host = torch.zeros((4,), dtype=torch.float32, pin_memory=True)
-            self.host_np = self.host.numpy()
-        p = self.p
+            self.host = lib.gsvc_host_alloc(16)
+            if not self.host:
+                raise RuntimeError(lib.gsvc_last_error().decode(errors="replace"))
+            self.host_f = (ctypes.c_float * 4).from_address(self.host)
+            a.loss = self.host
         self.stream = _raw_stream(self.dev.index)
-        rc = self.fn(self.n, p[0], p[1], p[2], p[3], p[4], self.rgbw_train, p[5], gt.data_ptr(),
-                     self.H, self.W, self.kind, ws.frame, self.state, self.hp, int(adan_flags),
-                     self.host.data_ptr(), None, None, ws.buf_ptr, ws.buf.numel(), self.stream)
+        self.seq = ((ws.frame + 1) & 0xFFFFFFFF) | 0x80000000
+        a.gt = gt.data_ptr()
+        a.frame_index = ws.frame
+        a.adan_flags = int(adan_flags) | TRAIN_LOSS_SEQ
+        a.workspace = ws.buf_ptr
+        a.workspace_bytes = ws.buf.numel()
+        a.stream = self.stream
+        rc = self.fn(self.args_ref)
         if rc != 0:
             ws.dirty = True
-            msg = L.load().gsvc_last_error().decode(errors="replace")
+            msg = lib.gsvc_last_error().decode(errors="replace")
             raise RuntimeError(f"gsvc_train_step_sum failed (status {rc}): {msg}")
         ws.frame += 1
 
     def result(self):
         """(mean squared error, mean absolute error) of the last launched step:
-        waits for the stream (the reference's PSNR ``.item()``)."""
-        L.call("gsvc_stream_sync", self.stream)
-        return float(self.host_np[0]), float(self.host_np[1])
+        waits for its sequence word (the reference's PSNR ``.item()``); after
+        50 ms of spinning, for the whole stream, which reports a failed kernel."""
+        L.call("gsvc_wait_host_seq", self.host + 8, self.seq, self.stream, 50000)
+        return self.host_f[0], self.host_f[1]
 
 
 def train_step_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, rgb_w: Optional[Tensor],

@@ -103,6 +103,16 @@ int gsvc_debug_set(int key, int value);
  * this before reading them (the reference's PSNR .item(),
  * GaussianSplats_Represent.py:196-198).  Not part of the reference. */
 int gsvc_stream_sync(void *stream);
+/* Coherent pinned host memory (hipHostMallocCoherent), zeroed: a kernel's
+ * system-scope stores to it are seen by the host while the kernel runs.
+ * Not part of the reference. */
+void *gsvc_host_alloc(size_t bytes);
+int gsvc_host_free(void *p);
+/* Spin until the unsigned at ``word`` (coherent host memory) equals ``seq``;
+ * after spin_us microseconds fall back to gsvc_stream_sync(stream), which
+ * reports a failed kernel, and then require it.  The fused training step's
+ * early loss read-back (GSVC_TRAIN_LOSS_SEQ).  Not part of the reference. */
+int gsvc_wait_host_seq(const unsigned *word, unsigned seq, void *stream, int spin_us);
 /* Diagnostic device buffer for timestamp kernel variants (int64 per tile x 4). */
 void gsvc_debug_set_ptr(void *ptr);
 
@@ -296,12 +306,18 @@ int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_tanh,
  * double[10] = {beta1, beta2, beta3, bias_correction1, bias_correction2,
  * sqrt(bias_correction3), lr, weight_decay, eps, clip_global_grad_norm}.
  * adan_flags: bit 0 no_prox; bit 1 + q: parameter q takes its first step
- * (neg_pre_grad starts from -grad, optimizer.py:187-189).
+ * (neg_pre_grad starts from -grad, optimizer.py:187-189); GSVC_TRAIN_LOSS_SEQ:
+ * ``loss`` is coherent host memory (gsvc_host_alloc) of at least 3 words and,
+ * once loss[0..1] are stored, word 2 receives (frame_index + 1) | 0x80000000
+ * with a system-scope release -- the host may read the losses then
+ * (gsvc_wait_host_seq) while the rest of the step still runs; every later
+ * operation on ``stream`` sees the updated parameters.
  * grads_out (test hook): when non-NULL nothing is updated and the parameter
  * gradients go to grads_out [N,9] = {d_xyz 2, d_cholesky 3, d_features 3,
  * d_rgb_w 1}.  Workspace: gsvc_train_step_workspace_bytes; its first
  * gsvc_render_frame_zeroed_bytes(H, W) bytes zero before the first call (every
  * call leaves them zero); frame_index alternates parity between calls. */
+#define GSVC_TRAIN_LOSS_SEQ 0x100
 size_t gsvc_train_step_workspace_bytes(int num_points, unsigned img_height,
                                        unsigned img_width);
 int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
@@ -312,6 +328,28 @@ int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
                         const double *adan_hparams, int adan_flags, float *loss,
                         float *render_out, float *grads_out, void *workspace,
                         size_t workspace_bytes, void *stream);
+/* gsvc_train_step_sum with its arguments in one struct (the same names and
+ * meaning): a binding that keeps the struct across calls and updates only
+ * what changes pays one argument conversion per step.  Not part of the
+ * reference. */
+typedef struct gsvc_train_step_args {
+    int num_points;
+    float *xyz, *cholesky;
+    const float *cholesky_bound;
+    float *features, *rgb_w;
+    int rgb_w_trainable;
+    const float *background, *gt;
+    unsigned img_height, img_width;
+    int loss_kind, frame_index;
+    float *const *adan_state;
+    const double *adan_hparams;
+    int adan_flags;
+    float *loss, *render_out, *grads_out;
+    void *workspace;
+    size_t workspace_bytes;
+    void *stream;
+} gsvc_train_step_args;
+int gsvc_train_step_sum_args(const gsvc_train_step_args *args);
 
 /* The same render for a batch of ``frames`` frame models of one video (a
  * decoder's GOP: frame k of GSVC's gmodels_state_dict is its own model), one

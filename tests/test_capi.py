@@ -103,3 +103,35 @@ def test_dropin_package_surface():
         C.nd_rasterize_sum_forward  # noqa: B018  (not exported by the reference either)
     with pytest.raises(NotImplementedError):
         gsplat.project_gaussians()
+
+
+def test_train_step_args_struct_layout(tmp_path):
+    """gsvc_amd.train._StepArgs mirrors include/gsvc_amd.h gsvc_train_step_args
+    field by field (offsets from the C compiler)."""
+    import shutil
+    import subprocess
+    from gsvc_amd.train import _StepArgs
+    if shutil.which("gcc") is None:
+        pytest.skip("no C compiler")
+    names = [f[0] for f in _StepArgs._fields_]
+    body = "".join(f'printf("%zu ", offsetof(gsvc_train_step_args, {n}));' for n in names)
+    src = tmp_path / "off.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "%s"\nint main(void){%s'
+                   'printf("%%zu\\n", sizeof(gsvc_train_step_args));return 0;}\n' % (HEADER, body))
+    exe = tmp_path / "off"
+    subprocess.run(["gcc", str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True,
+                                          text=True).stdout.split()]
+    assert got[:-1] == [getattr(_StepArgs, n).offset for n in names]
+    assert got[-1] == ctypes.sizeof(_StepArgs)
+
+
+def test_host_seq_wait_without_gpu_work():
+    """gsvc_wait_host_seq returns at once when the word already holds the
+    sequence (coherent host memory needs a HIP runtime; skip without one)."""
+    from gsvc_amd import _lib
+    lib = _lib.load()
+    rc = lib.gsvc_wait_host_seq(None, 1, None, 10)
+    assert rc != 0 and b"null" in lib.gsvc_last_error()
+    buf = (ctypes.c_uint * 4)(0, 0, 0x80000005, 0)
+    assert lib.gsvc_wait_host_seq(ctypes.addressof(buf) + 8, 0x80000005, None, 10) == 0

@@ -35,30 +35,40 @@ def main():
         m.train_iter(gt, it)
     torch.cuda.synchronize()
     # instrument BoundStep.launch / result
-    acc = dict(launch=0.0, result=0.0)
+    acc = dict(launch=0.0, result=0.0, pre=0.0, mid=0.0, post=0.0)
     orig_l, orig_r = T.BoundStep.launch, T.BoundStep.result
+    mark = {}
 
     def launch(self, *x):
         t = time.perf_counter()
+        acc["pre"] += t - mark["start"]
         orig_l(self, *x)
-        acc["launch"] += time.perf_counter() - t
+        mark["launched"] = time.perf_counter()
+        acc["launch"] += mark["launched"] - t
 
     def result(self):
         t = time.perf_counter()
+        acc["mid"] += t - mark["launched"]
         r = orig_r(self)
-        acc["result"] += time.perf_counter() - t
+        mark["waited"] = time.perf_counter()
+        acc["result"] += mark["waited"] - t
         return r
 
     T.BoundStep.launch, T.BoundStep.result = launch, result
     t0 = time.perf_counter()
     for it in range(21, 21 + a.iters):
+        mark["start"] = time.perf_counter()
         m.train_iter(gt, it)
+        acc["post"] += time.perf_counter() - mark["waited"]
     total = (time.perf_counter() - t0) / a.iters * 1e6
     T.BoundStep.launch, T.BoundStep.result = orig_l, orig_r
     print(json.dumps(dict(us_per_iter=round(total, 2),
                           launch_us=round(acc["launch"] / a.iters * 1e6, 2),
                           wait_us=round(acc["result"] / a.iters * 1e6, 2),
-                          other_python_us=round(total - (acc["launch"] + acc["result"]) / a.iters * 1e6, 2))),
+                          other_python_us=round(total - (acc["launch"] + acc["result"]) / a.iters * 1e6, 2),
+                          pre_launch_us=round(acc["pre"] / a.iters * 1e6, 2),
+                          launch_to_wait_us=round(acc["mid"] / a.iters * 1e6, 2),
+                          post_wait_us=round(acc["post"] / a.iters * 1e6, 2))),
           flush=True)
     if a.profile:
         pr = cProfile.Profile()

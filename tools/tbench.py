@@ -30,6 +30,8 @@ def main():
                     help="two 8-row bands per tile (production) or the 256-thread kernel (knob 8 = 1)")
     ap.add_argument("--knob", action="append", default=[],
                     help="A/B knob K=V (gsvc_debug_set), repeatable")
+    ap.add_argument("--proj-stamps", action="store_true",
+                    help="also stamp the projection kernel's waves (start, projected, inserted, end)")
     ap.add_argument("--channels", action="store_true",
                     help="also print HIP-event kernel averages (us) over 200 extra iterations")
     a = ap.parse_args()
@@ -66,6 +68,26 @@ def main():
             ts = ops.channel_times_ms(c, 200)
             chan[c] = round(1e3 * sum(ts) / max(len(ts), 1), 2)
             ops.channel_timing(c, False)
+    if a.proj_stamps:
+        import ctypes
+        import numpy as np
+        from gsvc_amd import _lib as L
+        lib = L.load()
+        st = torch.zeros(((a.splats + 63) // 64, 4), dtype=torch.int64, device=dev)
+        lib.gsvc_debug_set_ptr(ctypes.c_void_p(st.data_ptr()))
+        lib.gsvc_debug_set(5, 1)
+        model.train_iter(gt, a.warmup + a.iters + 300)
+        torch.cuda.synchronize()
+        lib.gsvc_debug_set(5, 0)
+        lib.gsvc_debug_set_ptr(None)
+        t = st.cpu().numpy().astype(np.float64) * 0.01
+        t = t[t[:, 3] > 0]
+        t0 = t[:, 0].min()
+        q = lambda x: [round(float(np.percentile(x, p)), 2) for p in (0, 10, 50, 90, 100)]  # noqa
+        print(json.dumps(dict(proj_stamps="percentiles 0/10/50/90/100 (us)", waves=int(len(t)),
+                              start=q(t[:, 0] - t0), project=q(t[:, 1] - t[:, 0]),
+                              insert=q(t[:, 2] - t[:, 1]), reduce=q(t[:, 3] - t[:, 2]),
+                              end=q(t[:, 3] - t0))), flush=True)
     if a.stamps:
         import ctypes
         import numpy as np
