@@ -16,6 +16,14 @@ int tile_bins_from_counts(int num_points, const float2 *xys, const int *radii, i
                           int *ids_sorted, int2 *bins, int *meta, bool zero_counts,
                           hipStream_t s);
 
+// Stable LSD radix sort of n (key, value) pairs on key bits [0, bits); result
+// in (kout, vout); kbuf / vbuf scratch of n; counts / offsets each of
+// sort_u32_counts_bytes(n) bytes.
+size_t sort_u32_counts_bytes(int n);
+int sort_u32_pairs(int n, const unsigned *kin, const int *vin, unsigned *kout, int *vout,
+                   unsigned *kbuf, int *vbuf, int bits, unsigned *counts, unsigned *offsets,
+                   hipStream_t s);
+
 // Exclusive scan of the per-tile counts by one workgroup of kThreads threads:
 // tiles in chunks of kR * kThreads, every thread issuing its kR loads (one per
 // round, coalesced) up front -- one memory round trip per chunk -- wave scans by shuffles, one LDS exchange of the

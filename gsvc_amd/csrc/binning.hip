@@ -565,6 +565,16 @@ static int radix_sort(int n, const K *kin, const int *vin, K *kout, int *vout, K
     return GSVC_OK;
 }
 
+size_t sort_u32_counts_bytes(int n) { return sort_plan(n).counts_bytes; }
+
+int sort_u32_pairs(int n, const unsigned *kin, const int *vin, unsigned *kout, int *vout,
+                   unsigned *kbuf, int *vbuf, int bits, unsigned *counts, unsigned *offsets,
+                   hipStream_t s) {
+    if (n <= 0) return GSVC_OK;
+    return radix_sort<unsigned>(n, kin, vin, kout, vout, kbuf, vbuf, 0, bits, false, counts,
+                                offsets, s);
+}
+
 static int bits_for(int count) {
     int b = 0;
     while ((1ll << b) < (long long)count) ++b;

@@ -60,10 +60,22 @@ FrameSlots frame_slots(const FrameWs &w, int ntiles, int frame_index);
 // records zeroed for the consumer's atomics.
 // frames > 1: the splats of frame b are [frame_off[b], frame_off[b + 1]) of
 // the n (device array frame_off) and max_frame_n is the largest frame.
+// ord (single frame only): lane t projects splat ord->order[t] (NULL:
+// identity) and the workgroup aggregates its slot atomics per tile (the same
+// entries per tile); ord->key / key_id (optional): every splat's strip key and
+// id, the input of the next order's sort (frame.hip strip_key).
+struct SplatOrder {
+    const int *order = nullptr;
+    unsigned *key = nullptr;
+    int *key_id = nullptr;
+};
 int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *chol,
                          const float *chol_bound, const float *feat, const float *rgb_w,
                          const float *opac, unsigned img_h, unsigned img_w, const FrameWs &w,
                          const FrameSlots &f, float4 *grad_zero, hipStream_t s, int frames = 1,
-                         const int *frame_off = nullptr, int max_frame_n = 0);
+                         const int *frame_off = nullptr, int max_frame_n = 0,
+                         const SplatOrder *ord = nullptr);
+// Bits of the strip keys at this image size (invisible splats: the largest).
+int strip_key_bits(int tbx, int tby);
 
 }  // namespace gsvc

@@ -26,6 +26,7 @@
 //       parameter element; an extra first workgroup sums the tiles' errors in
 //       a fixed order into the loss.
 #include "adan.h"
+#include "binning.h"
 #include "frame.h"
 #include "tile_ids.h"
 
@@ -36,7 +37,7 @@ constexpr int kT = kTilePix;  // threads = pixels = entries of one tile
 struct TrainTileArgs {
     int tbx, img_w, img_h, ntiles, num_points, loss_l1;
     float norm;  // d loss / d pixel scale: float(2 / numel) for L2, 1.0f / numel for L1
-    float4 *slab;  // read; a brute tile parks its sorted ids in its own slab
+    float4 *slab;  // read; a dense tile parks its sorted ids in its own slab
     const unsigned *counts;
     unsigned *counts_clear;
     const int *m_dev;
@@ -502,13 +503,18 @@ __device__ __forceinline__ void wave_seg_sums(float (&g)[8], int key) {
     seg_step8<0x143, 0xc>(g, key);  // row_bcast:31 -> rows 2, 3
 }
 
+// v_out rows padded to 17 words: the backward's lanes read pixels of
+// different rows of one column, which with 16-word rows share a bank every 4
+// rows (measured: LDS bank conflicts ~ the VALU time at trained density).
+constexpr int kVRow = kTile + 1;
+
 struct BandLds {
-    float v[3][kTilePix];          // v_out planes
+    float v[3][kTile * kVRow];     // v_out planes, rows padded to kVRow words
     float4 geo[kBChunk];           // staged entries (rank order): x, y, a/2, b
     float4 col[kBChunk];           //   c/2, r, g, b
     unsigned ro[kBChunk];          //   rectangle (16 bits) | first work item << 16
     int gid[kBChunk];              //   splat id
-    float part[8][kBThreads];      // backward: item partials; ranking / flush scratch
+    float part[8][kBThreads + 1];  // backward: item partials; ranking / flush scratch
     signed char own[kBThreads];    // backward: entry of the round's first items
     int misc[8];
 };
@@ -556,8 +562,10 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     if (tid == 0) A.counts_clear[tile] = 0u;  // the next frame's counts
     const bool dense = n_all > kBChunk;
     const bool brute = n_all > kTilePix;  // the slab dropped entries: ids rebuilt
-    int *s_key = reinterpret_cast<int *>(&S.part[0][0]);     // dense: key (slot / id) by rank
-    int *s_ids = reinterpret_cast<int *>(&S.part[2][0]);     // dense: slot ids (scratch)
+    // dense: the splat ids by rank (part rows 0-1), the slab's ids (rows 2-3,
+    // scratch) and the sort's 512-word bitmap (rows 4-7)
+    int *s_key = reinterpret_cast<int *>(&S.part[0][0]);
+    int *s_ids = reinterpret_cast<int *>(&S.part[2][0]);
     int n = n_all;
 
     // 1. the order
@@ -582,14 +590,17 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                                (A.img_h + kTile - 1) / kTile, tile, s_key);
         n = min(n_all, kTilePix);  // both waves: wave_brute_ids finds >= 256 of them
     } else {
+        // the slab's ids, sorted by wave 0 with an LDS bitmap over the id range
+        // (tile_ids.h; O(n + id range / 16384 windows), not O(n^2) compares)
         for (int j = tid; j < n; j += kBThreads)
             s_ids[j] = __float_as_int(slab_rec(A.slab, A.ntiles, tile, j)[2].y);
         __syncthreads();
-        for (int j = tid; j < n; j += kBThreads) {
-            const int v = s_ids[j];
-            int rank = 0;
-            for (int k = 0; k < n; ++k) rank += s_ids[k] < v ? 1 : 0;
-            s_key[rank] = j;
+        if (w == 0) {
+            SegIds ids;
+            ids.ids = s_ids;
+            ids.recs = nullptr;
+            ids.head = nullptr;
+            wave_sorted_tile_ids(ids, n, s_key, reinterpret_cast<unsigned *>(&S.part[4][0]));
         }
     }
     __syncthreads();
@@ -606,11 +617,12 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     const float py = (float)pi;
     const v2f px = {(float)pj, (float)(pj + 1)};
     const int y_lo = 8 * w, y_hi = 8 * w + 7;
-    // dense: stage chunk [c0, c0 + cnt) of the order (both waves load half)
+    // dense: stage chunk [c0, c0 + cnt) of the order from the splats' records
+    // (rec holds the slab's records by splat id)
     auto stage_chunk = [&](const int *keys, int cnt) {
         if (tid < cnt) {
             const int key = keys[tid];
-            const float4 *rr = brute ? A.rec + 3 * (size_t)key : slab_rec(A.slab, A.ntiles, tile, key);
+            const float4 *rr = A.rec + 3 * (size_t)key;
             const float4 a = rr[0], b = rr[1], c = rr[2];
             S.geo[tid] = a;
             S.col[tid] = make_float4(b.x, b.z, b.w, c.x);
@@ -645,20 +657,11 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
         }
         if (dense) __syncthreads();  // the next chunk overwrites the staging
     }
-    // dense: the keys of ranks tid and tid + 128, kept for the backward (its
-    // partials overwrite s_key)
-    // (slab slots < 256: two 16-bit halves of one register); a brute tile's
-    // keys are splat ids, parked in its own slab (whose records it never reads)
-    unsigned krp = 0u;
+    // dense: the sorted ids, kept for the backward (its partials overwrite
+    // s_key) in the tile's own slab body, whose records it no longer reads
     int *kpark = reinterpret_cast<int *>(slab_rec(A.slab, A.ntiles, tile, kHeadSlots));  // 248 slots, contiguous
-    if (dense) {
-        if (!brute) {
-            krp = (unsigned)(tid < n ? s_key[tid] : 0) |
-                  ((unsigned)(tid + kBThreads < n ? s_key[tid + kBThreads] : 0) << 16);
-        } else {
-            for (int j = tid; j < n; j += kBThreads) kpark[j] = s_key[j];
-        }
-    }
+    if (dense)
+        for (int j = tid; j < n; j += kBThreads) kpark[j] = s_key[j];
     if (kStamp && tid == 0) st[2] = tstamp();
 
     // 3. clamp, loss gradient (mse_loss backward: norm * (a - b); l1: norm * sgn),
@@ -691,9 +694,12 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             for (int c = 0; c < 3; ++c)
                 for (int q = 0; q < nin; ++q) A.out[c * hw + pix0 + q] = clamp_unit(o[c][q]);
         }
-        const int p = prow * kTile + pcol;
+        const int p = prow * kVRow + pcol;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) *reinterpret_cast<float2 *>(&S.v[c][p]) = make_float2(v[c][0], v[c][1]);
+        for (int c = 0; c < 3; ++c) {
+            S.v[c][p] = v[c][0];
+            S.v[c][p + 1] = v[c][1];
+        }
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             se += __shfl_xor(se, off, 64);
@@ -716,13 +722,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
         if (dense) {
             __syncthreads();  // misc / staging / partial readers done
             // this chunk's keys, by rank, into the gid slots stage_chunk overwrites
-            if (!brute) {
-                if (tid >= c0 && tid < c0 + gn) S.gid[tid - c0] = (int)(krp & 0xffffu);
-                if (tid + kBThreads >= c0 && tid + kBThreads < c0 + gn)
-                    S.gid[tid + kBThreads - c0] = (int)(krp >> 16);
-            } else if (tid < gn) {
-                S.gid[tid] = kpark[c0 + tid];  // written by this workgroup before the forward's end
-            }
+            if (tid < gn) S.gid[tid] = kpark[c0 + tid];  // written by this workgroup after its forward
             __syncthreads();
             stage_chunk(S.gid, gn);
             __syncthreads();
@@ -792,7 +792,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                     const float fa = 2.0f * eha;
                     for (int col = cs; col <= ce; ++col) {
                         const float pxf = tx0 + (float)col;
-                        const int pix = row * kTile + col;
+                        const int pix = row * kVRow + col;
                         const float Px = S.v[0][pix], Py = S.v[1][pix], Pz = S.v[2][pix];
                         const float dx = ex - pxf;
                         const float sgm = fmaf(fmaf(eha, dx, bdy), dx, cq);
@@ -848,6 +848,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     if (kStamp && tid == 0) {
         st[4] = tstamp();
         st[5] = tstamp();
+        st[6] = n_all;  // the tile's entry count, for per-density breakdowns
     }
 }
 
@@ -1020,6 +1021,10 @@ struct TrainWs {
     FrameWs f;
     float4 *grad;
     float2 *err;
+    // the splat order (GSVC_TRAIN_ORDER): strip keys + ids written by a
+    // refreshing call's projection, sorted into ``order`` after its step
+    unsigned *okey, *skey, *kbuf, *sort_counts, *sort_offsets;
+    int *okey_id, *order, *vbuf;
     size_t bytes;
 };
 
@@ -1028,10 +1033,22 @@ static TrainWs train_ws(char *base, int n, int ntiles) {
     w.f = frame_ws(base, n, ntiles);
     size_t off = w.f.bytes;
     const size_t nn = (size_t)(n > 0 ? n : 1), nt = (size_t)(ntiles > 0 ? ntiles : 1);
-    w.grad = (float4 *)(base ? base + off : nullptr);
-    off += ws_align(sizeof(float4) * 4 * nn);
-    w.err = (float2 *)(base ? base + off : nullptr);
-    off += ws_align(sizeof(float2) * nt);
+    auto take = [&](size_t bytes) {
+        char *p = base ? base + off : nullptr;
+        off += ws_align(bytes);
+        return p;
+    };
+    w.grad = (float4 *)take(sizeof(float4) * 4 * nn);
+    w.err = (float2 *)take(sizeof(float2) * nt);
+    w.okey = (unsigned *)take(sizeof(unsigned) * nn);
+    w.skey = (unsigned *)take(sizeof(unsigned) * nn);
+    w.kbuf = (unsigned *)take(sizeof(unsigned) * nn);
+    w.okey_id = (int *)take(sizeof(int) * nn);
+    w.order = (int *)take(sizeof(int) * nn);
+    w.vbuf = (int *)take(sizeof(int) * nn);
+    const size_t cb = sort_u32_counts_bytes(n > 0 ? n : 1);
+    w.sort_counts = (unsigned *)take(cb);
+    w.sort_offsets = (unsigned *)take(cb);
     w.bytes = off;
     return w;
 }
@@ -1077,8 +1094,20 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
                          workspace_bytes, w.bytes);
     hipStream_t s = (hipStream_t)stream;
     const FrameSlots f = frame_slots(w.f, ntiles, frame_index);
+    // GSVC_TRAIN_ORDER: project in the workspace's splat order (windowed slot
+    // atomics); GSVC_TRAIN_ORDER_REFRESH: write keys and sort a new order
+    // after the step
+    const bool use_order = (adan_flags & GSVC_TRAIN_ORDER) != 0;
+    const bool refresh = (adan_flags & GSVC_TRAIN_ORDER_REFRESH) != 0 && num_points > 0;
+    SplatOrder ord;
+    ord.order = use_order ? w.order : nullptr;
+    if (refresh) {
+        ord.key = w.okey;
+        ord.key_id = w.okey_id;
+    }
     int rc = frame_project_launch(num_points, xyz, 1, cholesky, cholesky_bound, features, rgb_w,
-                                  nullptr, img_height, img_width, w.f, f, w.grad, s);
+                                  nullptr, img_height, img_width, w.f, f, w.grad, s, 1, nullptr, 0,
+                                  (use_order || refresh) ? &ord : nullptr);
     if (rc) return rc;
 
     const double count = 3.0 * (double)img_height * (double)img_width;  // numel of [3, H, W]
@@ -1156,7 +1185,11 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     const int tslot = timing_begin(s, tev, kTimingTrainSplat);
     launch_timed(train_splat_kernel, dim3(blocks), dim3(256), 0, s, tev, P);
     timing_end(s, tslot, kTimingTrainSplat);
-    return check_launch("train_step_sum: splats");
+    rc = check_launch("train_step_sum: splats");
+    if (rc || !refresh) return rc;
+    // the next calls' order: ids by strip key (stable: ties in id order)
+    return sort_u32_pairs(num_points, w.okey, w.okey_id, w.skey, w.order, w.kbuf, w.vbuf,
+                          strip_key_bits(tbx, tby), w.sort_counts, w.sort_offsets, s);
 }
 
 extern "C" int gsvc_train_step_sum_args(const gsvc_train_step_args *a) {

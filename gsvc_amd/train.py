@@ -22,6 +22,9 @@ from . import _lib as L
 
 LOSS_KIND = {"L2": 0, "L1": 1}
 TRAIN_LOSS_SEQ = 0x100  # include/gsvc_amd.h GSVC_TRAIN_LOSS_SEQ
+TRAIN_ORDER = 0x200  # GSVC_TRAIN_ORDER
+TRAIN_ORDER_REFRESH = 0x400  # GSVC_TRAIN_ORDER_REFRESH
+ORDER_REFRESH_EVERY = 64  # fused steps between splat-order sorts (0: no order)
 
 
 class _TrainWorkspace:
@@ -32,6 +35,24 @@ class _TrainWorkspace:
         self.dirty = True
         self.frame = 0
         self.shape = None
+        self.order_for = None  # (n, H, W) the workspace's splat order was sorted for
+        self.order_age = 0     # steps since it was sorted
+
+    def order_flags(self) -> int:
+        """GSVC_TRAIN_ORDER when a valid order exists, GSVC_TRAIN_ORDER_REFRESH
+        every ORDER_REFRESH_EVERY steps (splats drift; a stale order costs
+        speed only)."""
+        if ORDER_REFRESH_EVERY <= 0:
+            return 0
+        flags = 0
+        if self.order_for == self.shape:
+            flags |= TRAIN_ORDER
+            self.order_age += 1
+        if self.order_for != self.shape or self.order_age >= ORDER_REFRESH_EVERY:
+            flags |= TRAIN_ORDER_REFRESH
+            self.order_for = self.shape
+            self.order_age = 0
+        return flags
 
 
 _workspaces = {}
@@ -57,6 +78,7 @@ def _workspace(dev: torch.device, n: int, H: int, W: int) -> _TrainWorkspace:
         ws.frame = 0
         ws.hw = (H, W)
         ws.dirty = False
+        ws.order_for = None
     return ws
 
 
@@ -171,7 +193,7 @@ class BoundStep:
         self.seq = ((ws.frame + 1) & 0xFFFFFFFF) | 0x80000000
         a.gt = gt.data_ptr()
         a.frame_index = ws.frame
-        a.adan_flags = int(adan_flags) | TRAIN_LOSS_SEQ
+        a.adan_flags = int(adan_flags) | TRAIN_LOSS_SEQ | ws.order_flags()
         a.workspace = ws.buf_ptr
         a.workspace_bytes = ws.buf.numel()
         a.stream = self.stream

@@ -318,6 +318,13 @@ int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_tanh,
  * gsvc_render_frame_zeroed_bytes(H, W) bytes zero before the first call (every
  * call leaves them zero); frame_index alternates parity between calls. */
 #define GSVC_TRAIN_LOSS_SEQ 0x100
+/* Splat order (speed only; the same results): GSVC_TRAIN_ORDER projects the
+ * splats in the order an earlier GSVC_TRAIN_ORDER_REFRESH call of the same
+ * workspace, num_points and image size sorted (by the tile strip of their
+ * centres), so a workgroup's slot atomics aggregate per tile;
+ * GSVC_TRAIN_ORDER_REFRESH sorts a new one from this call's positions. */
+#define GSVC_TRAIN_ORDER 0x200
+#define GSVC_TRAIN_ORDER_REFRESH 0x400
 size_t gsvc_train_step_workspace_bytes(int num_points, unsigned img_height,
                                        unsigned img_width);
 int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,

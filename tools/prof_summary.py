@@ -70,9 +70,10 @@ def pmc_per_launch(d, counter):
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
-def pmc_all(dirs):
+def pmc_all(dirs, last=0):
     """{kernel: {counter: average per dispatch}} over every counter in the
-    --pmc pass directories ``dirs``."""
+    --pmc pass directories ``dirs`` (last > 0: over each kernel's last
+    ``last`` dispatches only, e.g. the trained state of a long run)."""
     vals = defaultdict(lambda: defaultdict(list))
     for d in dirs:
         for f in _csvs(d, "*counter_collection.csv"):
@@ -80,8 +81,16 @@ def pmc_all(dirs):
                 for r in csv.DictReader(fh):
                     k = _short(r["Kernel_Name"])
                     if k:
-                        vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in vals.items()}
+                        vals[k][r["Counter_Name"]].append((int(r["Dispatch_Id"]),
+                                                          float(r["Counter_Value"])))
+    out = {}
+    for k, cs in vals.items():
+        out[k] = {}
+        for c, v in cs.items():
+            v.sort()
+            v = v[-last:] if last > 0 else v
+            out[k][c] = sum(x for _, x in v) / len(v)
+    return out
 
 
 def main():
@@ -92,9 +101,11 @@ def main():
     ap.add_argument("--out")
     ap.add_argument("--key", default="10000")
     ap.add_argument("--pmc-dirs", nargs="*", help="print every counter per kernel")
+    ap.add_argument("--last", type=int, default=0,
+                    help="--pmc-dirs: average each kernel's last N dispatches only")
     a = ap.parse_args()
     if a.pmc_dirs:
-        print(json.dumps(pmc_all(a.pmc_dirs), indent=1))
+        print(json.dumps(pmc_all(a.pmc_dirs, a.last), indent=1))
     rec = {}
     if a.trace:
         st = trace_stats(a.trace)

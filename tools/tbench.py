@@ -32,11 +32,18 @@ def main():
                     help="A/B knob K=V (gsvc_debug_set), repeatable")
     ap.add_argument("--proj-stamps", action="store_true",
                     help="also stamp the projection kernel's waves (start, projected, inserted, end)")
+    ap.add_argument("--order-every", type=int, default=None,
+                    help="steps between splat-order sorts (gsvc_amd.train.ORDER_REFRESH_EVERY; 0: none)")
+    ap.add_argument("--shape", action="store_true",
+                    help="also report N_vis, M, M_eff of the trained frame (op-path binning)")
     ap.add_argument("--channels", action="store_true",
                     help="also print HIP-event kernel averages (us) over 200 extra iterations")
     a = ap.parse_args()
     from gsvc_amd.frame import make_frame_model, synthetic_gt
     from gsvc_amd import _lib
+    from gsvc_amd import train as _train
+    if a.order_every is not None:
+        _train.ORDER_REFRESH_EVERY = a.order_every
     _lib.load().gsvc_debug_set(8, 1 if a.tile_kernel == "wg256" else 0)
     for kv in a.knob:
         k, v = kv.split("=")
@@ -51,10 +58,25 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     psnr = 0.0
+    blocks = []
+    tb = t0
     for it in range(a.warmup + 1, a.warmup + a.iters + 1):
         _, psnr = model.train_iter(gt, it)
+        if (it - a.warmup) % 100 == 0:
+            tn = time.perf_counter()
+            blocks.append((tn - tb) / 100)
+            tb = tn
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.iters
+    blocks.sort()
+    block_us = dict(min=round(1e6 * blocks[0], 2), median=round(1e6 * blocks[len(blocks) // 2], 2)) \
+        if blocks else {}
+    shape = {}
+    if a.shape:
+        sys.path.insert(0, REPO)
+        import bench as B
+        shape = B.frame_shape(model.get_xyz.detach(), model.get_cholesky_elements.detach(),
+                              model.tile_bounds)
     chan = {}
     if a.channels:
         from gsvc_amd import ops
@@ -113,10 +135,25 @@ def main():
             rec[nm] = q(t[:, k + 1] - t[:, k])
         rec.update(life=q(t[:, 5] - t[:, 0]), end=q(t[:, 5] - t0))
         print(json.dumps(rec), flush=True)
+        if a.tile_kernel == "band":
+            # medians per entry-count bucket (stamp slot 6 = the tile's count)
+            cnt = st.cpu().numpy()[:, 6][st.cpu().numpy()[:, 5] > 0]
+            by = {}
+            for lo, hi in ((0, 16), (17, 32), (33, 64), (65, 128), (129, 256), (257, 1 << 30)):
+                sel = (cnt >= lo) & (cnt <= hi)
+                if sel.sum() == 0:
+                    continue
+                ts = t[sel]
+                by[f"{lo}-{hi}"] = dict(tiles=int(sel.sum()), **{
+                    nm: round(float(np.median(ts[:, k + 1] - ts[:, k])), 2)
+                    for k, nm in enumerate(names)}, life=round(float(np.median(ts[:, 5] - ts[:, 0])), 2))
+            print(json.dumps(dict(by_count=by, count_mean=round(float(cnt.mean()), 2))), flush=True)
     print(json.dumps(dict(splats=a.splats, tile_kernel=a.tile_kernel,
                           fused_train=model.fused_steps > 0, iters_per_s=round(1 / dt, 1),
                           ms_per_iter=round(1e3 * dt, 4), psnr=round(psnr, 3),
-                          knobs=a.knob, kernel_us=chan)), flush=True)
+                          us_per_iter_100=block_us, knobs=a.knob,
+                          order_every=_train.ORDER_REFRESH_EVERY, shape=shape,
+                          kernel_us=chan)), flush=True)
 
 
 if __name__ == "__main__":
