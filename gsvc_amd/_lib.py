@@ -51,7 +51,8 @@ _SIGS = {
     "gsvc_get_tile_bin_edges": [_I, _P, _P, _I, _P],
     "gsvc_bin_tiles_workspace_bytes": [_I, _I, _I],
     "gsvc_bin_tiles_counted_workspace_bytes": [_I],
-    "gsvc_bin_tiles_counted": [_I, _P, _P, _I, _I, ctypes.c_longlong, _P, _P, _P, _P, _P, _SZ, _P],
+    "gsvc_bin_tiles_counted": [_I, _P, _P, _I, _I, ctypes.c_longlong, _I, _P, _P, _P, _P, _P, _SZ,
+                               _P],
     "gsvc_bin_and_sort_tiles": [_I, _I, _P, _P, _P, _P, _I, _I, _P, _P, _I, _P, _P, _SZ, _P],
     "gsvc_rasterize_sum_forward": [_I, _I, _I, _I, _I, _I, _U, _U, _U, _P, _P, _P, _P, _P, _P, _P,
                                    _P, _P, _P, _P],

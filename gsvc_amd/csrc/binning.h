@@ -11,10 +11,14 @@ namespace gsvc {
 // zero_counts the scan clears counts for the next call.  counts NULL skips the
 // scan (the producer ran scan_tile_counts itself); ids_sorted NULL skips the
 // segment sort (ids_scratch then holds each tile's ids in fill order).
+// tile_cap > 0 (with ids_sorted): each tile keeps at most tile_cap entries --
+// the first tile_cap by splat id; a tile with more has its list rebuilt from
+// the splats' bboxes in id order (tile_ids.h wave_brute_ids); capacity need
+// only cover sum(min(count, tile_cap)).
 int tile_bins_from_counts(int num_points, const float2 *xys, const int *radii, int tbx, int tby,
                           long long capacity, unsigned *counts, unsigned *cursor, int *ids_scratch,
                           int *ids_sorted, int2 *bins, int *meta, bool zero_counts,
-                          hipStream_t s);
+                          hipStream_t s, unsigned tile_cap = 0u);
 
 // Stable LSD radix sort of n (key, value) pairs on key bits [0, bits); result
 // in (kout, vout); kbuf / vbuf scratch of n; counts / offsets each of
@@ -29,23 +33,28 @@ int sort_u32_pairs(int n, const unsigned *kin, const int *vin, unsigned *kout, i
 // round, coalesced) up front -- one memory round trip per chunk -- wave scans by shuffles, one LDS exchange of the
 // wave totals per chunk.  Writes tile_bins ((0,0) when empty), the fill
 // cursors and meta = {M, M > capacity}; with zero_counts the reading thread
-// clears each counter for the next call.
+// clears each counter for the next call.  tile_cap > 0: each tile's segment
+// holds at most tile_cap entries (the consumers read only the first 256 of a
+// tile); M stays the uncapped total.
 template <int kThreads, int kR = 8>
 __device__ __forceinline__ void scan_tile_counts(int ntiles, unsigned *__restrict__ counts,
                                                  int2 *__restrict__ bins,
                                                  unsigned *__restrict__ cursor,
                                                  int *__restrict__ meta, long long capacity,
-                                                 bool zero_counts) {
+                                                 bool zero_counts, unsigned tile_cap = 0u) {
     constexpr int kW = kThreads / 64;
     __shared__ unsigned s_tot[kR][kW];
+    __shared__ unsigned s_all[kW];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    unsigned carry = 0u;
+    unsigned carry = 0u, all = 0u;
     for (int c0 = 0; c0 < ntiles; c0 += kThreads * kR) {
         unsigned v[kR], incl[kR];
 #pragma unroll
         for (int r = 0; r < kR; ++r) {
             const int i = c0 + r * kThreads + tid;
             v[r] = i < ntiles ? counts[i] : 0u;
+            all += v[r];
+            if (tile_cap) v[r] = min(v[r], tile_cap);
         }
 #pragma unroll
         for (int r = 0; r < kR; ++r) {
@@ -81,8 +90,15 @@ __device__ __forceinline__ void scan_tile_counts(int ntiles, unsigned *__restric
         carry = base;
         __syncthreads();
     }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) all += __shfl_xor(all, off, 64);
+    if (lane == 0) s_all[w] = all;
+    __syncthreads();
     if (tid == 0) {
-        meta[0] = (int)carry;
+        unsigned tot = 0u;
+#pragma unroll
+        for (int k = 0; k < kW; ++k) tot += s_all[k];
+        meta[0] = (int)tot;
         meta[1] = (long long)carry > capacity ? 1 : 0;
     }
 }

@@ -18,6 +18,7 @@
 // bin_and_sort_gaussians when depth bits differ) runs the same kernels on all
 // 8 digits.
 #include "binning.h"
+#include "tile_ids.h"
 
 namespace gsvc {
 
@@ -400,16 +401,18 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(int ntiles, unsigned *_
                                                          int2 *__restrict__ bins,
                                                          unsigned *__restrict__ cursor,
                                                          int *__restrict__ meta, long long capacity,
-                                                         int zero_counts) {
-    scan_tile_counts<1024>(ntiles, counts, bins, cursor, meta, capacity, zero_counts != 0);
+                                                         int zero_counts, unsigned tile_cap) {
+    scan_tile_counts<1024>(ntiles, counts, bins, cursor, meta, capacity, zero_counts != 0, tile_cap);
 }
 
 // The cursor atomics of a splat are issued in batches of 8 before any of
 // their results is waited for (one round trip per batch, not per tile).
+// ``ends`` (tile_cap mode): a slot at or past the tile's capped end is dropped.
 __global__ __launch_bounds__(256) void tile_fill_kernel(int n, const float2 *__restrict__ xys,
                                                         const int *__restrict__ radii, int tbx, int tby,
                                                         unsigned *__restrict__ cursor,
-                                                        int *__restrict__ ids, long long capacity) {
+                                                        int *__restrict__ ids, long long capacity,
+                                                        const int2 *__restrict__ ends) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int r = radii[i];
@@ -427,7 +430,8 @@ __global__ __launch_bounds__(256) void tile_fill_kernel(int n, const float2 *__r
             if (k < cnt) sl[k] = atomicAdd(cursor + tl[k], 1u);
 #pragma unroll
         for (int k = 0; k < kBatch; ++k)
-            if (k < cnt && (long long)sl[k] < capacity) ids[sl[k]] = i;
+            if (k < cnt && (long long)sl[k] < capacity && (!ends || (int)sl[k] < ends[tl[k]].y))
+                ids[sl[k]] = i;
         cnt = 0;
     };
     for (unsigned y = y0; y < y1; ++y)
@@ -502,6 +506,20 @@ __global__ __launch_bounds__(64) void tile_segsort_kernel(int ntiles, const int2
         written += __shfl(incl, 63, 64);
         __syncthreads();
     }
+}
+
+// tile_cap mode: a tile with more than tile_cap entries kept an arbitrary
+// tile_cap of them; its first tile_cap ids are rebuilt in id order by one
+// wave scanning every splat's bbox (rare: trained frames' densest tiles).
+__global__ __launch_bounds__(64) void tile_overflow_kernel(int n, const float2 *__restrict__ xys,
+                                                           const int *__restrict__ radii, int tbx,
+                                                           int tby, const unsigned *__restrict__ counts,
+                                                           const int2 *__restrict__ bins,
+                                                           int *__restrict__ ids_out, unsigned tile_cap) {
+    const int tile = blockIdx.x;
+    if (counts[tile] <= tile_cap) return;
+    const int2 range = bins[tile];
+    wave_brute_ids(xys, radii, 0, n, tbx, tby, tile, ids_out + range.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -584,19 +602,26 @@ static int bits_for(int count) {
 int tile_bins_from_counts(int num_points, const float2 *xys, const int *radii, int tbx, int tby,
                           long long capacity, unsigned *counts, unsigned *cursor, int *ids_scratch,
                           int *ids_sorted, int2 *bins, int *meta, bool zero_counts,
-                          hipStream_t s) {
+                          hipStream_t s, unsigned tile_cap) {
     const int ntiles = tbx * tby;
+    if (tile_cap && (!counts || !ids_sorted || zero_counts))
+        return set_error(GSVC_ERR_ARG, "tile binning: a per-tile cap needs the counts and the sort");
     if (counts)  // NULL: the producer already scanned (bins, cursor, meta written)
         hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, ntiles, counts, bins, cursor,
-                           meta, capacity, zero_counts ? 1 : 0);
+                           meta, capacity, zero_counts ? 1 : 0, tile_cap);
     if (num_points > 0) {
         hipLaunchKernelGGL(tile_fill_kernel, dim3(ceil_div(num_points, 256)), dim3(256), 0, s,
-                           num_points, xys, radii, tbx, tby, cursor, ids_scratch, capacity);
+                           num_points, xys, radii, tbx, tby, cursor, ids_scratch, capacity,
+                           tile_cap ? (const int2 *)bins : nullptr);
     }
     if (num_points > 0 && ids_sorted) {  // NULL: the consumer sorts each tile itself
         const int bm_words = min(ceil_div(num_points, 32) + 1, 4096);
         hipLaunchKernelGGL(tile_segsort_kernel, dim3(ntiles), dim3(64), sizeof(unsigned) * bm_words, s,
                            ntiles, (const int2 *)bins, ids_scratch, ids_sorted, bm_words, capacity);
+        if (tile_cap)
+            hipLaunchKernelGGL(tile_overflow_kernel, dim3(ntiles), dim3(64), 0, s, num_points, xys,
+                               radii, tbx, tby, (const unsigned *)counts, (const int2 *)bins,
+                               ids_sorted, tile_cap);
     }
     return check_launch("tile binning");
 }
@@ -759,12 +784,14 @@ extern "C" size_t gsvc_bin_tiles_counted_workspace_bytes(int num_tiles) {
 }
 
 extern "C" int gsvc_bin_tiles_counted(int num_points, const float *xys, const int *radii, int tbx,
-                                      int tby, long long capacity, int *ids_scratch,
+                                      int tby, long long capacity, int tile_cap, int *ids_scratch,
                                       int *gaussian_ids_sorted, int *tile_bins, int *meta,
                                       void *workspace, size_t workspace_bytes, void *stream) {
     const int ntiles = tbx * tby;
-    if (num_points < 0 || tbx <= 0 || tby <= 0 || capacity < 0)
+    if (num_points < 0 || tbx <= 0 || tby <= 0 || capacity < 0 || tile_cap < 0)
         return set_error(GSVC_ERR_ARG, "bin_tiles_counted: bad sizes");
+    if (tile_cap && !gaussian_ids_sorted)
+        return set_error(GSVC_ERR_ARG, "bin_tiles_counted: tile_cap needs gaussian_ids_sorted");
     if (workspace_bytes < gsvc_bin_tiles_counted_workspace_bytes(ntiles))
         return set_error(GSVC_ERR_WORKSPACE, "bin_tiles_counted: workspace too small");
     hipStream_t s = (hipStream_t)stream;
@@ -777,5 +804,5 @@ extern "C" int gsvc_bin_tiles_counted(int num_points, const float *xys, const in
                            num_points, (const float2 *)xys, radii, tbx, tby, counts);
     return tile_bins_from_counts(num_points, (const float2 *)xys, radii, tbx, tby, capacity, counts,
                                  cursor, ids_scratch, gaussian_ids_sorted, (int2 *)tile_bins, meta,
-                                 false, s);
+                                 false, s, (unsigned)tile_cap);
 }

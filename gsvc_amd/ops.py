@@ -283,11 +283,12 @@ def bin_and_sort_tiles(num_points, num_intersects, xys, depths, radii, cum_tiles
     return gids, bins, isect
 
 
-def bin_tiles_counted(num_points, xys, radii, tile_bounds, capacity):
+def bin_tiles_counted(num_points, xys, radii, tile_bounds, capacity, tile_cap=0):
     """Sync-free tile binning (gsvc_bin_tiles_counted): returns
     (gaussian_ids_sorted [capacity], tile_bins [#tiles, 2], meta [2] = {M,
     overflow}) with M only on the device.  Valid when every emitting splat has
-    the same depth bits (the order is (tile, splat id))."""
+    the same depth bits (the order is (tile, splat id)).  tile_cap > 0 keeps
+    each tile's first tile_cap entries only."""
     xys = _f32(xys, "xys")
     radii = _i32(radii, "radii")
     tb = _tb(tile_bounds)
@@ -300,8 +301,9 @@ def bin_tiles_counted(num_points, xys, radii, tile_bounds, capacity):
     meta = torch.empty((2,), dtype=torch.int32, device=dev)
     ws = torch.empty((L.size("gsvc_bin_tiles_counted_workspace_bytes", ntiles),), dtype=torch.uint8,
                      device=dev)
-    L.call("gsvc_bin_tiles_counted", n, L.ptr(xys), L.ptr(radii), tb[0], tb[1], cap, L.ptr(scratch),
-           L.ptr(gids), L.ptr(bins), L.ptr(meta), L.ptr(ws), ws.numel(), L.stream(dev))
+    L.call("gsvc_bin_tiles_counted", n, L.ptr(xys), L.ptr(radii), tb[0], tb[1], cap, int(tile_cap),
+           L.ptr(scratch), L.ptr(gids), L.ptr(bins), L.ptr(meta), L.ptr(ws), ws.numel(),
+           L.stream(dev))
     return gids, bins, meta
 
 

@@ -18,6 +18,7 @@ from . import ops as _C
 # may allocate (its capacity is num_points * num_tiles, which cannot
 # overflow).  Above it the rasterizers read M on the host first.
 BIN_CAPACITY_BUDGET = int(os.environ.get("GSVC_BIN_CAPACITY_BUDGET", str(1 << 30)))
+TILE_KEEP = 256  # entries per tile the sum rasterizer blends (config.h BLOCK_SIZE)
 
 
 def mark_zero_depths(depths: Tensor) -> Tensor:
@@ -157,14 +158,18 @@ def bin_for_raster(num_points: int, xys: Tensor, depths: Optional[Tensor], radii
 
     When the depths are known to be zero (project_gaussians_2d's output) the
     (tile, splat id) order IS the reference's sorted order, and the sync-free
-    CSR binning runs with capacity num_points * tiles (no host round trip);
+    CSR binning runs (no host round trip) keeping each tile's first 256
+    entries -- all the sum rasterizer reads (forward.cu:569-571,613) -- so the
+    id buffers are tiles * min(num_points, 256) ints (8.4 MB at 1080p);
     otherwise -- or when that capacity exceeds BIN_CAPACITY_BUDGET -- M is read
     on the host and the sorted path of ``bin_and_sort_for_raster`` runs.
     """
     ntiles = int(tile_bounds[0]) * int(tile_bounds[1])
-    cap = int(num_points) * ntiles
+    per_tile = min(int(num_points), TILE_KEEP)
+    cap = per_tile * ntiles
     if depths_known_zero(depths) and cap <= BIN_CAPACITY_BUDGET:
-        gids, bins, meta = _C.bin_tiles_counted(num_points, xys, radii, tile_bounds, cap)
+        gids, bins, meta = _C.bin_tiles_counted(num_points, xys, radii, tile_bounds, cap,
+                                                TILE_KEEP if int(num_points) > TILE_KEEP else 0)
         m_dev = meta[:1]
         return TileBinning(None, m_dev, gids, bins, _density_hint(m_dev))
     m, gids, bins = bin_and_sort_for_raster(num_points, xys, depths, radii, num_tiles_hit,

@@ -208,15 +208,20 @@ int gsvc_bin_and_sort_tiles(
  * host): builds gaussian_ids_sorted in the stable (tile, splat id) order of
  * the reference's sorted pairs and tile_bins[tbx*tby] ([start,end), (0,0)
  * when empty), every size staying on the device.  meta[0] <- M,
- * meta[1] <- 1 if M > capacity (outputs then incomplete).  ids_scratch and
- * gaussian_ids_sorted hold >= capacity ints; capacity = num_points * tiles
- * can never overflow.  Results are deterministic. */
+ * meta[1] <- 1 if the entries kept exceed capacity (outputs then
+ * incomplete).  ids_scratch and gaussian_ids_sorted hold >= capacity ints.
+ * tile_cap > 0 keeps only each tile's first tile_cap entries in id order (the
+ * sum rasterizer reads no more than 256 per tile, forward.cu:569-571,613; a
+ * tile with more is rebuilt from the splats' bboxes in id order), so
+ * capacity = tiles * min(num_points, tile_cap) can never overflow; with
+ * tile_cap 0 every entry is kept and capacity = num_points * tiles is the
+ * safe bound.  M is the uncapped total either way.  Deterministic. */
 size_t gsvc_bin_tiles_counted_workspace_bytes(int num_tiles);
 int gsvc_bin_tiles_counted(int num_points, const float *xys, const int *radii,
                            int tile_bounds_x, int tile_bounds_y, long long capacity,
-                           int *ids_scratch, int *gaussian_ids_sorted, int *tile_bins,
-                           int *meta, void *workspace, size_t workspace_bytes,
-                           void *stream);
+                           int tile_cap, int *ids_scratch, int *gaussian_ids_sorted,
+                           int *tile_bins, int *meta, void *workspace,
+                           size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Sum rasterizer (the GSVC renderer, rasterize_sum.py).

@@ -115,6 +115,57 @@ def test_segment_sort_boundaries(cuda, oracle, count):
     assert (ref["bins"][:, 1] - ref["bins"][:, 0]).max() == count
 
 
+def _capped_matches(n, xys, radii, tb, ref, keep=256):
+    """bin_tiles_counted with tile_cap: every tile holds exactly the first
+    min(count, keep) ids of the reference's sorted segment, M uncapped, and
+    the buffers are tiles * min(n, keep) ints."""
+    from gsvc_amd import ops
+    ntiles = tb[0] * tb[1]
+    cap = ntiles * min(n, keep)
+    gids, bins, meta = ops.bin_tiles_counted(n, xys, radii, tb, cap, keep)
+    m, ovf = (int(x) for x in meta.tolist())
+    assert m == ref["m"] and ovf == 0 and gids.numel() == cap
+    g, b = N(gids), N(bins)
+    rb = ref["bins"][:ntiles]
+    over = 0
+    for t in range(ntiles):
+        cnt = rb[t, 1] - rb[t, 0]
+        want = ref["gids_sorted"][rb[t, 0]: rb[t, 0] + min(cnt, keep)] if cnt > 0 else []
+        got = g[b[t, 0]: b[t, 1]] if b[t, 1] > b[t, 0] else []
+        np.testing.assert_array_equal(np.asarray(got), np.asarray(want), err_msg=f"tile {t}")
+        over += int(cnt > keep)
+    return over
+
+
+@pytest.mark.parametrize("count", [200, 300, 700])
+def test_capped_binning_overflow_tile(cuda, oracle, count):
+    """T*256 id buffers: a tile past 256 entries keeps its first 256 ids
+    (rebuilt in id order from the bboxes)."""
+    from gsvc_amd import ops
+    n = 4000
+    ids = np.random.default_rng(count).choice(n, count, replace=False)
+    means, L, colors, opac, H, W = _clustered_frame(n, ids)
+    ref = oracle.render_sum(means, L, colors, opac, H, W)
+    tb = _tb(H, W)
+    xys, depths, radii, conics, nth = ops.project_gaussians_2d_forward(n, T(means), T(L), H, W, tb,
+                                                                      0.01)
+    over = _capped_matches(n, xys, radii, tb, ref)
+    assert (over > 0) == (count > 256)
+
+
+def test_capped_binning_1080p_dense(cuda, oracle):
+    """1080p with large splats (20k, chol x24: hundreds of entries per tile):
+    many tiles past 256 entries."""
+    from gsvc_amd import ops
+    H, W, n = 1080, 1920, 20000
+    tb = _tb(H, W)
+    means, L, colors, opac = oracle.synthetic_frame(n, seed=n + 3, chol_scale=24.0)
+    ref = oracle.render_sum(means, L, colors, opac, H, W)
+    xys, depths, radii, conics, nth = ops.project_gaussians_2d_forward(n, T(means), T(L), H, W, tb,
+                                                                      0.01)
+    assert _capped_matches(n, xys, radii, tb, ref) > 0
+
+
 def test_segment_sort_multi_window(cuda, oracle):
     """Splat ids spanning more than one 4096-word LDS bitmap (131072 ids)."""
     from gsvc_amd import ops

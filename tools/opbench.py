@@ -39,11 +39,14 @@ def run(n, H, W, calls, dev, backward):
     for _ in range(20):
         step()
     torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated(dev)
+    torch.cuda.reset_peak_memory_stats(dev)
     t0 = time.perf_counter()
     for _ in range(calls):
         step()
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / calls * 1e6
+    us = (time.perf_counter() - t0) / calls * 1e6
+    return us, (torch.cuda.max_memory_allocated(dev) - base) / 2**20
 
 
 def main():
@@ -53,8 +56,15 @@ def main():
     dev = torch.device("cuda:0")
     res = {}
     for bw in (False, True):
-        res[f"tiny_{'fwd_bwd' if bw else 'fwd'}_us"] = round(run(16, 16, 16, a.calls, dev, bw), 1)
-        res[f"1080p_50k_{'fwd_bwd' if bw else 'fwd'}_us"] = round(run(50000, 1080, 1920, a.calls // 5, dev, bw), 1)
+        tag = "fwd_bwd" if bw else "fwd"
+        us, _ = run(16, 16, 16, a.calls, dev, bw)
+        res[f"tiny_{tag}_us"] = round(us, 1)
+        us, mib = run(50000, 1080, 1920, a.calls // 5, dev, bw)
+        res[f"1080p_50k_{tag}_us"] = round(us, 1)
+        res[f"1080p_50k_{tag}_peak_extra_MiB"] = round(mib, 1)
+    res["note"] = ("unchanged-caller path: gsplat.project_gaussians_2d + rasterize_gaussians_sum "
+                   "(+ .sum().backward()); peak_extra = max_memory_allocated above the "
+                   "resident inputs during the timed calls")
     print(json.dumps(res))
 
 
