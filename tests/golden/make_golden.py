@@ -251,6 +251,37 @@ def make_alpha_case(gs, name, H, W, means, L, colors, opac, seed):
     print(f"{name}: N={means.shape[0]} M={M} |oracle - _torch_impl| max = {err:.3e}")
 
 
+def make_alpha_dense_cases(gs):
+    """Alpha compositing past one 256-entry batch (forward.cu:252-374 loops over
+    every batch of the tile) and with the T <= 1e-4 early stop firing: 400
+    large splats over a 32x32 frame (4 tiles, ~400 entries each).
+    ``alpha_32x32_stop``: opaque splats, most pixels stop within a few
+    entries; ``alpha_32x32_deep``: faint splats, T stays above 1e-4 past entry
+    256.  Each fixture stores the per-pixel entry position the compositing
+    reached (final_idx - tile start) and whether it stopped early."""
+    rng = np.random.default_rng(21)
+    n = 400
+    for name, lo, hi in (("alpha_32x32_stop", 0.6, 1.0), ("alpha_32x32_deep", 0.004, 0.012)):
+        means = rng.uniform(-0.6, 0.6, (n, 2)).astype(np.float32)
+        L = (rng.random((n, 3), dtype=np.float32) * np.array([2, 0.5, 2], np.float32)
+             + np.array([4.0, 0, 4.0], np.float32)).astype(np.float32)
+        colors = rng.random((n, 3), dtype=np.float32)
+        opac = rng.uniform(lo, hi, (n, 1)).astype(np.float32)
+        make_alpha_case(gs, name, 32, 32, means, L, colors, opac, 21)
+        z = dict(np.load(os.path.join(OUT, name + ".npz")))
+        tb = O.tile_bounds(32, 32)
+        b = z["tile_bins"]
+        ty, tx = np.meshgrid(np.arange(32) // 16, np.arange(32) // 16, indexing="ij")
+        tile = ty * tb[0] + tx
+        start = b[tile, 0]
+        count = b[tile, 1] - b[tile, 0]
+        z["reach"] = (z["final_idx"] - start).astype(np.int32)
+        z["tile_count"] = count.astype(np.int32)
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), **z)
+        print(f"{name}: entries/tile {count.min()}..{count.max()}, reach max {z['reach'].max()}, "
+              f"final_Ts min {z['final_Ts'].min():.2e}")
+
+
 def make_ref_tests_case():
     """Inputs and expected outputs of gsplat/tests/test_map_gaussians.py:8-73,
     test_get_tile_bin_edges.py:9-81 and test_cov2d_bounds.py:8-35 (seed 42)."""
@@ -440,6 +471,10 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "prune":
         _import_reference()
         make_prune_cases()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "alpha":
+        gs = _import_reference()
+        make_alpha_dense_cases(gs)
         return
     if len(sys.argv) > 1 and sys.argv[1] == "trajectory":
         _import_reference()

@@ -1,0 +1,77 @@
+"""BASELINE configs 4 and 5 at full frame size on one GPU: the video loop of
+train_video_Represent.py:358-398 (gsvc_amd.video.main) over 1920x1080
+synthetic frames,
+
+* config 4: 50k splats per frame, two GOPs (K-frames 1 and 3), the fused
+  training step on every plain iteration;
+* config 5: 100k splats with --is_rm --is_ad, run long enough to pass through
+  a K-frame removal window (removal_control every densification_interval
+  iterations, GaussianSplats_Represent.py:98-128) and a P-frame densify +
+  prune window (adaptive_control, :130-172: densify at iteration 1, prune in
+  (500, 1000]);
+
+each checked against the same loop with the fused step switched off (the
+op-by-op path that GSVC's unchanged GaussianSplats_Represent.py runs): the
+splat counts the controls leave must be identical and the per-frame PSNRs
+close (float atomics in the backward make the two trajectories differ in the
+last bits, which Adan's normalisation amplifies, so PSNR is compared with a
+tolerance rather than bit for bit).
+"""
+import functools
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(tmp_path, argv, fused):
+    from gsvc_amd import frame as Fm
+    from gsvc_amd import video as V
+    orig = V.GaussianVideoFrame
+    if not fused:
+        V.GaussianVideoFrame = functools.partial(Fm.GaussianVideoFrame, fused_train=False)
+    try:
+        return V.main(argv + ["--root", str(tmp_path / ("fused" if fused else "ops"))])
+    finally:
+        V.GaussianVideoFrame = orig
+
+
+def test_config4_two_gops_1080p_50k(cuda, tmp_path):
+    argv = ["--synthetic", "4", "--height", "1080", "--width", "1920", "--num_points", "50000",
+            "--iterations", "300", "--k_frames", "1,3", "--cut_every", "2"]
+    res = _run(tmp_path, argv, True)
+    ref = _run(tmp_path, argv, False)
+    assert [r["frame"] for r in res["frames"]] == [1, 2, 3, 4]
+    assert res["gops"] == [[1, 3], [3, 5]]
+    p, q = (np.array([r["psnr"] for r in x["frames"]]) for x in (res, ref))
+    # 300 iterations from random init on the synthetic 1080p video: ~10 dB
+    assert np.all(np.isfinite(p)) and np.all(p > 8.0)
+    # P-frames start from the previous frame's model
+    assert p[1] > p[0] and p[3] > p[2]
+    np.testing.assert_allclose(p, q, atol=0.05)
+    assert [r["num_gaussians"] for r in res["frames"]] == [50000] * 4
+    assert res["average"]["psnr"] == pytest.approx(float(p.mean()), rel=1e-9)
+
+
+def test_config5_removal_and_densify_1080p_100k(cuda, tmp_path):
+    """A K-frame with removal (11 pruning steps at interval 100) and two
+    P-frames with densify at iteration 1 and pruning in (500, 1000]."""
+    argv = ["--synthetic", "3", "--height", "1080", "--width", "1920", "--num_points", "100000",
+            "--iterations", "1100", "--k_frames", "1", "--is_rm", "--is_ad",
+            "--densification_interval", "100", "--removal_rate", "0.1"]
+    res = _run(tmp_path, argv, True)
+    ref = _run(tmp_path, argv, False)
+    n = [r["num_gaussians"] for r in res["frames"]]
+    assert n == [r["num_gaussians"] for r in ref["frames"]]
+    assert n[0] < 100000  # the K-frame pruned
+    # a P-frame: densified at iteration 1, then pruned back in (500, 1000]
+    assert n[1] <= 100000 + int(100000 * 0.1)
+    p, q = (np.array([r["psnr"] for r in x["frames"]]) for x in (res, ref))
+    assert np.all(np.isfinite(p)) and np.all(p > 8.0)
+    # the controls prune the lowest-scoring splats: near-ties pick different
+    # splats on the two paths, so the P-frames drift further apart (measured
+    # 0.13 dB at 39.7 dB)
+    np.testing.assert_allclose(p, q, rtol=0.01)
+    assert all(r["iterations"] == 1100 for r in res["frames"])
