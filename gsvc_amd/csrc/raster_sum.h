@@ -16,6 +16,7 @@ struct SumFwdArgs {
     bool vec;      // HWC: W % 4 == 0 and 16-byte aligned outputs
     bool vec_chw;  // CHW: W % 4 == 0, H*W % 4 == 0, 16-byte aligned
     int store_policy;  // CHW plane stores: kStore* (gsvc_debug_set(7) selects)
+    int spec_slots;    // frame path: slab records loaded with the count (<= kHeadSlots)
     const int *m_dev;  // device num_intersects (NULL: > 0); 0 -> background
     const float *bg;
     const int *ids;

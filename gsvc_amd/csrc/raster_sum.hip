@@ -45,7 +45,12 @@
 namespace gsvc {
 
 constexpr int kChunk = 64;
-constexpr int kSpecSlots = kHeadSlots;  // slab records loaded with the count (frame path)
+// Frame path: the first spec_slots (<= kHeadSlots) slab records are loaded in
+// the count's round trip (speculatively: most tiles have that few); slot j of a
+// tile is in its head (j < kHeadSlots) or at index j of its body.
+__device__ __forceinline__ const float4 *slot_rec(const float4 *head, const float4 *body, int j) {
+    return j < kHeadSlots ? head + 3 * j : body + 3 * j;
+}
 constexpr int kSlice = kTilePix * 3 / 4;  // float4s of LDS per wave (3 KB)
 
 // Forward kernel modes.  Production: the launcher picks kModeSparse (one wave
@@ -213,7 +218,8 @@ template <int kMode, bool kIdx>
 __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, int2 range, int n,
                                                float4 *s_slice, float3 init, bool ids_in_lds,
                                                const int *s_ids, const float4 *seg_rec,
-                                               float4 spec0, float4 spec1, float4 spec2) {
+                                               const float4 *seg_head, float4 spec0, float4 spec1,
+                                               float4 spec2) {
     float4 *s_geo = s_slice;                           // x, y, 0.5a, b
     float4 *s_col = s_slice + kChunk;                  // 0.5c, opacity, r, g
     float *s_blu = (float *)(s_slice + 2 * kChunk);    // b
@@ -232,10 +238,11 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         if (seg_rec) {
             // <= 64 slab records in fill order: staged at their rank by id
             float4 geo = spec0, col = spec1, bx = spec2;
-            if (lane >= kSpecSlots && lane < cnt) {
-                geo = seg_rec[3 * lane];  // body slots (lanes >= kSpecSlots = kHeadSlots)
-                col = seg_rec[3 * lane + 1];
-                bx = seg_rec[3 * lane + 2];
+            if (lane >= A.spec_slots && lane < cnt) {
+                const float4 *r = slot_rec(seg_head, seg_rec, lane);
+                geo = r[0];
+                col = r[1];
+                bx = r[2];
             }
             const int id = lane < cnt ? __float_as_int(bx.y) : 0x7fffffff;
             const int rank = rank_below(id, cnt);
@@ -329,7 +336,8 @@ template <int kMode, bool kIdx>
 __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int band, int2 range,
                                              int n, float4 *s_slice, float3 init, bool ids_in_lds,
                                              const int *s_ids, const float4 *seg_rec,
-                                             float4 spec0, float4 spec1, float4 spec2) {
+                                             const float4 *seg_head, float4 spec0, float4 spec1,
+                                             float4 spec2) {
     float4 *s_geo = s_slice;                                      // x, y, 0.5a, b
     float4 *s_col = s_slice + kChunk;                             // 0.5c, opacity, r, g
     float *s_blu = reinterpret_cast<float *>(s_slice + 2 * kChunk);
@@ -357,10 +365,11 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
                 float4 bx = spec2;
                 geo = spec0;
                 col = spec1;
-                if (lane >= kSpecSlots) {
-                    geo = seg_rec[3 * j];  // body slots (j >= kSpecSlots = kHeadSlots)
-                    col = seg_rec[3 * j + 1];
-                    bx = seg_rec[3 * j + 2];
+                if (lane >= A.spec_slots) {
+                    const float4 *r = slot_rec(seg_head, seg_rec, j);
+                    geo = r[0];
+                    col = r[1];
+                    bx = r[2];
                 }
                 blu = bx.x;
                 id = __float_as_int(bx.y);
@@ -497,7 +506,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         // slots >= kHeadSlots at their index from recs; the first ones in the head
         const float4 *recs = slab_rec(A.slab, A.ntiles, tile, kHeadSlots) - 3 * kHeadSlots;
         n_all = (int)__builtin_amdgcn_readfirstlane(A.slab_counts[tile]);
-        if (lane < kSpecSlots) {
+        if (lane < A.spec_slots) {
             const float4 *h = slab_rec(A.slab, A.ntiles, tile, lane);
             spec0 = h[0];
             spec1 = h[1];
@@ -542,16 +551,16 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
             n = (A.slab && n_all > kTilePix)
                     ? wave_brute_tile_ids(A, tile, s_ids[0])
                     : wave_sorted_tile_ids(seg, n_all, s_ids[0], reinterpret_cast<unsigned *>(s_buf[0]));
-        sum_fwd_sparse<kMode, kIdx>(A, tile, range, n, s_buf[0], init, by_ids, s_ids[0], seg_rec, spec0,
-                              spec1, spec2);
+        sum_fwd_sparse<kMode, kIdx>(A, tile, range, n, s_buf[0], init, by_ids, s_ids[0], seg_rec,
+                                    seg.head, spec0, spec1, spec2);
     } else {
         if (ty * kTile + w * 8 >= A.img_h) return;  // band below the image
         if (by_ids)
             n = (A.slab && n_all > kTilePix)
                     ? wave_brute_tile_ids(A, tile, s_ids[w])
                     : wave_sorted_tile_ids(seg, n_all, s_ids[w], reinterpret_cast<unsigned *>(s_buf[w]));
-        sum_fwd_band<kMode, kIdx>(A, tile, w, range, n, s_buf[w], init, by_ids, s_ids[w], seg_rec, spec0,
-                            spec1, spec2);
+        sum_fwd_band<kMode, kIdx>(A, tile, w, range, n, s_buf[w], init, by_ids, s_ids[w], seg_rec,
+                                  seg.head, spec0, spec1, spec2);
     }
     if (kMode == kModeStamp && (threadIdx.x & 63) == 0) {
         long long *st = A.stamps + 4 * (size_t)tile;
@@ -703,6 +712,8 @@ static int check_tiles(const char *what, int bx, int by, int tbx, int tby, unsig
 void sum_fwd_args_init(SumFwdArgs &A) {
     A = SumFwdArgs{};
     A.sparse_max = g_knobs[3] > 0 ? g_knobs[3] : 8;
+    // A/B knob 10: speculative slab records per tile (default all kHeadSlots)
+    A.spec_slots = g_knobs[10] > 0 && g_knobs[10] < kHeadSlots ? g_knobs[10] : kHeadSlots;
     A.layout = kLayoutHWC;
     A.frames = 1;
 }
