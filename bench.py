@@ -416,8 +416,8 @@ def main():
                     "train_tile")
     kernels = {
         "train_tile": roof,
-        "frame_project": roofline("frame_project_kernel", project_bytes(shape, args.splats),
-                                  kt["project"], prof, "frame_project"),
+        "frame_project": roofline("frame_project_ordered_kernel", project_bytes(shape, args.splats),
+                                  kt["project"], prof, "frame_project_ordered"),
         "train_splat": roofline("train_splat_kernel", train_splat_bytes(args.splats),
                                 kt["train_splat"], prof, "train_splat"),
     }

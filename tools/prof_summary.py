@@ -23,6 +23,7 @@ import os
 from collections import defaultdict
 
 KERNELS = {"raster_sum_fwd_kernel": "rasterize_sum_forward",
+           "frame_project_ordered_kernel": "frame_project_ordered",
            "train_tile_wave_kernel": "train_tile",
            "train_tile_band_kernel": "train_tile",
            "raster_sum_bwd_kernel": "rasterize_sum_backward",
@@ -42,22 +43,24 @@ def _csvs(d, pattern):
     return sorted(glob.glob(os.path.join(d, "**", pattern), recursive=True))
 
 
-def trace_stats(d):
+def trace_stats(d, last=0):
     rows = defaultdict(list)
     for f in _csvs(d, "*kernel_trace.csv"):
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-                rows[r["Kernel_Name"]].append(dur)
+                rows[r["Kernel_Name"]].append((int(r.get("Dispatch_Id", 0) or 0), dur))
     out = {}
-    for name, durs in rows.items():
+    for name, ds in rows.items():
+        ds.sort()
+        durs = [x for _, x in (ds[-last:] if last > 0 else ds)]
         durs.sort()
         out[name] = dict(calls=len(durs), avg_us=sum(durs) / len(durs) / 1e3,
                          median_us=durs[len(durs) // 2] / 1e3, min_us=durs[0] / 1e3)
     return out
 
 
-def pmc_per_launch(d, counter):
+def pmc_per_launch(d, counter, last=0):
     vals = defaultdict(list)
     for f in _csvs(d, "*counter_collection.csv"):
         with open(f) as fh:
@@ -66,8 +69,13 @@ def pmc_per_launch(d, counter):
                     continue
                 k = _short(r["Kernel_Name"])
                 if k:
-                    vals[k].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in vals.items()}
+                    vals[k].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
+    out = {}
+    for k, v in vals.items():
+        v.sort()
+        v = v[-last:] if last > 0 else v
+        out[k] = sum(x for _, x in v) / len(v)
+    return out
 
 
 def pmc_all(dirs, last=0):
@@ -102,13 +110,13 @@ def main():
     ap.add_argument("--key", default="10000")
     ap.add_argument("--pmc-dirs", nargs="*", help="print every counter per kernel")
     ap.add_argument("--last", type=int, default=0,
-                    help="--pmc-dirs: average each kernel's last N dispatches only")
+                    help="average each kernel's last N dispatches only (trace and PMC)")
     a = ap.parse_args()
     if a.pmc_dirs:
         print(json.dumps(pmc_all(a.pmc_dirs, a.last), indent=1))
     rec = {}
     if a.trace:
-        st = trace_stats(a.trace)
+        st = trace_stats(a.trace, a.last)
         for name, s in sorted(st.items(), key=lambda kv: -kv[1]["avg_us"] * kv[1]["calls"]):
             print(f"{s['calls']:6d}  avg {s['avg_us']:9.2f} us  med {s['median_us']:9.2f}  "
                   f"min {s['min_us']:9.2f}  {name[:110]}")
@@ -116,10 +124,10 @@ def main():
             if k:
                 rec.setdefault(k, {})["trace_avg_us"] = s["avg_us"]
     if a.fetch:
-        for k, v in pmc_per_launch(a.fetch, "FETCH_SIZE").items():
+        for k, v in pmc_per_launch(a.fetch, "FETCH_SIZE", a.last).items():
             rec.setdefault(k, {})["fetch_bytes"] = 2.0 * v * 1024.0
     if a.write:
-        for k, v in pmc_per_launch(a.write, "WRITE_SIZE").items():
+        for k, v in pmc_per_launch(a.write, "WRITE_SIZE", a.last).items():
             rec.setdefault(k, {})["write_bytes"] = v * 1024.0
     if rec:
         print(json.dumps(rec, indent=1))
