@@ -48,6 +48,7 @@ struct TrainTileArgs {
     const float *gt;  // [3, H, W]
     float *grad;      // [N, 16]: v_xy 0:2, v_conic 2:5, v_colors 5:8, v_opacity 8
     float2 *err;      // [ntiles]: sum of squared, sum of absolute errors
+    int brun;         // band kernel: a rectangle row wider than this is two work items
     float *out;       // optional [3, H, W] clamped render
     long long *stamps;  // diagnostic: int64[ntiles][8]
 };
@@ -436,7 +437,7 @@ __global__ __launch_bounds__(256, 8) void train_tile_kernel(TrainTileArgs A) {
 // not formed.
 constexpr int kBSpec = 32;    // slab slots loaded with the count (64: slower, measured)
 constexpr int kBChunk = 64;   // entries staged at a time
-constexpr int kBRun = 8;      // pixels per backward work item (part of one rectangle row)
+constexpr int kBRun = 10;     // rows wider than this split into two work items (8: +4 %, 16: +3 % at trained density)
 constexpr int kBThreads = 128;
 
 typedef float v2f __attribute__((ext_vector_type(2)));
@@ -735,7 +736,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             if (rc != kNoRect) {
                 const int rw = (int)((rc >> 4) & 15u) - (int)(rc & 15u) + 1;
                 const int rh = (int)((rc >> 12) & 15u) - (int)((rc >> 8) & 15u) + 1;
-                items = rh * ((rw + kBRun - 1) / kBRun);
+                items = rh * (rw > A.brun ? 2 : 1);
             }
         }
         const int incl = wave_scan_dpp<false>(items, 0);
@@ -777,11 +778,14 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                 const unsigned ro = S.ro[own];
                 const int j = item - (int)(ro >> 16);  // item index within the entry
                 const int rx0 = (int)(ro & 15u), rx1 = (int)((ro >> 4) & 15u);
-                const int ipr = (rx1 - rx0 + kBRun) / kBRun;  // items per rectangle row (1, 2)
+                // items per rectangle row: 1, or 2 halves when it is wider than brun
+                const int rwid = rx1 - rx0 + 1;
+                const int ipr = rwid > A.brun ? 2 : 1;
                 const int jr = ipr == 1 ? j : (j >> 1);
                 const int row = (int)((ro >> 8) & 15u) + jr;
-                const int cs = rx0 + kBRun * (j - jr * ipr);
-                const int ce = min(min(cs + kBRun - 1, rx1), A.img_w - 1 - (int)tx0);
+                const int half = (rwid + 1) >> 1;
+                const int cs = ipr == 1 ? rx0 : rx0 + half * (j & 1);
+                const int ce = min(ipr == 1 ? rx1 : min(cs + half - 1, rx1), A.img_w - 1 - (int)tx0);
                 const float pyf = ty0 + (float)row;
                 if ((int)pyf < A.img_h) {
                     const float ex = G.x, eha = G.z, eb = G.w;
@@ -1131,6 +1135,8 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     T.grad = reinterpret_cast<float *>(w.grad);
     T.err = w.err;
     T.out = render_out;
+    // A/B knob 11: the band kernel's work-item split width (default kBRun)
+    T.brun = g_knobs[11] >= 4 && g_knobs[11] <= 16 ? g_knobs[11] : kBRun;
     if (g_knobs[5] == 2 && g_debug_ptr) {  // diagnostic: per-tile stamps
         T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
         auto kfn = train_tile_kernel<true>;
