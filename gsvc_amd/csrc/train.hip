@@ -49,6 +49,7 @@ struct TrainTileArgs {
     float *grad;      // [N, 16]: v_xy 0:2, v_conic 2:5, v_colors 5:8, v_opacity 8
     float2 *err;      // [ntiles]: sum of squared, sum of absolute errors
     int brun;         // band kernel: a rectangle row wider than this is two work items
+    int spec;         // band kernel: slab records loaded with the count
     float *out;       // optional [3, H, W] clamped render
     long long *stamps;  // diagnostic: int64[ntiles][8]
 };
@@ -462,6 +463,28 @@ __device__ __forceinline__ void blend2_unit(float gx, float ha, float bdy, float
     ab = (v2f){v0 ? nb.x : ab.x, v1 ? nb.y : ab.y};
 }
 
+// blend2_unit for an entry whose colour is finite: a failing pair adds
+// c * 0 (= +-0) instead of selecting -- the same bits, since an accumulator
+// is never -0 (it starts at +0 or the background, and an exact cancellation
+// rounds to +0) -- 2 selects instead of 6.  A non-finite colour times 0 is NaN,
+// so such entries keep blend2_unit.
+__device__ __forceinline__ void blend2_unit_fin(float gx, float ha, float bdy, float cq, float cr,
+                                                float cg, float cb, v2f px, v2f &ar, v2f &ag,
+                                                v2f &ab) {
+    const v2f dx = gx - px;
+    const v2f q = __builtin_elementwise_fma((v2f)ha, dx, (v2f)bdy);
+    const v2f sg = __builtin_elementwise_fma(q, dx, (v2f)cq);
+    const v2f x = sg * kNegLog2e;
+    const v2f e = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+    const v2f a = {fminf(1.0f, e.x), fminf(1.0f, e.y)};
+    const bool v0 = !(sg.x < 0.0f) && !(a.x < kAlphaMin);
+    const bool v1 = !(sg.y < 0.0f) && !(a.y < kAlphaMin);
+    const v2f av = {v0 ? a.x : 0.0f, v1 ? a.y : 0.0f};
+    ar = __builtin_elementwise_fma((v2f)cr, av, ar);
+    ag = __builtin_elementwise_fma((v2f)cg, av, ag);
+    ab = __builtin_elementwise_fma((v2f)cb, av, ab);
+}
+
 // Inclusive scans over one wave's 64 lanes with DPP (no LDS traffic):
 // row_shr 1, 2, 4, 8 inside each 16-lane row, then row_bcast 15 / 31 carry a
 // row's last lane into the rows above; ``id`` is the operation's identity.
@@ -552,7 +575,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     }
     // this tile's count and its first kBSpec slab records in the same round trip
     float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
-    if (tid < kBSpec) {
+    if (tid < A.spec) {
         const float4 *h = slab_rec(A.slab, A.ntiles, tile, tid);
         r0 = h[0];
         r1 = h[1];
@@ -571,7 +594,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
 
     // 1. the order
     if (!dense) {
-        if (tid >= kBSpec && tid < n) {
+        if (tid >= A.spec && tid < n) {
             const float4 *h = slab_rec(A.slab, A.ntiles, tile, tid);
             r0 = h[0];
             r1 = h[1];
@@ -638,13 +661,28 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             __syncthreads();
         }
         // the entries whose rectangle reaches this band, as a wave-uniform mask
-        bool keep = false;
+        bool keep = false, fin = false;
         if (lane < cnt) {
             const unsigned rc = S.ro[lane];
             keep = rc != kNoRect && (int)((rc >> 12) & 15u) >= y_lo && (int)((rc >> 8) & 15u) <= y_hi;
+            const float4 C = S.col[lane];
+            fin = __builtin_isfinite(C.y) && __builtin_isfinite(C.z) && __builtin_isfinite(C.w);
         }
         unsigned long long m = __ballot(keep);
-        if (m) {
+        const unsigned long long fm = __ballot(fin);  // entries with a finite colour
+        if (m && (m & ~fm) == 0) {
+            // every colour finite (the rule): the select-free blend
+            do {
+                const int k = __builtin_ctzll(m);
+                m &= m - 1ull;
+                const float4 G = S.geo[k];
+                const float4 C = S.col[k];
+                const float dy = G.y - py;
+                const float cq = (C.x * dy) * dy;
+                const float bdy = G.w * dy;
+                blend2_unit_fin(G.x, G.z, bdy, cq, C.y, C.z, C.w, px, ar, ag, ab);
+            } while (m);
+        } else if (m) {
             do {
                 const int k = __builtin_ctzll(m);
                 m &= m - 1ull;
@@ -1137,6 +1175,8 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     T.out = render_out;
     // A/B knob 11: the band kernel's work-item split width (default kBRun)
     T.brun = g_knobs[11] >= 4 && g_knobs[11] <= 16 ? g_knobs[11] : kBRun;
+    // A/B knob 12: speculative slab records per tile (default kBSpec)
+    T.spec = g_knobs[12] > 0 && g_knobs[12] <= 64 ? g_knobs[12] : kBSpec;
     if (g_knobs[5] == 2 && g_debug_ptr) {  // diagnostic: per-tile stamps
         T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
         auto kfn = train_tile_kernel<true>;
