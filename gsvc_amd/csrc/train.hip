@@ -50,6 +50,7 @@ struct TrainTileArgs {
     float2 *err;      // [ntiles]: sum of squared, sum of absolute errors
     int brun;         // band kernel: a rectangle row wider than this is two work items
     int spec;         // band kernel: slab records loaded with the count
+    int diag;         // diagnostic knob 13 (timing experiments only; wrong results)
     float *out;       // optional [3, H, W] clamped render
     long long *stamps;  // diagnostic: int64[ntiles][8]
 };
@@ -834,7 +835,9 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                     const float fa = 2.0f * eha;
                     for (int col = cs; col <= ce; ++col) {
                         const float pxf = tx0 + (float)col;
-                        const int pix = row * kVRow + col;
+                        // (diagnostic knob 13 = 1: a conflict-free read pattern, wrong
+                        // results -- isolates the LDS cost of these reads)
+                        const int pix = (A.diag & 1) ? (tid & 255) : row * kVRow + col;
                         const float Px = S.v[0][pix], Py = S.v[1][pix], Pz = S.v[2][pix];
                         const float dx = ex - pxf;
                         const float sgm = fmaf(fmaf(eha, dx, bdy), dx, cq);
@@ -1177,6 +1180,7 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     T.brun = g_knobs[11] >= 4 && g_knobs[11] <= 16 ? g_knobs[11] : kBRun;
     // A/B knob 12: speculative slab records per tile (default kBSpec)
     T.spec = g_knobs[12] > 0 && g_knobs[12] <= 64 ? g_knobs[12] : kBSpec;
+    T.diag = g_knobs[13];
     if (g_knobs[5] == 2 && g_debug_ptr) {  // diagnostic: per-tile stamps
         T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
         auto kfn = train_tile_kernel<true>;

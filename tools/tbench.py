@@ -30,10 +30,17 @@ def main():
                     help="two 8-row bands per tile (production) or the 256-thread kernel (knob 8 = 1)")
     ap.add_argument("--knob", action="append", default=[],
                     help="A/B knob K=V (gsvc_debug_set), repeatable")
+    ap.add_argument("--knob-after", action="append", default=[],
+                    help="knob K=V set only after the warmup (diagnostic variants that change "
+                         "results must not steer the training state being measured)")
     ap.add_argument("--proj-stamps", action="store_true",
                     help="also stamp the projection kernel's waves (start, projected, inserted, end)")
     ap.add_argument("--order-every", type=int, default=None,
                     help="steps between splat-order sorts (gsvc_amd.train.ORDER_REFRESH_EVERY; 0: none)")
+    ap.add_argument("--frozen", type=int, default=0,
+                    help="after the warmup, time N gradient-only fused steps (grads_out: no "
+                         "parameter update), so kernel variants are compared on one fixed state; "
+                         "prints the tile kernel's event average")
     ap.add_argument("--shape", action="store_true",
                     help="also report N_vis, M, M_eff of the trained frame (op-path binning)")
     ap.add_argument("--channels", action="store_true",
@@ -56,6 +63,33 @@ def main():
     for it in range(1, a.warmup + 1):
         model.train_iter(gt, it)
     torch.cuda.synchronize()
+    for kv in a.knob_after:
+        k, v = kv.split("=")
+        _lib.load().gsvc_debug_set(int(k), int(v))
+    if a.frozen:
+        from gsvc_amd import ops
+        from gsvc_amd.train import train_step_sum
+        P = model._parameters
+        rgbw = model._buffers.get("rgb_W") if "rgb_W" not in P else P["rgb_W"]
+        gout = torch.empty((a.splats, 9), device=dev)
+        gtc = gt.reshape(-1).contiguous()
+
+        def gstep():
+            train_step_sum(P["_xyz"].data, P["_cholesky"].data, P["_features_dc"].data,
+                           rgbw.data if rgbw is not None else None, False,
+                           model._buffers["cholesky_bound"], model._buffers["background"], gtc,
+                           H, W, grads_out=gout)
+        for _ in range(10):
+            gstep()
+        ops.channel_timing("train_tile", True, max_launches=a.frozen, every=1, dispatch=True)
+        for _ in range(a.frozen):
+            gstep()
+        torch.cuda.synchronize()
+        ts = ops.channel_times_ms("train_tile", a.frozen)
+        ops.channel_timing("train_tile", False)
+        print(json.dumps(dict(frozen_steps=a.frozen, knobs=a.knob + a.knob_after,
+                              train_tile_us=round(1e3 * sum(ts) / len(ts), 2))), flush=True)
+        return
     t0 = time.perf_counter()
     psnr = 0.0
     blocks = []
