@@ -62,6 +62,8 @@ _SIGS = {
     "gsvc_render_frame_zeroed_bytes": [_U, _U],
     "gsvc_render_frame_sum": [_I, _P, _I, _P, _P, _P, _P, _P, _P, _U, _U, _I, _I, _P, _P, _SZ, _P,
                               _P],
+    "gsvc_render_frame_sum_ex": [_I, _P, _I, _P, _P, _P, _P, _P, _P, _U, _U, _I, _I, _P, _P, _SZ,
+                                 _P, _P, _I],
     "gsvc_train_step_workspace_bytes": [_I, _U, _U],
     "gsvc_train_step_sum_args": [_P],
     "gsvc_train_step_sum": [_I, _P, _P, _P, _P, _P, _I, _P, _P, _U, _U, _I, _I, _P, _P, _I, _P, _P,

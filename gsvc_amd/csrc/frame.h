@@ -40,6 +40,10 @@ struct FrameWs {
     float2 *xys;       // [N] (N = splats of all F frames)
     int *radii;        // [N]
     float4 *rec;       // [N][3] splat records
+    // single frame only (F = 1): the splat order (SplatOrder) -- strip keys and
+    // ids written by a refreshing call's projection, radix-sorted into order
+    unsigned *okey, *skey, *kbuf, *sort_counts, *sort_offsets;
+    int *okey_id, *order, *vbuf;
     size_t zeroed, bytes;
 };
 FrameWs frame_ws(char *base, int n, int ntiles, int frames = 1);
@@ -77,5 +81,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
                          const SplatOrder *ord = nullptr);
 // Bits of the strip keys at this image size (invisible splats: the largest).
 int strip_key_bits(int tbx, int tby);
+// Sort the keys a refreshing projection wrote into w.order (F = 1 workspaces).
+int splat_order_sort(const FrameWs &w, int n, int tbx, int tby, hipStream_t s);
 
 }  // namespace gsvc

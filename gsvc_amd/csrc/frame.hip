@@ -25,6 +25,7 @@
 // Counts and M live in two parity slots used on alternate frames
 // (frame_index & 1): each frame clears the other parity, which the previous
 // frame has finished with.  Nothing is read back to the host.
+#include "binning.h"
 #include "frame.h"
 #include "project2d.h"
 #include "raster_sum.h"
@@ -467,8 +468,29 @@ FrameWs frame_ws(char *base, int n, int ntiles, int frames) {
     w.xys = (float2 *)take(sizeof(float2) * nn);
     w.radii = (int *)take(sizeof(int) * nn);
     w.rec = (float4 *)take(sizeof(float4) * 3 * nn);
+    w.okey = w.skey = w.kbuf = w.sort_counts = w.sort_offsets = nullptr;
+    w.okey_id = w.order = w.vbuf = nullptr;
+    if (nf == 1) {
+        w.okey = (unsigned *)take(sizeof(unsigned) * nn);
+        w.skey = (unsigned *)take(sizeof(unsigned) * nn);
+        w.kbuf = (unsigned *)take(sizeof(unsigned) * nn);
+        w.okey_id = (int *)take(sizeof(int) * nn);
+        w.order = (int *)take(sizeof(int) * nn);
+        w.vbuf = (int *)take(sizeof(int) * nn);
+        const size_t cb = sort_u32_counts_bytes(n > 0 ? n : 1);
+        w.sort_counts = (unsigned *)take(cb);
+        w.sort_offsets = (unsigned *)take(cb);
+    }
     w.bytes = off;
     return w;
+}
+
+int splat_order_sort(const FrameWs &w, int n, int tbx, int tby, hipStream_t s) {
+    if (n <= 0) return GSVC_OK;
+    if (!w.order) return set_error(GSVC_ERR_ARG, "splat order: a multi-frame workspace has none");
+    // ids by strip key (stable: ties in id order)
+    return sort_u32_pairs(n, w.okey, w.okey_id, w.skey, w.order, w.kbuf, w.vbuf,
+                          strip_key_bits(tbx, tby), w.sort_counts, w.sort_offsets, s);
 }
 
 FrameSlots frame_slots(const FrameWs &w, int ntiles, int frame_index) {
@@ -579,7 +601,8 @@ static int render_frames(int frames, const int *frame_off_host, const int *frame
                          const float *cholesky_bound, const float *features, const float *rgb_w,
                          const float *opacity, const float *background, unsigned img_height,
                          unsigned img_width, int frame_index, int density_hint, int *meta,
-                         void *workspace, size_t workspace_bytes, float *out, hipStream_t s) {
+                         void *workspace, size_t workspace_bytes, float *out, hipStream_t s,
+                         int flags = 0) {
     const int tbx = ceil_div((int)img_width, kTile), tby = ceil_div((int)img_height, kTile);
     const int ntiles = tbx * tby;
     const FrameWs w = frame_ws((char *)workspace, num_points, ntiles, frames);
@@ -597,9 +620,18 @@ static int render_frames(int frames, const int *frame_off_host, const int *frame
         }
     }
     const FrameSlots f = frame_slots(w, ntiles, frame_index);
+    // GSVC_TRAIN_ORDER / _REFRESH (single frame): the training path's splat order
+    const bool use_order = frames == 1 && (flags & GSVC_TRAIN_ORDER) != 0;
+    const bool refresh = frames == 1 && (flags & GSVC_TRAIN_ORDER_REFRESH) != 0 && num_points > 0;
+    SplatOrder ord;
+    ord.order = use_order ? w.order : nullptr;
+    if (refresh) {
+        ord.key = w.okey;
+        ord.key_id = w.okey_id;
+    }
     int rc = frame_project_launch(num_points, xyz, xyz_tanh, cholesky, cholesky_bound, features,
                                   rgb_w, opacity, img_height, img_width, w, f, nullptr, s, frames,
-                                  frame_off_dev, max_n);
+                                  frame_off_dev, max_n, (use_order || refresh) ? &ord : nullptr);
     if (rc) return rc;
     SumFwdArgs A;
     sum_fwd_args_init(A);
@@ -628,7 +660,9 @@ static int render_frames(int frames, const int *frame_off_host, const int *frame
         A.slab_stride = slab_frame_f4(ntiles);
         A.out_stride = (size_t)3 * img_width * img_height;
     }
-    return sum_forward_launch(A, density_hint, s);
+    rc = sum_forward_launch(A, density_hint, s);
+    if (rc || !refresh) return rc;
+    return splat_order_sort(w, num_points, tbx, tby, s);
 }
 
 }  // namespace gsvc
@@ -673,6 +707,26 @@ extern "C" size_t gsvc_render_frame_workspace_bytes(int num_points, unsigned img
 
 extern "C" size_t gsvc_render_frame_zeroed_bytes(unsigned img_height, unsigned img_width) {
     return frame_ws(nullptr, 1, tiles_of(img_height, img_width)).zeroed;
+}
+
+extern "C" int gsvc_render_frame_sum_ex(int num_points, const float *xyz, int xyz_tanh,
+                                        const float *cholesky, const float *cholesky_bound,
+                                        const float *features, const float *rgb_w,
+                                        const float *opacity, const float *background,
+                                        unsigned img_height, unsigned img_width, int frame_index,
+                                        int density_hint, int *meta, void *workspace,
+                                        size_t workspace_bytes, float *out, void *stream,
+                                        int flags) {
+    if (num_points < 0 || img_height == 0 || img_width == 0)
+        return set_error(GSVC_ERR_ARG, "render_frame_sum: bad sizes");
+    if ((num_points > 0 && (!xyz || !cholesky || !features)) || !background || !meta || !out)
+        return set_error(GSVC_ERR_ARG, "render_frame_sum: missing input");
+    if (flags & ~(GSVC_TRAIN_ORDER | GSVC_TRAIN_ORDER_REFRESH))
+        return set_error(GSVC_ERR_ARG, "render_frame_sum_ex: unknown flags");
+    return render_frames(1, nullptr, nullptr, num_points, xyz, xyz_tanh, cholesky, cholesky_bound,
+                         features, rgb_w, opacity, background, img_height, img_width, frame_index,
+                         density_hint, meta, workspace, workspace_bytes, out, (hipStream_t)stream,
+                         flags);
 }
 
 extern "C" int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_tanh,

@@ -1063,13 +1063,9 @@ __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
 }
 
 struct TrainWs {
-    FrameWs f;
+    FrameWs f;  // with the splat order buffers (GSVC_TRAIN_ORDER)
     float4 *grad;
     float2 *err;
-    // the splat order (GSVC_TRAIN_ORDER): strip keys + ids written by a
-    // refreshing call's projection, sorted into ``order`` after its step
-    unsigned *okey, *skey, *kbuf, *sort_counts, *sort_offsets;
-    int *okey_id, *order, *vbuf;
     size_t bytes;
 };
 
@@ -1085,15 +1081,6 @@ static TrainWs train_ws(char *base, int n, int ntiles) {
     };
     w.grad = (float4 *)take(sizeof(float4) * 4 * nn);
     w.err = (float2 *)take(sizeof(float2) * nt);
-    w.okey = (unsigned *)take(sizeof(unsigned) * nn);
-    w.skey = (unsigned *)take(sizeof(unsigned) * nn);
-    w.kbuf = (unsigned *)take(sizeof(unsigned) * nn);
-    w.okey_id = (int *)take(sizeof(int) * nn);
-    w.order = (int *)take(sizeof(int) * nn);
-    w.vbuf = (int *)take(sizeof(int) * nn);
-    const size_t cb = sort_u32_counts_bytes(n > 0 ? n : 1);
-    w.sort_counts = (unsigned *)take(cb);
-    w.sort_offsets = (unsigned *)take(cb);
     w.bytes = off;
     return w;
 }
@@ -1145,10 +1132,10 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     const bool use_order = (adan_flags & GSVC_TRAIN_ORDER) != 0;
     const bool refresh = (adan_flags & GSVC_TRAIN_ORDER_REFRESH) != 0 && num_points > 0;
     SplatOrder ord;
-    ord.order = use_order ? w.order : nullptr;
+    ord.order = use_order ? w.f.order : nullptr;
     if (refresh) {
-        ord.key = w.okey;
-        ord.key_id = w.okey_id;
+        ord.key = w.f.okey;
+        ord.key_id = w.f.okey_id;
     }
     int rc = frame_project_launch(num_points, xyz, 1, cholesky, cholesky_bound, features, rgb_w,
                                   nullptr, img_height, img_width, w.f, f, w.grad, s, 1, nullptr, 0,
@@ -1237,9 +1224,7 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     timing_end(s, tslot, kTimingTrainSplat);
     rc = check_launch("train_step_sum: splats");
     if (rc || !refresh) return rc;
-    // the next calls' order: ids by strip key (stable: ties in id order)
-    return sort_u32_pairs(num_points, w.okey, w.okey_id, w.skey, w.order, w.kbuf, w.vbuf,
-                          strip_key_bits(tbx, tby), w.sort_counts, w.sort_offsets, s);
+    return splat_order_sort(w.f, num_points, tbx, tby, s);  // the next calls' order
 }
 
 extern "C" int gsvc_train_step_sum_args(const gsvc_train_step_args *a) {

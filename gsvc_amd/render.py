@@ -42,6 +42,8 @@ class _FrameWorkspace:
         self.frame = 0
         self.hint = _LazyCount()
         self.shape = None
+        self.order_for = None  # the splat order (train.order_flags)
+        self.order_age = 0
 
 
 _workspaces = {}
@@ -70,10 +72,16 @@ def _workspace(dev: torch.device, n: int, H: int, W: int) -> _FrameWorkspace:
         fw.frame = 0
         fw.hw = (H, W)
         fw.dirty = False
+        fw.order_for = None
     return fw
 
 
 _F32 = torch.float32
+
+
+def _order_flags(fw) -> int:
+    from .train import order_flags
+    return order_flags(fw)
 
 
 def _ptr_f32(t: Optional[Tensor], name: str, numel: int, keep: list) -> int:
@@ -97,9 +105,11 @@ _render_fn = None
 
 
 def _render_frame_fn():
+    """gsvc_render_frame_sum_ex: the frame render with the training path's
+    splat order (projection in spatial order, windowed slot atomics)."""
     global _render_fn
     if _render_fn is None:
-        _render_fn = L.load().gsvc_render_frame_sum
+        _render_fn = L.load().gsvc_render_frame_sum_ex
     return _render_fn
 
 
@@ -135,7 +145,8 @@ class BoundRender:
         out = torch.empty((1, 3, H, W), dtype=_F32, device=self.dev)
         p = self.p
         rc = self.fn(n, p[0], 1, p[1], p[4], p[2], p[5], 0, p[3], H, W, fw.frame, fw.hint.value,
-                     fw.meta_ptr, fw.buf_ptr, fw.buf.numel(), out.data_ptr(), fw.stream)
+                     fw.meta_ptr, fw.buf_ptr, fw.buf.numel(), out.data_ptr(), fw.stream,
+                     _order_flags(fw))
         if rc != 0:
             fw.dirty = True
             msg = L.load().gsvc_last_error().decode(errors="replace")
@@ -170,7 +181,7 @@ def render_frame_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, img_height
     rc = _render_frame_fn()(
         n, p_xyz, 1 if xyz_tanh else 0, p_chol, p_bound, p_feat, p_rgbw, p_opac, p_bg, H, W,
         fw.frame, fw.hint.value, fw.meta_ptr, fw.buf_ptr, fw.buf.numel(), out.data_ptr(),
-        fw.stream)
+        fw.stream, _order_flags(fw))
     if rc != 0:
         fw.dirty = True
         msg = L.load().gsvc_last_error().decode(errors="replace")

@@ -39,20 +39,26 @@ class _TrainWorkspace:
         self.order_age = 0     # steps since it was sorted
 
     def order_flags(self) -> int:
-        """GSVC_TRAIN_ORDER when a valid order exists, GSVC_TRAIN_ORDER_REFRESH
-        every ORDER_REFRESH_EVERY steps (splats drift; a stale order costs
-        speed only)."""
-        if ORDER_REFRESH_EVERY <= 0:
-            return 0
-        flags = 0
-        if self.order_for == self.shape:
-            flags |= TRAIN_ORDER
-            self.order_age += 1
-        if self.order_for != self.shape or self.order_age >= ORDER_REFRESH_EVERY:
-            flags |= TRAIN_ORDER_REFRESH
-            self.order_for = self.shape
-            self.order_age = 0
-        return flags
+        return order_flags(self)
+
+
+def order_flags(ws) -> int:
+    """For a workspace ``ws`` with ``shape`` (n, H, W), ``order_for`` and
+    ``order_age``: GSVC_TRAIN_ORDER when it holds a valid order (sorted for the
+    same n and image size), GSVC_TRAIN_ORDER_REFRESH every ORDER_REFRESH_EVERY
+    calls (splats drift; a stale order costs speed only: any permutation of
+    the splats gives the same results)."""
+    if ORDER_REFRESH_EVERY <= 0:
+        return 0
+    flags = 0
+    if ws.order_for == ws.shape:
+        flags |= TRAIN_ORDER
+        ws.order_age += 1
+    if ws.order_for != ws.shape or ws.order_age >= ORDER_REFRESH_EVERY:
+        flags |= TRAIN_ORDER_REFRESH
+        ws.order_for = ws.shape
+        ws.order_age = 0
+    return flags
 
 
 _workspaces = {}

@@ -287,6 +287,16 @@ int gsvc_render_frame_sum(int num_points, const float *xyz, int xyz_tanh,
                           unsigned img_height, unsigned img_width, int frame_index,
                           int density_hint, int *meta, void *workspace,
                           size_t workspace_bytes, float *out, void *stream);
+/* The same with ``flags``: GSVC_TRAIN_ORDER / GSVC_TRAIN_ORDER_REFRESH (below)
+ * project in / refresh the workspace's splat order, as the training step does
+ * (speed only: the same image).  Not part of the reference. */
+int gsvc_render_frame_sum_ex(int num_points, const float *xyz, int xyz_tanh,
+                             const float *cholesky, const float *cholesky_bound,
+                             const float *features, const float *rgb_w,
+                             const float *opacity, const float *background,
+                             unsigned img_height, unsigned img_width, int frame_index,
+                             int density_hint, int *meta, void *workspace,
+                             size_t workspace_bytes, float *out, void *stream, int flags);
 
 /* ---------------------------------------------------------------------------
  * Fused training step of GSVC's per-frame model: one

@@ -244,6 +244,30 @@ def test_render_frame_matches_op_path(cuda, oracle, mode, case):
     assert torch.equal(fast, ref)
 
 
+@pytest.mark.parametrize("case", ["sum_trained_like_48x80_n200", "1080p_50k", "1080p_50k_big"])
+def test_render_frame_splat_order(cuda, oracle, case, monkeypatch):
+    """The render with the training path's splat order (gsvc_render_frame_sum_ex:
+    a refreshing call, then ordered calls with windowed slot atomics, large
+    splats inserting directly) is bit-identical to the op path, call after call."""
+    from gsvc_amd import train as Tr
+    from gsvc_amd.render import render_sum_frame
+    if case.startswith("sum_"):
+        z = load_golden(case)
+        H, W = int(z["H"]), int(z["W"])
+        means, L, colors, opac = z["means2d"], z["L"], z["colors"], z["opacity"]
+    else:
+        H, W, n = 1080, 1920, 50000
+        means, L, colors, opac = oracle.synthetic_frame(n, seed=n + 5, rgb_w=2.0,
+                                                        chol_scale=6.0 if case.endswith("big") else 1.0)
+    bg = torch.ones(3, device="cuda")
+    with torch.no_grad():
+        ref = _op_path_frame(T(means), T(L), T(colors), T(opac), H, W, bg)
+    monkeypatch.setattr(Tr, "ORDER_REFRESH_EVERY", 3)
+    for _ in range(7):  # refresh, ordered, ordered, refresh + ordered, ...
+        fast = render_sum_frame(T(means), T(L), T(colors), T(opac), H, W, _tb(H, W), bg)
+        assert torch.equal(fast, ref)
+
+
 def test_render_frame_empty_is_background(cuda):
     from gsvc_amd.render import render_sum_frame
     z = load_golden("sum_empty_32x32_n10")
