@@ -82,6 +82,8 @@ class Adan(Optimizer):
             with torch.enable_grad():
                 loss = closure()
         from . import ops
+        from .train import bump_param_epoch
+        bump_param_epoch()  # a fused step's projection enqueued ahead is stale now
         clip = self._clip_factor()
         for group in self.param_groups:
             live = [p for p in group["params"] if p.grad is not None]

@@ -1137,10 +1137,34 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
         ord.key = w.f.okey;
         ord.key_id = w.f.okey_id;
     }
-    int rc = frame_project_launch(num_points, xyz, 1, cholesky, cholesky_bound, features, rgb_w,
+    // Where this call's one projection goes (GSVC_TRAIN_PROJECT_*): first, for
+    // this frame (default); none (PROJECTED: an earlier call's PROJECT_NEXT
+    // already enqueued it); only (PROJECT_ONLY); or last, for frame_index + 1
+    // with the parameters this step updates (PROJECT_NEXT).
+    const bool projected = (adan_flags & GSVC_TRAIN_PROJECTED) != 0;
+    const bool only = (adan_flags & GSVC_TRAIN_PROJECT_ONLY) != 0;
+    const bool next = (adan_flags & GSVC_TRAIN_PROJECT_NEXT) != 0;
+    if ((only && (projected || next)) || (next && !projected))
+        return set_error(GSVC_ERR_ARG, "train_step_sum: PROJECT_ONLY excludes the other "
+                                       "projection flags; PROJECT_NEXT needs PROJECTED");
+    if (next && !update)
+        return set_error(GSVC_ERR_ARG, "train_step_sum: PROJECT_NEXT needs the Adan update");
+    auto project = [&](const FrameSlots &fs) {
+        int r = frame_project_launch(num_points, xyz, 1, cholesky, cholesky_bound, features, rgb_w,
+                                     nullptr, img_height, img_width, w.f, fs, w.grad, s, 1,
+                                     nullptr, 0, (use_order || refresh) ? &ord : nullptr);
+        if (r || !refresh) return r;
+        return splat_order_sort(w.f, num_points, tbx, tby, s);  // the next calls' order
+    };
+    int rc = GSVC_OK;
+    if (!projected) {
+        // a refreshing projection's sort runs after the step (off the loss's path)
+        rc = frame_project_launch(num_points, xyz, 1, cholesky, cholesky_bound, features, rgb_w,
                                   nullptr, img_height, img_width, w.f, f, w.grad, s, 1, nullptr, 0,
                                   (use_order || refresh) ? &ord : nullptr);
-    if (rc) return rc;
+        if (rc) return rc;
+        if (only) return refresh ? splat_order_sort(w.f, num_points, tbx, tby, s) : GSVC_OK;
+    }
 
     const double count = 3.0 * (double)img_height * (double)img_width;  // numel of [3, H, W]
     TrainTileArgs T{};
@@ -1223,8 +1247,10 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     launch_timed(train_splat_kernel, dim3(blocks), dim3(256), 0, s, tev, P);
     timing_end(s, tslot, kTimingTrainSplat);
     rc = check_launch("train_step_sum: splats");
-    if (rc || !refresh) return rc;
-    return splat_order_sort(w.f, num_points, tbx, tby, s);  // the next calls' order
+    if (rc) return rc;
+    if (next) return project(frame_slots(w.f, ntiles, frame_index + 1));
+    if (!projected && refresh) return splat_order_sort(w.f, num_points, tbx, tby, s);
+    return GSVC_OK;
 }
 
 extern "C" int gsvc_train_step_sum_args(const gsvc_train_step_args *a) {

@@ -157,6 +157,8 @@ class GaussianVideoFrame(nn.Module):
         return {"render": out_img}
 
     def update_optimizer(self):
+        from .train import bump_param_epoch
+        bump_param_epoch()  # new parameters / optimizer: nothing projected ahead applies
         if self.opt_type == "adam":
             self.optimizer = torch.optim.Adam(self.parameters(), lr=self.lr)
         else:

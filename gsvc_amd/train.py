@@ -25,6 +25,25 @@ TRAIN_LOSS_SEQ = 0x100  # include/gsvc_amd.h GSVC_TRAIN_LOSS_SEQ
 TRAIN_ORDER = 0x200  # GSVC_TRAIN_ORDER
 TRAIN_ORDER_REFRESH = 0x400  # GSVC_TRAIN_ORDER_REFRESH
 ORDER_REFRESH_EVERY = 64  # fused steps between splat-order sorts (0: no order)
+TRAIN_PROJECT_ONLY = 0x800  # GSVC_TRAIN_PROJECT_ONLY
+TRAIN_PROJECTED = 0x1000  # GSVC_TRAIN_PROJECTED
+TRAIN_PROJECT_NEXT = 0x2000  # GSVC_TRAIN_PROJECT_NEXT
+PROJECT_AHEAD = True  # a bound step enqueues the next step's projection after itself
+
+# A step's projection of the NEXT frame is used only if nothing could have
+# changed the parameters since: no other fused launch anywhere (_launch_count),
+# no optimizer step or control of ours (_param_epoch, bump_param_epoch), no
+# in-place op through the bound Parameters (their _version), the same bound
+# step and workspace frame.  (In-place writes through ``.data`` bypass
+# _version; call bump_param_epoch() after such writes.)
+_launch_count = [0]
+_param_epoch = [0]
+
+
+def bump_param_epoch() -> None:
+    """Parameters changed outside the fused step: discard any projection a
+    bound step enqueued ahead."""
+    _param_epoch[0] += 1
 
 
 class _TrainWorkspace:
@@ -37,6 +56,7 @@ class _TrainWorkspace:
         self.shape = None
         self.order_for = None  # (n, H, W) the workspace's splat order was sorted for
         self.order_age = 0     # steps since it was sorted
+        self.pending = None    # the projection a bound step enqueued ahead (BoundStep.launch)
 
     def order_flags(self) -> int:
         return order_flags(self)
@@ -79,12 +99,13 @@ def _workspace(dev: torch.device, n: int, H: int, W: int) -> _TrainWorkspace:
         ws.buf_ptr = ws.buf.data_ptr()
         ws.dirty = True
     if ws.dirty or ws.hw != (H, W):
-        # per-tile counters and M slots start at zero; every call leaves them zero
+        # per-tile counters and M slots start at zero; every call leaves them zero.
+        # The frame counter keeps counting (it also numbers the loss read-backs).
         ws.buf[: L.size("gsvc_render_frame_zeroed_bytes", H, W)].zero_()
-        ws.frame = 0
         ws.hw = (H, W)
         ws.dirty = False
         ws.order_for = None
+        ws.pending = None
     return ws
 
 
@@ -157,6 +178,7 @@ class BoundStep:
         self.host = None  # coherent host words: mse, l1, sequence
         self.seq = 0
         self.stream = None
+        self.params = tuple(t for t in (xyz, cholesky, features, rgb_w) if t is not None)
 
     def __del__(self):
         if getattr(self, "host", None) is not None:
@@ -196,10 +218,33 @@ class BoundStep:
             self.host_f = (ctypes.c_float * 4).from_address(self.host)
             a.loss = self.host
         self.stream = _raw_stream(self.dev.index)
+        flags = int(adan_flags) | TRAIN_LOSS_SEQ
+        if PROJECT_AHEAD:
+            versions = tuple(t._version for t in self.params)
+            pend = ws.pending
+            ahead = (pend is not None and pend[0] is self and pend[1] == ws.frame
+                     and pend[2] == _launch_count[0] and pend[3] == _param_epoch[0]
+                     and pend[4] == versions)
+            if pend is not None and not ahead:
+                # an enqueued projection that cannot be used: its counts are in
+                # the workspace -- start from zeroed counters
+                ws.dirty = True
+                ws = _workspace(self.dev, self.n, self.H, self.W)
+            if not ahead:
+                self._call(ws, lib, gt, int(adan_flags) | TRAIN_PROJECT_ONLY | ws.order_flags())
+            flags |= TRAIN_PROJECTED | TRAIN_PROJECT_NEXT
         self.seq = ((ws.frame + 1) & 0xFFFFFFFF) | 0x80000000
+        self._call(ws, lib, gt, flags | ws.order_flags())
+        _launch_count[0] += 1
+        if PROJECT_AHEAD:
+            ws.pending = (self, ws.frame + 1, _launch_count[0], _param_epoch[0], versions)
+        ws.frame += 1
+
+    def _call(self, ws, lib, gt, flags):
+        a = self.args
         a.gt = gt.data_ptr()
         a.frame_index = ws.frame
-        a.adan_flags = int(adan_flags) | TRAIN_LOSS_SEQ | ws.order_flags()
+        a.adan_flags = flags
         a.workspace = ws.buf_ptr
         a.workspace_bytes = ws.buf.numel()
         a.stream = self.stream
@@ -208,7 +253,6 @@ class BoundStep:
             ws.dirty = True
             msg = lib.gsvc_last_error().decode(errors="replace")
             raise RuntimeError(f"gsvc_train_step_sum failed (status {rc}): {msg}")
-        ws.frame += 1
 
     def result(self):
         """(mean squared error, mean absolute error) of the last launched step:
@@ -256,6 +300,10 @@ def train_step_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, rgb_w: Optio
             state[k] = _f32_ptr(t, "adan_state", numels[k // 4]) or None
     hp = (ctypes.c_double * 10)(*[float(x) for x in (list(adan_hparams) or [0.0] * 10)])
     ws = _workspace(dev, n, H, W)
+    if ws.pending is not None:  # a bound step's projection ahead: not for this call
+        ws.dirty = True
+        ws = _workspace(dev, n, H, W)
+    _launch_count[0] += 1
     loss = torch.empty((2,), dtype=torch.float32, device=dev)
     rc = L.load().gsvc_train_step_sum(
         n, p_xyz, p_chol, p_bound, p_feat, p_rgbw, 1 if rgb_w_trainable else 0, p_bg, p_gt, H, W,

@@ -340,6 +340,19 @@ int gsvc_render_frame_sum_ex(int num_points, const float *xyz, int xyz_tanh,
  * GSVC_TRAIN_ORDER_REFRESH sorts a new one from this call's positions. */
 #define GSVC_TRAIN_ORDER 0x200
 #define GSVC_TRAIN_ORDER_REFRESH 0x400
+/* Projection placement (speed only): by default a call projects its frame
+ * first.  GSVC_TRAIN_PROJECT_ONLY: project frame_index and return (the order
+ * flags apply to it).  GSVC_TRAIN_PROJECTED: this frame's projection was
+ * already enqueued on the stream by the previous call's
+ * GSVC_TRAIN_PROJECT_NEXT, which (requiring PROJECTED) enqueues the projection
+ * of frame_index + 1 -- from the parameters this step updates -- after the
+ * step, so it follows the step on the device without waiting for the host; the
+ * order flags then apply to that projection.  The caller guarantees that
+ * nothing changes the parameters between the two calls (or discards the
+ * pending projection by re-zeroing the workspace). */
+#define GSVC_TRAIN_PROJECT_ONLY 0x800
+#define GSVC_TRAIN_PROJECTED 0x1000
+#define GSVC_TRAIN_PROJECT_NEXT 0x2000
 size_t gsvc_train_step_workspace_bytes(int num_points, unsigned img_height,
                                        unsigned img_width);
 int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,

@@ -91,3 +91,58 @@ def test_train_iter_fused_render_agrees(cuda):
     with torch.no_grad():
         fast = model()["render"]
     assert torch.equal(fast, model()["render"].detach())
+
+
+def _ahead_run(cuda, ahead, edits):
+    """20 fused train_iter steps at 256x256 / 2000 splats with the next step's
+    projection enqueued ahead (or not); ``edits`` maps step -> an in-place change
+    of the parameters made between two steps."""
+    from gsvc_amd import train as Tr
+    from gsvc_amd.frame import make_frame_model, synthetic_gt
+    old = Tr.PROJECT_AHEAD
+    Tr.PROJECT_AHEAD = ahead
+    try:
+        model = make_frame_model(256, 256, 2000, cuda, seed=3)
+        gt = synthetic_gt(256, 256, 4, cuda)
+        losses = []
+        for it in range(1, 21):
+            if it in edits:
+                edits[it](model)
+            loss, _ = model.train_iter(gt, it)
+            losses.append(float(loss))
+        assert model.fused_steps == 20
+        return np.array(losses), model._xyz.detach().clone()
+    finally:
+        Tr.PROJECT_AHEAD = old
+
+
+def test_projection_ahead_matches_and_honours_edits(cuda):
+    """The fused step's projection of the next frame, enqueued ahead, gives the
+    same trajectory as projecting at the start of each step, and is discarded
+    when the parameters change in between: an in-place op through the
+    Parameter (its _version), a write through .data announced with
+    bump_param_epoch, and an optimizer step of the op path."""
+    from gsvc_amd.train import bump_param_epoch
+
+    def via_param(m):
+        with torch.no_grad():
+            m._xyz.add_(0.02)
+
+    def via_data(m):
+        m._xyz.data.mul_(0.99)
+        bump_param_epoch()
+
+    def via_optimizer(m):
+        m._features_dc.grad = torch.full_like(m._features_dc, 0.1)
+        m.optimizer.step()
+        m.optimizer.zero_grad(set_to_none=True)
+
+    edits = {6: via_param, 11: via_data, 16: via_optimizer}
+    la, xa = _ahead_run(cuda, True, dict(edits))
+    lb, xb = _ahead_run(cuda, False, dict(edits))
+    # float atomics in the backward: equal up to their summation order
+    np.testing.assert_allclose(la, lb, rtol=2e-5, atol=1e-8)
+    np.testing.assert_allclose(xa.cpu().numpy(), xb.cpu().numpy(), rtol=1e-3, atol=1e-4)
+    # the edits matter: without them the trajectory differs clearly
+    lc, _ = _ahead_run(cuda, True, {})
+    assert np.abs(lc[6:] - la[6:]).max() > 1e-4
