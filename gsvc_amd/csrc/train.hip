@@ -50,7 +50,9 @@ struct TrainTileArgs {
     float2 *err;      // [ntiles]: sum of squared, sum of absolute errors
     int brun;         // band kernel: a rectangle row wider than this is two work items
     int spec;         // band kernel: slab records loaded with the count
-    int diag;         // diagnostic knob 13 (timing experiments only; wrong results)
+    int diag;         // diagnostic knob 13 (timing experiments only; wrong results):
+                      // bits 1 conflict-free v_out reads, 2 no backward, 4 no forward
+                      // blending, 8 no backward pixel work, 16 no run sums, 32 no atomics
     float *out;       // optional [3, H, W] clamped render
     long long *stamps;  // diagnostic: int64[ntiles][8]
 };
@@ -670,6 +672,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             fin = __builtin_isfinite(C.y) && __builtin_isfinite(C.z) && __builtin_isfinite(C.w);
         }
         unsigned long long m = __ballot(keep);
+        if (A.diag & 4) m = 0ull;  // diagnostic: no forward blending (wrong results)
         const unsigned long long fm = __ballot(fin);  // entries with a finite colour
         if (m && (m & ~fm) == 0) {
             // every colour finite (the rule): the select-free blend
@@ -756,6 +759,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     }
     if (kStamp && tid == 0) st[3] = tstamp();
 
+    if (A.diag & 2) return;  // diagnostic: no backward (wrong results)
     // 4. backward, kBChunk entries at a time (sparse tiles: the forward's staging)
     for (int c0 = 0; c0 < n; c0 += kBChunk) {
         const int gn = min(kBChunk, n - c0);
@@ -826,7 +830,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                 const int cs = ipr == 1 ? rx0 : rx0 + half * (j & 1);
                 const int ce = min(ipr == 1 ? rx1 : min(cs + half - 1, rx1), A.img_w - 1 - (int)tx0);
                 const float pyf = ty0 + (float)row;
-                if ((int)pyf < A.img_h) {
+                if ((int)pyf < A.img_h && !(A.diag & 8)) {  // diag 8: no pixel work
                     const float ex = G.x, eha = G.z, eb = G.w;
                     const float dy = G.y - pyf;
                     const float cq = (C.x * dy) * dy;  // splat_sigma_h's row terms
@@ -861,7 +865,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             }
             // per wave, segmented sums over the runs of items of one entry: the
             // last item of an entry's run holds the run's sum (fixed tree order)
-            wave_seg_sums(g, own);
+            if (!(A.diag & 16)) wave_seg_sums(g, own);  // diag 16: no run sums (wrong)
 #pragma unroll
             for (int c = 0; c < 8; ++c) S.part[c][tid] = g[c];
             __syncthreads();
@@ -885,7 +889,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             for (int c = 0; c < 8; ++c) S.part[c][lane] = acc[c];
         }
         __syncthreads();
-        for (int q = tid; q < gn * 8; q += kBThreads) {
+        for (int q = tid; q < gn * 8 && !(A.diag & 32); q += kBThreads) {  // diag 32: no atomics
             const int e = q >> 3, c = q & 7;
             unsafeAtomicAdd(A.grad + (size_t)S.gid[e] * 16 + c, S.part[c][e]);
         }
