@@ -541,9 +541,9 @@ struct BandLds {
     float4 col[kBChunk];           //   c/2, r, g, b
     unsigned ro[kBChunk];          //   rectangle (16 bits) | first work item << 16
     int gid[kBChunk];              //   splat id
-    float part[8][kBThreads + 1];  // backward: item partials; ranking / flush scratch
-    signed char own[kBThreads];    // backward: entry of the round's first items
-    int misc[8];
+    float part[8][kBThreads + 1];  // order: ranking / sort scratch; backward: entry sums per wave
+    signed char own[kBThreads];    // backward: per wave, the entry of the round's first items
+    int misc[4];   // the waves' error sums
 };
 
 template <bool kStamp>
@@ -561,7 +561,16 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     const int nin = row_in ? min(2, A.img_w - pj) : 0;  // pixels of the pair inside the image
     const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
     const size_t pix0 = row_in ? (size_t)pi * (size_t)A.img_w + (size_t)pj : 0;
-    // the pair's targets, loaded first
+    // this tile's count and its first kBSpec slab records in the same round trip
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+    if (tid < A.spec) {
+        const float4 *h = slab_rec(A.slab, A.ntiles, tile, tid);
+        r0 = h[0];
+        r1 = h[1];
+        r2 = h[2];
+    }
+    // the pair's targets, issued after the records (the order phase waits for
+    // those only; vmcnt retires in order) and needed only by the loss
     float gt[3][2];
     if (nin == 2 && (A.img_w & 1) == 0) {
 #pragma unroll
@@ -575,14 +584,6 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
         for (int c = 0; c < 3; ++c)
 #pragma unroll
             for (int q = 0; q < 2; ++q) gt[c][q] = q < nin ? A.gt[c * hw + pix0 + q] : 0.0f;
-    }
-    // this tile's count and its first kBSpec slab records in the same round trip
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
-    if (tid < A.spec) {
-        const float4 *h = slab_rec(A.slab, A.ntiles, tile, tid);
-        r0 = h[0];
-        r1 = h[1];
-        r2 = h[2];
     }
     const bool empty = *A.m_dev < 1;  // rasterize_sum.py:121-127: background, no gradient
     const int n_all = empty ? 0 : (int)__builtin_amdgcn_readfirstlane(A.counts[tile]);
@@ -760,72 +761,62 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     if (kStamp && tid == 0) st[3] = tstamp();
 
     if (A.diag & 2) return;  // diagnostic: no backward (wrong results)
-    // 4. backward, kBChunk entries at a time (sparse tiles: the forward's staging)
+    // 4. backward, kBChunk entries at a time (sparse tiles: the forward's staging).
+    // Each wave takes the rectangle rows of its own band -- the v_out rows it
+    // wrote itself -- so the waves need no barrier until the chunk's flush.
+    float *eacc = &S.part[0][0] + w * (8 * kBChunk);  // [8][kBChunk] entry sums per wave
+    signed char *wown = S.own + w * 64;
     for (int c0 = 0; c0 < n; c0 += kBChunk) {
         const int gn = min(kBChunk, n - c0);
         if (dense) {
-            __syncthreads();  // misc / staging / partial readers done
+            __syncthreads();  // staging / entry-sum readers done
             // this chunk's keys, by rank, into the gid slots stage_chunk overwrites
             if (tid < gn) S.gid[tid] = kpark[c0 + tid];  // written by this workgroup after its forward
             __syncthreads();
             stage_chunk(S.gid, gn);
             __syncthreads();
         }
-        // work items of entry e (wave 0, lane e): one per kBRun pixels of each rectangle row
+        // work items of entry `lane` in this band: one per rectangle row, two
+        // halves when the row is wider than brun
         int items = 0;
         unsigned rc = kNoRect;
-        if (w == 0 && lane < gn) {
+        if (lane < gn) {
             rc = S.ro[lane];
             if (rc != kNoRect) {
+                const int ry0 = max((int)((rc >> 8) & 15u), y_lo), ry1 = min((int)((rc >> 12) & 15u), y_hi);
                 const int rw = (int)((rc >> 4) & 15u) - (int)(rc & 15u) + 1;
-                const int rh = (int)((rc >> 12) & 15u) - (int)((rc >> 8) & 15u) + 1;
-                items = rh * (rw > A.brun ? 2 : 1);
+                if (ry0 <= ry1) items = (ry1 - ry0 + 1) * (rw > A.brun ? 2 : 1);
             }
         }
         const int incl = wave_scan_dpp<false>(items, 0);
         const int off = incl - items;
-        if (w == 0) {
-            if (lane < gn) S.ro[lane] = (rc & 0xffffu) | ((unsigned)off << 16);
-            if (lane == 63) S.misc[4] = incl;
-        }
-        __syncthreads();
-        const int total = S.misc[4];
-        float acc[8];
+        const int total = __builtin_amdgcn_readlane(incl, 63);
 #pragma unroll
-        for (int c = 0; c < 8; ++c) acc[c] = 0.0f;
-        for (int base = 0; base < total; base += kBThreads) {
-            // the entry of item base + tid: the last entry whose first item is <= it
-            S.own[tid] = -1;
-            __syncthreads();
-            if (items > 0 && off >= base && off < base + kBThreads) S.own[off - base] = (signed char)lane;
-            if (w == 0) {
-                const unsigned long long before = __ballot(lane < gn && off <= base);
-                if (lane == 0) S.misc[5] = __popcll(before) - 1;  // entry straddling into this round
-            }
-            __syncthreads();
-            int own = max((int)S.own[tid], S.misc[5]);
+        for (int c = 0; c < 8; ++c) eacc[c * kBChunk + lane] = 0.0f;
+        for (int base = 0; base < total; base += 64) {
+            // the entry of item base + lane: the last entry whose first item is <= it
+            wown[lane] = -1;
+            __builtin_amdgcn_wave_barrier();
+            if (items > 0 && off >= base && off < base + 64) wown[off - base] = (signed char)lane;
+            const int straddle = __popcll(__ballot(lane < gn && off <= base)) - 1;
+            __builtin_amdgcn_wave_barrier();
+            int own = max((int)wown[lane], straddle);
             own = wave_scan_dpp<true>(own, -2147483647 - 1);
-            if (w == 1) {
-                // wave 1 continues wave 0's scan: the largest head among items base .. base+63
-                int m = (int)S.own[lane];
-#pragma unroll
-                for (int o2 = 32; o2 > 0; o2 >>= 1) m = max(m, __shfl_xor(m, o2, 64));
-                own = max(own, max(m, S.misc[5]));
-            }
-            const int item = base + tid;
+            const int item = base + lane;
+            // the entry's first item and rectangle, from its lane
+            const int eoff = __shfl(off, own, 64);
+            const unsigned ro = (unsigned)__shfl((int)rc, own, 64);
             float g[8];
 #pragma unroll
             for (int c = 0; c < 8; ++c) g[c] = 0.0f;
             if (item < total) {
                 const float4 G = S.geo[own], C = S.col[own];
-                const unsigned ro = S.ro[own];
-                const int j = item - (int)(ro >> 16);  // item index within the entry
+                const int j = item - eoff;  // item index within the entry
                 const int rx0 = (int)(ro & 15u), rx1 = (int)((ro >> 4) & 15u);
-                // items per rectangle row: 1, or 2 halves when it is wider than brun
                 const int rwid = rx1 - rx0 + 1;
                 const int ipr = rwid > A.brun ? 2 : 1;
                 const int jr = ipr == 1 ? j : (j >> 1);
-                const int row = (int)((ro >> 8) & 15u) + jr;
+                const int row = max((int)((ro >> 8) & 15u), y_lo) + jr;
                 const int half = (rwid + 1) >> 1;
                 const int cs = ipr == 1 ? rx0 : rx0 + half * (j & 1);
                 const int ce = min(ipr == 1 ? rx1 : min(cs + half - 1, rx1), A.img_w - 1 - (int)tx0);
@@ -835,8 +826,11 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                     const float dy = G.y - pyf;
                     const float cq = (C.x * dy) * dy;  // splat_sigma_h's row terms
                     const float bdy = eb * dy;
-                    const float fcdy = (2.0f * C.x) * dy;
-                    const float fa = 2.0f * eha;
+                    // dy is constant along the item's row, so the per-pixel sums of
+                    // backward.cu:822-848 factor: v_conic = 1/2 (S2, dy S1, dy^2 S0),
+                    // v_xy = (2 ha S1 + b dy S0, b S1 + 2 c dy S0) with S_k = sum
+                    // v_sigma dx^k -- 4 VALU per pixel instead of 11
+                    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
                     for (int col = cs; col <= ce; ++col) {
                         const float pxf = tx0 + (float)col;
                         // (diagnostic knob 13 = 1: a conflict-free read pattern, wrong
@@ -853,45 +847,38 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                         g[5] = fmaf(al, Px, g[5]);
                         g[6] = fmaf(al, Py, g[6]);
                         g[7] = fmaf(al, Pz, g[7]);
-                        const float hs = 0.5f * v_sigma;
-                        const float hsdx = hs * dx;
-                        g[2] = fmaf(hsdx, dx, g[2]);
-                        g[3] = fmaf(hsdx, dy, g[3]);
-                        g[4] = fmaf(hs * dy, dy, g[4]);
-                        g[0] = fmaf(v_sigma, fmaf(fa, dx, bdy), g[0]);
-                        g[1] = fmaf(v_sigma, fmaf(eb, dx, fcdy), g[1]);
+                        s0 += v_sigma;
+                        const float vdx = v_sigma * dx;
+                        s1 += vdx;
+                        s2 = fmaf(vdx, dx, s2);
                     }
+                    const float hdy = 0.5f * dy;
+                    g[0] = fmaf(2.0f * eha, s1, bdy * s0);
+                    g[1] = fmaf(eb, s1, ((2.0f * C.x) * dy) * s0);
+                    g[2] = 0.5f * s2;
+                    g[3] = hdy * s1;
+                    g[4] = (hdy * dy) * s0;
                 }
             }
-            // per wave, segmented sums over the runs of items of one entry: the
-            // last item of an entry's run holds the run's sum (fixed tree order)
+            // segmented sums over the runs of items of one entry: the last item
+            // of an entry's run holds the run's sum (fixed tree order) and adds it
+            // to the entry's (a fixed order: rounds in sequence)
             if (!(A.diag & 16)) wave_seg_sums(g, own);  // diag 16: no run sums (wrong)
+            const int own_next = __shfl_down(own, 1, 64);
+            if (item < total && (lane == 63 || item + 1 == total || own_next != own)) {
 #pragma unroll
-            for (int c = 0; c < 8; ++c) S.part[c][tid] = g[c];
-            __syncthreads();
-            // each entry adds its (at most two: one per wave) run sums of this round
-            if (w == 0 && items > 0) {
-                const int i0 = max(off, base) - base, i1 = min(off + items, base + kBThreads) - base;
-                if (i0 < i1) {
-                    if (i0 < 64 && i1 > 64) {
-#pragma unroll
-                        for (int c = 0; c < 8; ++c) acc[c] += S.part[c][63];
-                    }
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) acc[c] += S.part[c][i1 - 1];
-                }
+                for (int c = 0; c < 8; ++c) eacc[c * kBChunk + own] += g[c];
             }
-            __syncthreads();  // partials read before the next round rewrites them
-        }
-        // 8 lanes per entry add the entry's sums into the splat's gradient record
-        if (w == 0 && lane < gn) {
-#pragma unroll
-            for (int c = 0; c < 8; ++c) S.part[c][lane] = acc[c];
+            __builtin_amdgcn_wave_barrier();
         }
         __syncthreads();
+        // 8 lanes per entry add the entry's sums (band 0 + band 1) into the
+        // splat's gradient record
         for (int q = tid; q < gn * 8 && !(A.diag & 32); q += kBThreads) {  // diag 32: no atomics
             const int e = q >> 3, c = q & 7;
-            unsafeAtomicAdd(A.grad + (size_t)S.gid[e] * 16 + c, S.part[c][e]);
+            const float *ea = &S.part[0][0];
+            unsafeAtomicAdd(A.grad + (size_t)S.gid[e] * 16 + c,
+                            ea[c * kBChunk + e] + ea[8 * kBChunk + c * kBChunk + e]);
         }
     }
     if (kStamp && tid == 0) {

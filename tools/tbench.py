@@ -169,6 +169,15 @@ def main():
             rec[nm] = q(t[:, k + 1] - t[:, k])
         rec.update(life=q(t[:, 5] - t[:, 0]), end=q(t[:, 5] - t0))
         print(json.dumps(rec), flush=True)
+        # the same phases for the tiles of the first wave of workgroups (started
+        # within 5 us) and for the rest
+        early = (t[:, 0] - t0) < 5.0
+        for lab, sel in (("first_round", early), ("later", ~early)):
+            if sel.sum():
+                ts = t[sel]
+                print(json.dumps({lab: dict(tiles=int(sel.sum()), **{
+                    nm: q(ts[:, k + 1] - ts[:, k]) for k, nm in enumerate(names)},
+                    t_start=q(ts[:, 0] - t0), t_end=q(ts[:, 5] - t0))}), flush=True)
         if a.tile_kernel == "band":
             # medians per entry-count bucket (stamp slot 6 = the tile's count)
             cnt = st.cpu().numpy()[:, 6][st.cpu().numpy()[:, 5] > 0]
