@@ -561,32 +561,28 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     const int nin = row_in ? min(2, A.img_w - pj) : 0;  // pixels of the pair inside the image
     const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
     const size_t pix0 = row_in ? (size_t)pi * (size_t)A.img_w + (size_t)pj : 0;
-    // this tile's count and its first kBSpec slab records in the same round trip
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
-    if (tid < A.spec) {
-        const float4 *h = slab_rec(A.slab, A.ntiles, tile, tid);
-        r0 = h[0];
-        r1 = h[1];
-        r2 = h[2];
-    }
-    // the pair's targets, issued after the records (the order phase waits for
-    // those only; vmcnt retires in order) and needed only by the loss
+    // one round trip for everything the tile starts from, with no wait in
+    // between (a branch around a load makes the compiler wait for it at the
+    // join): the frame's M and this tile's count (scalar), the first kBSpec
+    // slab records (lanes past kBSpec re-read slot 0: the same lines), the
+    // pair's targets (lanes outside the image read pixel 0; only the loss
+    // reads them, masked)
+    const int m_frame = *A.m_dev;
+    const unsigned cnt_raw = A.counts[tile];
+    const float4 *h0 = slab_rec(A.slab, A.ntiles, tile, tid < A.spec ? tid : 0);
+    float4 r0 = h0[0], r1 = h0[1], r2 = h0[2];
     float gt[3][2];
-    if (nin == 2 && (A.img_w & 1) == 0) {
+    {
+        const size_t b0 = nin > 0 ? pix0 : 0, b1 = nin > 1 ? pix0 + 1 : b0;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const float2 v = *reinterpret_cast<const float2 *>(A.gt + c * hw + pix0);
-            gt[c][0] = v.x;
-            gt[c][1] = v.y;
+            gt[c][0] = A.gt[c * hw + b0];
+            gt[c][1] = A.gt[c * hw + b1];
         }
-    } else {
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-#pragma unroll
-            for (int q = 0; q < 2; ++q) gt[c][q] = q < nin ? A.gt[c * hw + pix0 + q] : 0.0f;
     }
-    const bool empty = *A.m_dev < 1;  // rasterize_sum.py:121-127: background, no gradient
-    const int n_all = empty ? 0 : (int)__builtin_amdgcn_readfirstlane(A.counts[tile]);
+    const bool empty = m_frame < 1;  // rasterize_sum.py:121-127: background, no gradient
+    // (a mask, not a branch: the count's load must not sink behind M's)
+    const int n_all = (int)__builtin_amdgcn_readfirstlane(cnt_raw) & -(int)!empty;
     if (tid == 0) A.counts_clear[tile] = 0u;  // the next frame's counts
     const bool dense = n_all > kBChunk;
     const bool brute = n_all > kTilePix;  // the slab dropped entries: ids rebuilt
