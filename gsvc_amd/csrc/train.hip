@@ -858,7 +858,10 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             }
             // segmented sums over the runs of items of one entry: the last item
             // of an entry's run holds the run's sum (fixed tree order) and adds it
-            // to the entry's (a fixed order: rounds in sequence)
+            // to the entry's (a fixed order: rounds in sequence).  Measured
+            // alternatives: every item adding its sums with LDS float atomics
+            // (2.9x slower kernel: the LDS serialises an entry's items); a packed
+            // two-pixel loop (80 VGPRs, 6 waves per SIMD: 64.0 vs 58.5 us)
             if (!(A.diag & 16)) wave_seg_sums(g, own);  // diag 16: no run sums (wrong)
             const int own_next = __shfl_down(own, 1, 64);
             if (item < total && (lane == 63 || item + 1 == total || own_next != own)) {
