@@ -504,9 +504,34 @@ __device__ __forceinline__ int wave_scan_dpp(int v, int id) {
 }
 
 // One step of a segmented inclusive sum: lanes whose DPP source lane carries
-// the same key add its 8 sums (sources outside the row / masked rows: key -1).
+// the same key add its 8 sums (sources outside the row / masked rows: key -1,
+// and the lane is not written).  ``g += m * g[src]`` with m = 1 or 0 as ONE
+// v_fmac_f32_dpp per sum (the compiler does not fold the DPP move into an fma);
+// exact while the sums are finite (x * 0 = 0), so a wave with a non-finite sum
+// takes the select form (seg_step8_sel).
+#define GSVC_FMAC_DPP8(CTRL)                                                               \
+    asm volatile("s_nop 1\n\t"                                                             \
+                 "v_fmac_f32_dpp %0, %0, %8 " CTRL "\n\t"                                  \
+                 "v_fmac_f32_dpp %1, %1, %8 " CTRL "\n\t"                                  \
+                 "v_fmac_f32_dpp %2, %2, %8 " CTRL "\n\t"                                  \
+                 "v_fmac_f32_dpp %3, %3, %8 " CTRL "\n\t"                                  \
+                 "v_fmac_f32_dpp %4, %4, %8 " CTRL "\n\t"                                  \
+                 "v_fmac_f32_dpp %5, %5, %8 " CTRL "\n\t"                                  \
+                 "v_fmac_f32_dpp %6, %6, %8 " CTRL "\n\t"                                  \
+                 "v_fmac_f32_dpp %7, %7, %8 " CTRL "\n\t"                                  \
+                 "s_nop 1"                                                                 \
+                 : "+v"(g[0]), "+v"(g[1]), "+v"(g[2]), "+v"(g[3]), "+v"(g[4]), "+v"(g[5]), \
+                   "+v"(g[6]), "+v"(g[7])                                                  \
+                 : "v"(m))
+
 template <int kCtrl, int kRowMask>
-__device__ __forceinline__ void seg_step8(float (&g)[8], int key) {
+__device__ __forceinline__ float seg_mask(int key) {
+    const int ks = __builtin_amdgcn_update_dpp(-1, key, kCtrl, kRowMask, 0xf, false);
+    return ks == key ? 1.0f : 0.0f;
+}
+
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void seg_step8_sel(float (&g)[8], int key) {
     const int ks = __builtin_amdgcn_update_dpp(-1, key, kCtrl, kRowMask, 0xf, false);
     const bool same = ks == key;
 #pragma unroll
@@ -522,13 +547,33 @@ __device__ __forceinline__ void seg_step8(float (&g)[8], int key) {
 // The wave_scan_dpp steps; a source lane is added only inside the run, so
 // each lane's sum covers exactly [max(run start, ...), i].
 __device__ __forceinline__ void wave_seg_sums(float (&g)[8], int key) {
-    seg_step8<0x111, 0xf>(g, key);  // row_shr:1
-    seg_step8<0x112, 0xf>(g, key);  // row_shr:2
-    seg_step8<0x114, 0xf>(g, key);  // row_shr:4
-    seg_step8<0x118, 0xf>(g, key);  // row_shr:8
-    seg_step8<0x142, 0xa>(g, key);  // row_bcast:15 -> rows 1, 3
-    seg_step8<0x143, 0xc>(g, key);  // row_bcast:31 -> rows 2, 3
+    // finite unless some sum is inf / NaN (or the total overflows: then the
+    // exact select form runs, which is still right)
+    const float tot = ((g[0] + g[1]) + (g[2] + g[3])) + ((g[4] + g[5]) + (g[6] + g[7]));
+    if (__ballot(!__builtin_isfinite(tot)) == 0ull) {
+        float m;
+        m = seg_mask<0x111, 0xf>(key);
+        GSVC_FMAC_DPP8("row_shr:1 row_mask:0xf bank_mask:0xf");
+        m = seg_mask<0x112, 0xf>(key);
+        GSVC_FMAC_DPP8("row_shr:2 row_mask:0xf bank_mask:0xf");
+        m = seg_mask<0x114, 0xf>(key);
+        GSVC_FMAC_DPP8("row_shr:4 row_mask:0xf bank_mask:0xf");
+        m = seg_mask<0x118, 0xf>(key);
+        GSVC_FMAC_DPP8("row_shr:8 row_mask:0xf bank_mask:0xf");
+        m = seg_mask<0x142, 0xa>(key);
+        GSVC_FMAC_DPP8("row_bcast:15 row_mask:0xa bank_mask:0xf");
+        m = seg_mask<0x143, 0xc>(key);
+        GSVC_FMAC_DPP8("row_bcast:31 row_mask:0xc bank_mask:0xf");
+    } else {
+        seg_step8_sel<0x111, 0xf>(g, key);  // row_shr:1
+        seg_step8_sel<0x112, 0xf>(g, key);  // row_shr:2
+        seg_step8_sel<0x114, 0xf>(g, key);  // row_shr:4
+        seg_step8_sel<0x118, 0xf>(g, key);  // row_shr:8
+        seg_step8_sel<0x142, 0xa>(g, key);  // row_bcast:15 -> rows 1, 3
+        seg_step8_sel<0x143, 0xc>(g, key);  // row_bcast:31 -> rows 2, 3
+    }
 }
+#undef GSVC_FMAC_DPP8
 
 // v_out rows padded to 17 words: the backward's lanes read pixels of
 // different rows of one column, which with 16-word rows share a bank every 4
