@@ -52,7 +52,8 @@ struct TrainTileArgs {
     int spec;         // band kernel: slab records loaded with the count
     int diag;         // diagnostic knob 13 (timing experiments only; wrong results):
                       // bits 1 conflict-free v_out reads, 2 no backward, 4 no forward
-                      // blending, 8 no backward pixel work, 16 no run sums, 32 no atomics
+                      // blending, 8 no backward pixel work, 16 no run sums, 32 no atomics;
+                      // 64 (A/B, exact): items in entry order, not longest first
     float *out;       // optional [3, H, W] clamped render
     long long *stamps;  // diagnostic: int64[ntiles][8]
 };
@@ -588,6 +589,7 @@ struct BandLds {
     int gid[kBChunk];              //   splat id
     float part[8][kBThreads + 1];  // order: ranking / sort scratch; backward: entry sums per wave
     signed char own[kBThreads];    // backward: per wave, the entry of the round's first items
+    signed char perm[kBThreads];   // backward: per wave, the chunk's entries by item length
     int misc[4];   // the waves' error sums
 };
 
@@ -807,6 +809,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     // wrote itself -- so the waves need no barrier until the chunk's flush.
     float *eacc = &S.part[0][0] + w * (8 * kBChunk);  // [8][kBChunk] entry sums per wave
     signed char *wown = S.own + w * 64;
+    signed char *wperm = S.perm + w * 64;
     for (int c0 = 0; c0 < n; c0 += kBChunk) {
         const int gn = min(kBChunk, n - c0);
         if (dense) {
@@ -819,18 +822,48 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
         }
         // work items of entry `lane` in this band: one per rectangle row, two
         // halves when the row is wider than brun
-        int items = 0;
+        int items = 0, ilen = 0;
         unsigned rc = kNoRect;
         if (lane < gn) {
             rc = S.ro[lane];
             if (rc != kNoRect) {
                 const int ry0 = max((int)((rc >> 8) & 15u), y_lo), ry1 = min((int)((rc >> 12) & 15u), y_hi);
                 const int rw = (int)((rc >> 4) & 15u) - (int)(rc & 15u) + 1;
-                if (ry0 <= ry1) items = (ry1 - ry0 + 1) * (rw > A.brun ? 2 : 1);
+                if (ry0 <= ry1) {
+                    items = (ry1 - ry0 + 1) * (rw > A.brun ? 2 : 1);
+                    ilen = rw > A.brun ? (rw + 1) >> 1 : rw;
+                }
             }
         }
-        const int incl = wave_scan_dpp<false>(items, 0);
-        const int off = incl - items;
+        // the entries' items are laid out longest first (by class, stable), so a
+        // round's 64 items -- whose pixel loop runs as long as its longest --
+        // have similar lengths; each entry's sums are unchanged (its items
+        // stay together, in row order)
+        {
+            const unsigned long long below = (1ull << lane) - 1ull;
+            int rank = 0, seen = 0;
+            unsigned long long left = __ballot(true);
+            if (A.diag & 64) {  // A/B: entry order
+                rank = lane;
+                left = 0ull;
+            }
+            // four length classes (9+, 7-8, 5-6, <= 4 and no items), entry
+            // order within a class: most of an exact sort's gain for a quarter
+            // of its VALU
+            const int cls = ilen >= 9 ? 3 : (ilen >= 7 ? 2 : (ilen >= 5 ? 1 : 0));
+            for (int L = 3; L >= 0 && left; --L) {
+                const unsigned long long m = __ballot(cls == L);
+                if (cls == L) rank = seen + __popcll(m & below);
+                seen += __popcll(m);
+                left &= ~m;
+            }
+            wperm[rank] = (signed char)lane;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int ent = wperm[lane];  // the entry in sorted slot `lane`
+        const int sitems = __shfl(items, ent, 64);
+        const int incl = wave_scan_dpp<false>(sitems, 0);
+        const int off = incl - sitems;  // sorted slot `lane`'s first item
         const int total = __builtin_amdgcn_readlane(incl, 63);
 #pragma unroll
         for (int c = 0; c < 8; ++c) eacc[c * kBChunk + lane] = 0.0f;
@@ -838,14 +871,15 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             // the entry of item base + lane: the last entry whose first item is <= it
             wown[lane] = -1;
             __builtin_amdgcn_wave_barrier();
-            if (items > 0 && off >= base && off < base + 64) wown[off - base] = (signed char)lane;
+            if (sitems > 0 && off >= base && off < base + 64) wown[off - base] = (signed char)lane;
             const int straddle = __popcll(__ballot(lane < gn && off <= base)) - 1;
             __builtin_amdgcn_wave_barrier();
-            int own = max((int)wown[lane], straddle);
-            own = wave_scan_dpp<true>(own, -2147483647 - 1);
+            int slot = max((int)wown[lane], straddle);
+            slot = wave_scan_dpp<true>(slot, -2147483647 - 1);  // sorted slot of item base + lane
             const int item = base + lane;
-            // the entry's first item and rectangle, from its lane
-            const int eoff = __shfl(off, own, 64);
+            // the entry, its first item and rectangle
+            const int own = __shfl(ent, slot, 64);
+            const int eoff = __shfl(off, slot, 64);
             const unsigned ro = (unsigned)__shfl((int)rc, own, 64);
             float g[8];
 #pragma unroll
