@@ -51,7 +51,7 @@ struct TrainTileArgs {
     int brun;         // band kernel: a rectangle row wider than this is two work items
     int spec;         // band kernel: slab records loaded with the count
     int diag;         // diagnostic knob 13 (timing experiments only; wrong results):
-                      // bits 1 conflict-free v_out reads, 2 no backward, 4 no forward
+                      // bits 2 no backward, 4 no forward
                       // blending, 8 no backward pixel work, 16 no run sums, 32 no atomics;
                       // 64 (A/B, exact): items in entry order, not longest first
     float *out;       // optional [3, H, W] clamped render
@@ -906,13 +906,15 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                     // v_xy = (2 ha S1 + b dy S0, b S1 + 2 c dy S0) with S_k = sum
                     // v_sigma dx^k -- 4 VALU per pixel instead of 11
                     float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
-                    for (int col = cs; col <= ce; ++col) {
-                        const float pxf = tx0 + (float)col;
-                        // (diagnostic knob 13 = 1: a conflict-free read pattern, wrong
-                        // results -- isolates the LDS cost of these reads)
-                        const int pix = (A.diag & 1) ? (tid & 255) : row * kVRow + col;
-                        const float Px = S.v[0][pix], Py = S.v[1][pix], Pz = S.v[2][pix];
-                        const float dx = ex - pxf;
+                    // walk the row by its v_out word (the planes at fixed LDS
+                    // offsets) with dx stepping by -1 (exact: ex - px is exact
+                    // or, far off, rounds alike)
+                    const float *vf = &S.v[0][0];
+                    const int pe = row * kVRow + ce;
+                    float dx = ex - (tx0 + (float)cs);
+                    for (int pix = row * kVRow + cs; pix <= pe; ++pix, dx -= 1.0f) {
+                        const float Px = vf[pix], Py = vf[kTile * kVRow + pix],
+                                    Pz = vf[2 * kTile * kVRow + pix];
                         const float sgm = fmaf(fmaf(eha, dx, bdy), dx, cq);
                         const float vis = exp_neg(sgm);
                         const float al = fminf(1.0f, vis);  // opacity 1
