@@ -430,19 +430,25 @@ __global__ __launch_bounds__(256, 8) void train_tile_kernel(TrainTileArgs A) {
 //      entry order, with the render's op sequence at unit opacity (1 * e ==
 //      e: the same image bits); clamp, loss gradient, error sums; v_out planes
 //      into LDS.
-//   3. backward over work items = one row of an entry's rectangle, up to
-//      kBRun pixels (the row terms of sigma shared), laid out entry by entry
-//      over the 128 lanes; each item's 8 gradient sums go to an LDS partial
-//      slot and each entry adds its items' partials in item order
-//      (deterministic, no LDS atomics); then 8 lanes per entry add the
-//      entry's 32 bytes into the splat's gradient record (one request per
-//      (splat, tile)).
+//   3. backward, each wave over the rectangle rows of its own band: work
+//      items = one row of an entry's rectangle (the row terms of sigma
+//      shared; per-pixel sums factored by dy), entries laid out longest rows
+//      first in four length classes, rounds of 64 items; per round a DPP
+//      segmented scan (one v_fmac_f32_dpp per sum and step) gives each run of
+//      an entry's items its sum, which the run's last item adds to the
+//      entry's LDS sums (a fixed order, no LDS atomics); then 8 lanes per
+//      entry add the two bands' 32 bytes into the splat's gradient record
+//      (one request per (splat, tile)).
 // GSVC's opacity is ones (GaussianSplats_Represent.py:84) and the training
 // step projects with opacity 1, so the opacity gradient (record slot 8) is
 // not formed.
 constexpr int kBSpec = 32;    // slab slots loaded with the count (64: slower, measured)
 constexpr int kBChunk = 64;   // entries staged at a time
-constexpr int kBRun = 10;     // rows wider than this split into two work items (8: +4 %, 16: +3 % at trained density)
+// rows wider than this split into two work items (A/B knob 11).  16 = never:
+// measured 51.6 vs 54.0 us (10) at trained density, 31.8 vs 32.1 at init --
+// fewer rounds of segmented sums beat the longer pixel loops once items are
+// laid out by length (tools/item_sim.py models it)
+constexpr int kBRun = 16;
 constexpr int kBThreads = 128;
 
 typedef float v2f __attribute__((ext_vector_type(2)));
