@@ -28,6 +28,7 @@
 #include "adan.h"
 #include "binning.h"
 #include "frame.h"
+#include "frame_dev.h"
 #include "tile_ids.h"
 
 namespace gsvc {
@@ -50,6 +51,7 @@ struct TrainTileArgs {
     float2 *err;      // [ntiles]: sum of squared, sum of absolute errors
     int brun;         // band kernel: a rectangle row wider than this is two work items
     int spec;         // band kernel: slab records loaded with the count
+    int grouped;      // band kernel forward: lane-group entry lists (A/B knob 15 = 1: off)
     int diag;         // diagnostic knob 13 (timing experiments only; wrong results):
                       // bits 2 no backward, 4 no forward
                       // blending, 8 no backward pixel work, 16 no run sums, 32 no atomics;
@@ -589,9 +591,9 @@ constexpr int kVRow = kTile + 1;
 
 struct BandLds {
     float v[3][kTile * kVRow];     // v_out planes, rows padded to kVRow words
-    float4 geo[kBChunk];           // staged entries (rank order): x, y, a/2, b
-    float4 col[kBChunk];           //   c/2, r, g, b
-    unsigned ro[kBChunk];          //   rectangle (16 bits) | first work item << 16
+    float4 geo[kBChunk + 1];       // staged entries (rank order): x, y, a/2, b
+    float4 col[kBChunk + 1];       //   c/2, r, g, b  (slot kBChunk: the no-op sentinel)
+    unsigned short ro[kBChunk];    //   rectangle (ellipse_rect, 16 bits)
     int gid[kBChunk];              //   splat id
     float part[8][kBThreads + 1];  // order: ranking / sort scratch; backward: entry sums per wave
     signed char own[kBThreads];    // backward: per wave, the entry of the round's first items
@@ -636,7 +638,13 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     const bool empty = m_frame < 1;  // rasterize_sum.py:121-127: background, no gradient
     // (a mask, not a branch: the count's load must not sink behind M's)
     const int n_all = (int)__builtin_amdgcn_readfirstlane(cnt_raw) & -(int)!empty;
-    if (tid == 0) A.counts_clear[tile] = 0u;  // the next frame's counts
+    if (tid == 0) {
+        A.counts_clear[tile] = 0u;  // the next frame's counts
+        // the grouped forward's padding entry: sigma = +inf at every pixel, so
+        // alpha = 0 fails the test and it adds 0 * colour 0 (no change)
+        S.geo[kBChunk] = make_float4(0.0f, 1e30f, 0.0f, 0.0f);
+        S.col[kBChunk] = make_float4(1e30f, 0.0f, 0.0f, 0.0f);
+    }
     const bool dense = n_all > kBChunk;
     const bool brute = n_all > kTilePix;  // the slab dropped entries: ids rebuilt
     // dense: the splat ids by rank (part rows 0-1), the slab's ids (rows 2-3,
@@ -707,11 +715,80 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             S.ro[tid] = ellipse_rect(a.x, a.y, 2.0f * a.z, a.w, 2.0f * b.x, 1.0f, tx0, ty0);
         }
     };
+    // the forward's lane-group lists (A.grouped): [64 iterations][8 groups] entry
+    // indices per wave in part rows 2-3, free once the order is known (the
+    // dense sort's scratch)
+    unsigned char *wlist = reinterpret_cast<unsigned char *>(&S.part[2][0]) + w * 512;
+    const int grp = ((lane >> 5) << 2) | ((lane & 7) >> 1);
     for (int c0 = 0; c0 < n; c0 += kBChunk) {
         const int cnt = min(kBChunk, n - c0);
         if (dense) {
             stage_chunk(s_key + c0, cnt);
             __syncthreads();
+        }
+        if (A.grouped) {
+            // lane groups: 8 groups of 8 lanes, each a 4-row x 4-column block of
+            // the band (grp); every group walks, in rank order, only the
+            // entries whose rectangle reaches its block (lists[it][grp], padded
+            // with the no-op sentinel entry kBChunk up to the longest list).
+            // The pairs skipped contribute nothing (the band culling's own
+            // argument), so every pixel sees the same sequence of blends.
+            unsigned gm = 0u;
+            bool fin = false;
+            if (lane < cnt) {
+                const unsigned rc = S.ro[lane];
+                if (rc != kNoRect) {
+                    const int ry0 = (int)((rc >> 8) & 15u), ry1 = (int)((rc >> 12) & 15u);
+                    const unsigned rb = (unsigned)(ry0 <= y_lo + 3 && ry1 >= y_lo) |
+                                        ((unsigned)(ry0 <= y_hi && ry1 >= y_lo + 4) << 1);
+                    const unsigned cx0 = (rc & 15u) >> 2, cx1 = ((rc >> 4) & 15u) >> 2;
+                    const unsigned cb = ((2u << cx1) - 1u) & ~((1u << cx0) - 1u);
+                    gm = ((rb & 1u) ? cb : 0u) | ((rb & 2u) ? cb << 4 : 0u);
+                }
+                const float4 C = S.col[lane];
+                fin = __builtin_isfinite(C.y) && __builtin_isfinite(C.z) && __builtin_isfinite(C.w);
+            }
+            if (A.diag & 4) gm = 0u;  // diagnostic: no forward blending (wrong results)
+            // row `lane` of the lists: the sentinel, then the entries
+            *reinterpret_cast<unsigned long long *>(wlist + 8 * lane) = 0x4040404040404040ull;
+            __builtin_amdgcn_wave_barrier();
+            const unsigned long long below = (1ull << lane) - 1ull;
+            int maxlen = 0;
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const bool in = (gm >> g) & 1u;
+                const unsigned long long mg = __ballot(in);
+                if (in) wlist[8 * __popcll(mg & below) + g] = (unsigned char)lane;
+                maxlen = max(maxlen, __popcll(mg));
+            }
+            const unsigned long long any = __ballot(gm != 0u);
+            const unsigned long long fm = __ballot(fin);
+            __builtin_amdgcn_wave_barrier();
+            const unsigned char *ml = wlist + grp;
+            if ((any & ~fm) == 0) {
+                for (int it = 0; it < maxlen; ++it) {
+                    const int k = ml[8 * it];
+                    const float4 G = S.geo[k];
+                    const float4 C = S.col[k];
+                    const float dy = G.y - py;
+                    const float cq = (C.x * dy) * dy;
+                    const float bdy = G.w * dy;
+                    blend2_unit_fin(G.x, G.z, bdy, cq, C.y, C.z, C.w, px, ar, ag, ab);
+                }
+            } else {
+                for (int it = 0; it < maxlen; ++it) {
+                    const int k = ml[8 * it];
+                    const float4 G = S.geo[k];
+                    const float4 C = S.col[k];
+                    const float dy = G.y - py;
+                    const float cq = (C.x * dy) * dy;
+                    const float bdy = G.w * dy;
+                    blend2_unit(G.x, G.z, bdy, cq, C.y, C.z, C.w, px, ar, ag, ab);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();  // the next chunk rewrites the lists
+            if (dense) __syncthreads();  // the next chunk overwrites the staging
+            continue;
         }
         // the entries whose rectangle reaches this band, as a wave-uniform mask
         bool keep = false, fin = false;
@@ -980,9 +1057,9 @@ struct TrainSplatArgs {
     double inv_count;
     float *xyz, *chol, *feat, *rgbw;
     const float *chol_bound;
-    const int *radii;
-    const float4 *rec;
-    const float4 *grad;  // [N][4]
+    int *radii;
+    float4 *rec;
+    float4 *grad;        // [N][4]
     float *state[4][4];  // [xyz, chol, feat, rgb_w][exp_avg, exp_avg_sq, exp_avg_diff, neg_pre_grad]
     int first[4];        // the parameter's first Adan step (optimizer.py:187-189)
     AdanScalars S;
@@ -990,64 +1067,28 @@ struct TrainSplatArgs {
     const float2 *err;
     float *loss;         // [2]: mean squared error, mean absolute error
     unsigned loss_seq;   // non-zero: stored into word 2 of ``loss`` after the losses
+    // project != 0 (update only): the next frame's projection, fused -- lane t
+    // updates splat order[t] (NULL: t) and projects it from the parameters it
+    // has just written, as frame_project_ordered_kernel would (frame_dev.h)
+    int project, tbx, tby;
+    const int *order;
+    float2 *xys;
+    unsigned *counts;
+    float4 *slab;
+    int *m_acc, *m_clear;
+    unsigned *key;       // optional: strip keys and ids for the next order
+    int *key_id;
+    unsigned key_invisible;
 };
 
 // The loss workgroup's loads per round: 16 tile pairs per thread in flight, so
 // a 1080p frame (4080 pairs) is one round trip.
 constexpr int kLossBatch = 16;
 
-__global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
-    if (blockIdx.x == 0) {
-        // the first workgroup (no splats): the loss, the tiles' error sums in a
-        // fixed order, in double; dispatched first so it runs beside the splats
-        __shared__ double s_l[2][4];
-        double s2 = 0.0, s1 = 0.0;
-        const int npair = A.ntiles >> 1;
-        const float4 *e4 = reinterpret_cast<const float4 *>(A.err);
-        for (int t0 = threadIdx.x; t0 < npair; t0 += kLossBatch * 256) {
-            float4 e[kLossBatch];
-#pragma unroll
-            for (int k = 0; k < kLossBatch; ++k) {
-                const int t = t0 + 256 * k;
-                e[k] = t < npair ? e4[t] : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int k = 0; k < kLossBatch; ++k) {
-                s2 += (double)e[k].x;
-                s1 += (double)e[k].y;
-                s2 += (double)e[k].z;
-                s1 += (double)e[k].w;
-            }
-        }
-        if ((A.ntiles & 1) && threadIdx.x == 0) {
-            const float2 e = A.err[A.ntiles - 1];
-            s2 += (double)e.x;
-            s1 += (double)e.y;
-        }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            s2 += __shfl_xor(s2, off, 64);
-            s1 += __shfl_xor(s1, off, 64);
-        }
-        if ((threadIdx.x & 63) == 0) {
-            s_l[0][threadIdx.x >> 6] = s2;
-            s_l[1][threadIdx.x >> 6] = s1;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            A.loss[0] = (float)(((s_l[0][0] + s_l[0][1]) + (s_l[0][2] + s_l[0][3])) * A.inv_count);
-            A.loss[1] = (float)(((s_l[1][0] + s_l[1][1]) + (s_l[1][2] + s_l[1][3])) * A.inv_count);
-            // coherent host memory: the host stops waiting here, while the
-            // splat workgroups still run (later work on the stream is ordered
-            // after them anyway)
-            if (A.loss_seq)
-                __hip_atomic_store(reinterpret_cast<unsigned *>(A.loss) + 2, A.loss_seq,
-                                   __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        return;
-    }
-    const int i = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
-    if (i >= A.n) return;
+// One splat's step: the projection VJP, activation VJPs and the Adan update of
+// its elements (update == 0: the gradients into grads_out); np receives the
+// parameters as stored (xyz 2, chol 3, feat 3, rgb_W).
+__device__ __forceinline__ void splat_step(const TrainSplatArgs &A, int i, float (&np)[9]) {
     // Every operand is loaded up front, before any arithmetic: one round trip
     // per lane instead of three (gradient + radius -> record -> Adan state).
     // rec is written for every splat by the projection, so its load needs no
@@ -1061,6 +1102,7 @@ __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
     const float f0 = A.feat[3 * i], f1 = A.feat[3 * i + 1], f2 = A.feat[3 * i + 2];
     const float w = A.rgbw ? A.rgbw[i] : 1.0f;
     const bool upd = A.update != 0;
+    np[8] = w;  // rgb_W when it is not trained
     float m[9], v[9], df[9], npg[9];
 #pragma unroll
     for (int e = 0; e < 9; ++e) {
@@ -1132,11 +1174,114 @@ __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
                                                   : (q == 2 ? 3 * (size_t)i + (e - 5) : (size_t)i));
         float *param = q == 0 ? A.xyz : (q == 1 ? A.chol : (q == 2 ? A.feat : A.rgbw));
         param[j] = pv;
+        np[e] = pv;
         A.state[q][0][j] = m[e];
         A.state[q][1][j] = v[e];
         A.state[q][2][j] = df[e];
         A.state[q][3][j] = npg[e];
     }
+}
+
+__global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
+    __shared__ int s_hits[kProjThreads / 64];
+    __shared__ unsigned s_cnt[kAggWin];
+    __shared__ int s_box[4][kProjThreads / 64];
+    if (blockIdx.x == 0) {
+        // the first workgroup (no splats): the loss, the tiles' error sums in a
+        // fixed order, in double; dispatched first so it runs beside the splats
+        __shared__ double s_l[2][4];
+        double s2 = 0.0, s1 = 0.0;
+        const int npair = A.ntiles >> 1;
+        const float4 *e4 = reinterpret_cast<const float4 *>(A.err);
+        for (int t0 = threadIdx.x; t0 < npair; t0 += kLossBatch * 256) {
+            float4 e[kLossBatch];
+#pragma unroll
+            for (int k = 0; k < kLossBatch; ++k) {
+                const int t = t0 + 256 * k;
+                e[k] = t < npair ? e4[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int k = 0; k < kLossBatch; ++k) {
+                s2 += (double)e[k].x;
+                s1 += (double)e[k].y;
+                s2 += (double)e[k].z;
+                s1 += (double)e[k].w;
+            }
+        }
+        if ((A.ntiles & 1) && threadIdx.x == 0) {
+            const float2 e = A.err[A.ntiles - 1];
+            s2 += (double)e.x;
+            s1 += (double)e.y;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            s2 += __shfl_xor(s2, off, 64);
+            s1 += __shfl_xor(s1, off, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            s_l[0][threadIdx.x >> 6] = s2;
+            s_l[1][threadIdx.x >> 6] = s1;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            A.loss[0] = (float)(((s_l[0][0] + s_l[0][1]) + (s_l[0][2] + s_l[0][3])) * A.inv_count);
+            A.loss[1] = (float)(((s_l[1][0] + s_l[1][1]) + (s_l[1][2] + s_l[1][3])) * A.inv_count);
+            // coherent host memory: the host stops waiting here, while the
+            // splat workgroups still run (later work on the stream is ordered
+            // after them anyway)
+            if (A.loss_seq)
+                __hip_atomic_store(reinterpret_cast<unsigned *>(A.loss) + 2, A.loss_seq,
+                                   __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+    }
+    const int t = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
+    float np[9];
+    if (!A.project) {
+        if (t < A.n) splat_step(A, t, np);
+        return;
+    }
+    // the fused projection of the next frame (frame_project_ordered_kernel's
+    // sequence on the stored parameters: the same records, slots and M)
+    if (blockIdx.x == 1 && threadIdx.x == 0) *A.m_clear = 0;  // the frame after's slot
+    const int i = t < A.n ? (A.order ? A.order[t] : t) : A.n;
+    const bool have = i < A.n;
+    SplatOut S;
+    S.P.rad = 0;
+    unsigned x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+    if (have) {
+        splat_step(A, i, np);
+        // activations (GaussianSplats_Represent.py:57-70) as load_project
+        const float mx = tanhf(np[0]), my = tanhf(np[1]);
+        float l11 = np[2], l21 = np[3], l22 = np[4];
+        if (A.chol_bound) {
+            l11 = l11 + A.chol_bound[0];
+            l21 = l21 + A.chol_bound[1];
+            l22 = l22 + A.chol_bound[2];
+        }
+        float r = np[5], g = np[6], b = np[7];
+        if (A.rgbw) {
+            r = r * np[8];
+            g = g * np[8];
+            b = b * np[8];
+        }
+        S = splat_out(i, mx, my, l11, l21, l22, r, g, b, 1.0f, A.hw, A.hh, A.tbx, A.tby);
+        A.rec[3 * i] = S.r0;
+        A.rec[3 * i + 1] = S.r1;
+        A.rec[3 * i + 2] = S.r2;
+        A.xys[i] = S.P.xy;
+        A.radii[i] = S.P.rad;
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) A.grad[4 * i + q] = z;  // the next step's atomics
+        if (A.key) {
+            A.key[i] = strip_key(S.P.xy.x, S.P.xy.y, S.P.rad, A.tbx, A.tby, A.key_invisible);
+            A.key_id[i] = i;
+        }
+        if (S.P.rad > 0) tile_bbox(S.P.xy.x, S.P.xy.y, (float)S.P.rad, A.tbx, A.tby, x0, y0, x1, y1);
+    }
+    const int hits = slab_insert_window(S, x0, y0, x1, y1, A.tbx, A.tby, A.counts, A.slab, s_cnt, s_box);
+    add_hits(hits, s_hits, A.m_acc);
 }
 
 struct TrainWs {
@@ -1269,6 +1414,7 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     // A/B knob 12: speculative slab records per tile (default kBSpec)
     T.spec = g_knobs[12] > 0 && g_knobs[12] <= 64 ? g_knobs[12] : kBSpec;
     T.diag = g_knobs[13];
+    T.grouped = g_knobs[15] != 1;
     if (g_knobs[5] == 2 && g_debug_ptr) {  // diagnostic: per-tile stamps
         T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
         auto kfn = train_tile_kernel<true>;
@@ -1317,6 +1463,27 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     // GSVC_TRAIN_LOSS_SEQ: ``loss`` is coherent host memory of 3 words; word 2
     // receives the call's sequence number (frame_index + 1, never 0)
     P.loss_seq = (adan_flags & GSVC_TRAIN_LOSS_SEQ) ? ((unsigned)frame_index + 1u) | 0x80000000u : 0u;
+    // PROJECT_NEXT: a separate projection launch after the splat kernel; A/B
+    // knob 14 = 2: the splat kernel projects the next frame itself, lane t
+    // updating splat order[t] -- measured slower (38.6 us vs 8.1 + 13.9 at
+    // trained 1080p/50k: the Adan state of spatially ordered splats is
+    // gathered, 36 scattered 4-byte loads and stores per splat)
+    const bool fuse = next && g_knobs[14] == 2;
+    if (fuse) {
+        const FrameSlots fn = frame_slots(w.f, ntiles, frame_index + 1);
+        P.project = 1;
+        P.tbx = tbx;
+        P.tby = tby;
+        P.order = use_order ? w.f.order : nullptr;
+        P.xys = w.f.xys;
+        P.counts = fn.counts;
+        P.slab = w.f.slab;
+        P.m_acc = fn.m_acc;
+        P.m_clear = fn.m_clear;
+        P.key = refresh ? w.f.okey : nullptr;
+        P.key_id = refresh ? w.f.okey_id : nullptr;
+        P.key_invisible = strip_key_invisible(tbx, tby);
+    }
     // one extra (first) workgroup sums the loss, beside the splat workgroups
     const int blocks = (num_points > 0 ? ceil_div(num_points, 256) : 0) + 1;
     hipEvent_t tev[2];
@@ -1325,6 +1492,7 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     timing_end(s, tslot, kTimingTrainSplat);
     rc = check_launch("train_step_sum: splats");
     if (rc) return rc;
+    if (fuse) return refresh ? splat_order_sort(w.f, num_points, tbx, tby, s) : GSVC_OK;
     if (next) return project(frame_slots(w.f, ntiles, frame_index + 1));
     if (!projected && refresh) return splat_order_sort(w.f, num_points, tbx, tby, s);
     return GSVC_OK;
