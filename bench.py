@@ -69,6 +69,8 @@ def parse():
                     help="launches per kernel timed by HIP events after the timed region")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--knob", action="append", default=[],
+                    help="A/B knob K=V (gsvc_debug_set) for kernel-variant comparisons")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: start the ranks, all-reduce, print the line (tests)")
@@ -372,6 +374,11 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     from gsvc_amd.frame import make_frame_model, synthetic_gt
+    if args.knob:
+        from gsvc_amd import _lib
+        for kv in args.knob:
+            k, v = kv.split("=")
+            _lib.load().gsvc_debug_set(int(k), int(v))
 
     # ---- headline: configs[2] training iterations, one frame per rank
     model = make_frame_model(H, W, args.splats, device, seed=1000 + rank)

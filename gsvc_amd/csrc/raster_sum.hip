@@ -51,7 +51,7 @@ constexpr int kChunk = 64;
 __device__ __forceinline__ const float4 *slot_rec(const float4 *head, const float4 *body, int j) {
     return j < kHeadSlots ? head + 3 * j : body + 3 * j;
 }
-constexpr int kSlice = kTilePix * 3 / 4;  // float4s of LDS per wave (3 KB)
+constexpr int kSlice = 200;  // float4s of LDS per wave (3.1 KB; sum_fwd_band's layout)
 
 // Forward kernel modes.  Production: the launcher picks kModeSparse (one wave
 // per tile) when the frame averages <= 8 entries per tile and kModeBanded
@@ -128,6 +128,30 @@ __device__ __forceinline__ bool ellipse_hits_rect(float x, float y, float a, flo
     const float ex = sqrtf(S2 * c / det) * 1.001f + 0.01f;
     const float ey = sqrtf(S2 * a / det) * 1.001f + 0.01f;
     return (x + ex >= x0) && (x - ex <= x1) && (y + ey >= y0) && (y - ey <= y1);
+}
+
+// The 4x4-pixel blocks of the 8-row band at (bx0, by0) (bit 4 * r + c: rows
+// by0 + 4r .. + 3, columns bx0 + 4c .. + 3) that splat (x, y, conic, o) can
+// reach with alpha >= 1/255 -- ellipse_hits_rect's test per block, so a block
+// left out holds no contributing pixel centre.
+__device__ __forceinline__ unsigned ellipse_band_blocks(float x, float y, float a, float b, float c,
+                                                        float o, float bx0, float by0) {
+    if (!(o > 0.0f)) return (o <= 0.0f) ? 0u : 0xffu;  // o <= 0: never valid; NaN: keep
+    const float det = a * c - b * b;
+    if (!(a > 0.0f) || !(det > 0.0f) || !(o < 3.0e38f) || !(fabsf(x) < 1e30f) || !(fabsf(y) < 1e30f))
+        return 0xffu;  // not positive definite / non-finite: no culling
+    const float lg = __logf(255.0f * o);
+    if (lg < -0.01f) return 0u;  // o < e^-0.01 / 255: alpha < 1/255 everywhere
+    const float S2 = 2.0f * (lg * 1.001f + 0.01f);
+    const float ex = sqrtf(S2 * c / det) * 1.001f + 0.01f;
+    const float ey = sqrtf(S2 * a / det) * 1.001f + 0.01f;
+    unsigned cols = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        cols |= ((x + ex >= bx0 + 4.0f * k) && (x - ex <= bx0 + 4.0f * k + 3.0f)) ? 1u << k : 0u;
+    const bool r0 = (y + ey >= by0) && (y - ey <= by0 + 3.0f);
+    const bool r1 = (y + ey >= by0 + 4.0f) && (y - ey <= by0 + 7.0f);
+    return (r0 ? cols : 0u) | (r1 ? cols << 4 : 0u);
 }
 
 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -338,11 +362,26 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
                                              const int *s_ids, const float4 *seg_rec,
                                              const float4 *seg_head, float4 spec0, float4 spec1,
                                              float4 spec2) {
+    // staged entries (slot kChunk: the grouped loop's no-op sentinel), their
+    // blocks, and the lane groups' lists [64 iterations][8 groups]
+    constexpr int kS = kChunk + 1, kS4 = (kS + 3) / 4;
     float4 *s_geo = s_slice;                                      // x, y, 0.5a, b
-    float4 *s_col = s_slice + kChunk;                             // 0.5c, opacity, r, g
-    float *s_blu = reinterpret_cast<float *>(s_slice + 2 * kChunk);
-    int *s_k = reinterpret_cast<int *>(s_slice + 2 * kChunk + kChunk / 4);
+    float4 *s_col = s_slice + kS;                                 // 0.5c, opacity, r, g
+    float *s_blu = reinterpret_cast<float *>(s_slice + 2 * kS);
+    int *s_k = reinterpret_cast<int *>(s_slice + 2 * kS + kS4);
+    unsigned char *s_gm = reinterpret_cast<unsigned char *>(s_slice + 2 * kS + 2 * kS4);
+    unsigned char *s_list = s_gm + kChunk;
+    static_assert(2 * kS + 2 * kS4 + (kChunk + 8 * kChunk) / 16 <= kSlice, "band LDS layout");
     const int lane = threadIdx.x & 63;
+    const bool grouped = A.grouped != 0;
+    if (grouped && lane == 0) {
+        // sigma = +inf at every pixel: alpha = 0 fails the test, no change
+        s_geo[kChunk] = make_float4(0.0f, 1e30f, 0.0f, 0.0f);
+        s_col[kChunk] = make_float4(1e30f, 1.0f, 0.0f, 0.0f);
+        s_blu[kChunk] = 0.0f;
+        s_k[kChunk] = 0;
+    }
+    const int grp = ((lane >> 5) << 2) | ((lane & 7) >> 1);  // the lane's 4x4 block
     const int ty = tile / A.tbx, tx = tile - ty * A.tbx;
     const int row0 = ty * kTile + band * 8;
     const int pi = row0 + (lane >> 3);
@@ -357,6 +396,7 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
     for (int base = 0; base < n; base += kChunk) {
         const int j = base + lane;
         bool keep = false;
+        unsigned gm = 0u;
         float4 geo = make_float4(0.f, 0.f, 0.f, 0.f), col = geo;
         float blu = 0.f;
         int id = 0x7fffffff;
@@ -377,8 +417,13 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
                 load_splat(A, ids_in_lds ? s_ids[j] : A.ids[range.x + j], geo, col, blu);
             }
             // 2 * (a/2) == a except for subnormal a, where culling is off anyway
-            keep = ellipse_hits_rect(geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, bx0,
-                                     bx0 + 15.0f, by0, by0 + 7.0f);
+            if (grouped) {
+                gm = ellipse_band_blocks(geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, bx0, by0);
+                keep = gm != 0u;
+            } else {
+                keep = ellipse_hits_rect(geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, bx0,
+                                         bx0 + 15.0f, by0, by0 + 7.0f);
+            }
         }
         const unsigned long long m = __ballot(keep);
         if (seg_rec) {
@@ -394,6 +439,7 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
                 s_col[pos] = col;
                 s_blu[pos] = blu;
                 s_k[pos] = range.x + rank;
+                s_gm[pos] = (unsigned char)gm;
             }
         } else if (keep) {
             const int pos = __popcll(m & lt);
@@ -401,9 +447,40 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
             s_col[pos] = col;
             s_blu[pos] = blu;
             s_k[pos] = range.x + j;
+            s_gm[pos] = (unsigned char)gm;
         }
         const int cnt = __popcll(m);
         wave_lds_sync();
+        if (grouped) {
+            // each group walks, in order, only the staged entries reaching its
+            // block; its list is padded with the sentinel to the longest
+            const unsigned gmt = lane < cnt ? s_gm[lane] : 0u;
+            *reinterpret_cast<unsigned long long *>(s_list + 8 * lane) = 0x4040404040404040ull;
+            __builtin_amdgcn_wave_barrier();
+            int maxlen = 0;
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const bool in = (gmt >> g) & 1u;
+                const unsigned long long mg = __ballot(in);
+                if (in) s_list[8 * __popcll(mg & lt) + g] = (unsigned char)lane;
+                maxlen = max(maxlen, __popcll(mg));
+            }
+            wave_lds_sync();
+            const unsigned char *ml = s_list + grp;
+            for (int it = 0; it < maxlen; ++it) {
+                const int t = ml[8 * it];
+                const float4 G = s_geo[t];
+                const float4 C = s_col[t];
+                const float bl = s_blu[t];
+                const int k = kIdx ? s_k[t] : 0;
+                const float dy = G.y - py;
+                const float cq = (C.x * dy) * dy;
+                const float bdy = G.w * dy;
+                blend_pair<kIdx>(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, pxv, k, ar, ag, ab, l0, l1);
+            }
+            wave_lds_sync();
+            continue;
+        }
         for (int t = 0; t < cnt; ++t) {
             const float4 G = s_geo[t];
             const float4 C = s_col[t];
@@ -714,6 +791,7 @@ void sum_fwd_args_init(SumFwdArgs &A) {
     A.sparse_max = g_knobs[3] > 0 ? g_knobs[3] : 8;
     // A/B knob 10: speculative slab records per tile (default all kHeadSlots)
     A.spec_slots = g_knobs[10] > 0 && g_knobs[10] < kHeadSlots ? g_knobs[10] : kHeadSlots;
+    A.grouped = g_knobs[15] != 1;
     A.layout = kLayoutHWC;
     A.frames = 1;
 }

@@ -555,6 +555,7 @@ __device__ __forceinline__ void seg_step8_sel(float (&g)[8], int key) {
 // key >= 0 (contiguous): lane i ends with the sum of its run's lanes <= i.
 // The wave_scan_dpp steps; a source lane is added only inside the run, so
 // each lane's sum covers exactly [max(run start, ...), i].
+template <bool kLong>
 __device__ __forceinline__ void wave_seg_sums(float (&g)[8], int key) {
     // finite unless some sum is inf / NaN (or the total overflows: then the
     // exact select form runs, which is still right)
@@ -567,8 +568,10 @@ __device__ __forceinline__ void wave_seg_sums(float (&g)[8], int key) {
         GSVC_FMAC_DPP8("row_shr:2 row_mask:0xf bank_mask:0xf");
         m = seg_mask<0x114, 0xf>(key);
         GSVC_FMAC_DPP8("row_shr:4 row_mask:0xf bank_mask:0xf");
-        m = seg_mask<0x118, 0xf>(key);
-        GSVC_FMAC_DPP8("row_shr:8 row_mask:0xf bank_mask:0xf");
+        if (kLong) {  // runs longer than 8 lanes
+            m = seg_mask<0x118, 0xf>(key);
+            GSVC_FMAC_DPP8("row_shr:8 row_mask:0xf bank_mask:0xf");
+        }
         m = seg_mask<0x142, 0xa>(key);
         GSVC_FMAC_DPP8("row_bcast:15 row_mask:0xa bank_mask:0xf");
         m = seg_mask<0x143, 0xc>(key);
@@ -577,7 +580,7 @@ __device__ __forceinline__ void wave_seg_sums(float (&g)[8], int key) {
         seg_step8_sel<0x111, 0xf>(g, key);  // row_shr:1
         seg_step8_sel<0x112, 0xf>(g, key);  // row_shr:2
         seg_step8_sel<0x114, 0xf>(g, key);  // row_shr:4
-        seg_step8_sel<0x118, 0xf>(g, key);  // row_shr:8
+        if (kLong) seg_step8_sel<0x118, 0xf>(g, key);  // row_shr:8
         seg_step8_sel<0x142, 0xa>(g, key);  // row_bcast:15 -> rows 1, 3
         seg_step8_sel<0x143, 0xc>(g, key);  // row_bcast:31 -> rows 2, 3
     }
@@ -992,12 +995,11 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                     // walk the row by its v_out word (the planes at fixed LDS
                     // offsets) with dx stepping by -1 (exact: ex - px is exact
                     // or, far off, rounds alike)
-                    const float *vf = &S.v[0][0];
-                    const int pe = row * kVRow + ce;
+                    const float *vp = &S.v[0][0] + row * kVRow + cs;
+                    const float *const ve = &S.v[0][0] + row * kVRow + ce;
                     float dx = ex - (tx0 + (float)cs);
-                    for (int pix = row * kVRow + cs; pix <= pe; ++pix, dx -= 1.0f) {
-                        const float Px = vf[pix], Py = vf[kTile * kVRow + pix],
-                                    Pz = vf[2 * kTile * kVRow + pix];
+                    for (; vp <= ve; ++vp, dx -= 1.0f) {
+                        const float Px = vp[0], Py = vp[kTile * kVRow], Pz = vp[2 * kTile * kVRow];
                         const float sgm = fmaf(fmaf(eha, dx, bdy), dx, cq);
                         const float vis = exp_neg(sgm);
                         const float al = fminf(1.0f, vis);  // opacity 1
@@ -1026,7 +1028,15 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             // alternatives: every item adding its sums with LDS float atomics
             // (2.9x slower kernel: the LDS serialises an entry's items); a packed
             // two-pixel loop (80 VGPRs, 6 waves per SIMD: 64.0 vs 58.5 us)
-            if (!(A.diag & 16)) wave_seg_sums(g, own);  // diag 16: no run sums (wrong)
+            // an entry has at most 8 items in a band unless rows split in two
+            // (brun < 16): runs of <= 8 lanes need no row_shr:8 step (a run
+            // crossing a 16-lane row still takes the row broadcast)
+            if (!(A.diag & 16)) {  // diag 16: no run sums (wrong)
+                if (A.brun < 16)
+                    wave_seg_sums<true>(g, own);
+                else
+                    wave_seg_sums<false>(g, own);
+            }
             const int own_next = __shfl_down(own, 1, 64);
             if (item < total && (lane == 63 || item + 1 == total || own_next != own)) {
 #pragma unroll
