@@ -51,7 +51,7 @@ constexpr int kChunk = 64;
 __device__ __forceinline__ const float4 *slot_rec(const float4 *head, const float4 *body, int j) {
     return j < kHeadSlots ? head + 3 * j : body + 3 * j;
 }
-constexpr int kSlice = 200;  // float4s of LDS per wave (3.1 KB; sum_fwd_band's layout)
+constexpr int kSlice = 220;  // float4s of LDS per wave (3.4 KB; sum_fwd_sparse's layout)
 
 // Forward kernel modes.  Production: the launcher picks kModeSparse (one wave
 // per tile) when the frame averages <= 8 entries per tile and kModeBanded
@@ -69,7 +69,11 @@ constexpr int kSlice = 200;  // float4s of LDS per wave (3.1 KB; sum_fwd_band's 
 // the dispatch rate of sparse tiles.
 enum { kModeAdaptive = 6, kModeSparse = 1, kModeBanded = 2, kModeStamp = 3, kModeNoBlend = 4,
        kModeNoStore = 5, kModeSparseStamp = 7 };
-constexpr int kDenseEntriesPerTile = 8;  // measured crossover: 20k splats (6.1 per tile) sparse 22.1 vs banded 23.7 us, 30k (9.1) equal
+// Banded (two waves per tile) only past this many entries per tile on average.
+// Measured with the lane-group lists (1080p, tools/fbench.py, profiles/r02/composite_modes/):
+// sparse wins from 3 to 62 entries per tile (trained 50k, 28 per tile: 43.0 vs 48.0 us per
+// frame; 62 per tile: 82.1 vs 93.8) and ties at 107 (138.4 vs 137.2).
+constexpr int kDenseEntriesPerTile = 96;
 
 // Diagnostic only (kModeStamp): s_memrealtime (100 MHz) stamps per tile,
 // written to the final_Ts slot reinterpreted as int64[ntiles][4].
@@ -130,16 +134,19 @@ __device__ __forceinline__ bool ellipse_hits_rect(float x, float y, float a, flo
     return (x + ex >= x0) && (x - ex <= x1) && (y + ey >= y0) && (y - ey <= y1);
 }
 
-// The 4x4-pixel blocks of the 8-row band at (bx0, by0) (bit 4 * r + c: rows
-// by0 + 4r .. + 3, columns bx0 + 4c .. + 3) that splat (x, y, conic, o) can
-// reach with alpha >= 1/255 -- ellipse_hits_rect's test per block, so a block
-// left out holds no contributing pixel centre.
-__device__ __forceinline__ unsigned ellipse_band_blocks(float x, float y, float a, float b, float c,
-                                                        float o, float bx0, float by0) {
-    if (!(o > 0.0f)) return (o <= 0.0f) ? 0u : 0xffu;  // o <= 0: never valid; NaN: keep
+// The 4x4-pixel blocks of the kRows-row strip at (bx0, by0) (bit 4 * r + c:
+// rows by0 + 4r .. + 3, columns bx0 + 4c .. + 3) that splat (x, y, conic, o)
+// can reach with alpha >= 1/255 -- ellipse_hits_rect's test per block, so a
+// block left out holds no contributing pixel centre.  kRows = 8: a band, 16:
+// the whole tile.
+template <int kRows>
+__device__ __forceinline__ unsigned ellipse_blocks(float x, float y, float a, float b, float c,
+                                                   float o, float bx0, float by0) {
+    constexpr unsigned kAll = (1u << kRows) - 1u;  // kRows / 4 row blocks x 4 column blocks
+    if (!(o > 0.0f)) return (o <= 0.0f) ? 0u : kAll;  // o <= 0: never valid; NaN: keep
     const float det = a * c - b * b;
     if (!(a > 0.0f) || !(det > 0.0f) || !(o < 3.0e38f) || !(fabsf(x) < 1e30f) || !(fabsf(y) < 1e30f))
-        return 0xffu;  // not positive definite / non-finite: no culling
+        return kAll;  // not positive definite / non-finite: no culling
     const float lg = __logf(255.0f * o);
     if (lg < -0.01f) return 0u;  // o < e^-0.01 / 255: alpha < 1/255 everywhere
     const float S2 = 2.0f * (lg * 1.001f + 0.01f);
@@ -149,9 +156,11 @@ __device__ __forceinline__ unsigned ellipse_band_blocks(float x, float y, float 
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         cols |= ((x + ex >= bx0 + 4.0f * k) && (x - ex <= bx0 + 4.0f * k + 3.0f)) ? 1u << k : 0u;
-    const bool r0 = (y + ey >= by0) && (y - ey <= by0 + 3.0f);
-    const bool r1 = (y + ey >= by0 + 4.0f) && (y - ey <= by0 + 7.0f);
-    return (r0 ? cols : 0u) | (r1 ? cols << 4 : 0u);
+    unsigned m = 0u;
+#pragma unroll
+    for (int r = 0; r < kRows / 4; ++r)
+        m |= ((y + ey >= by0 + 4.0f * r) && (y - ey <= by0 + 4.0f * r + 3.0f)) ? cols << (4 * r) : 0u;
+    return m;
 }
 
 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -244,38 +253,58 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
                                                const int *s_ids, const float4 *seg_rec,
                                                const float4 *seg_head, float4 spec0, float4 spec1,
                                                float4 spec2) {
+    // staged entries (slot kChunk: the grouped loop's no-op sentinel), their
+    // blocks, and the lane groups' lists [64 iterations][16 groups]
+    constexpr int kS = kChunk + 1, kS4 = (kS + 3) / 4;
     float4 *s_geo = s_slice;                           // x, y, 0.5a, b
-    float4 *s_col = s_slice + kChunk;                  // 0.5c, opacity, r, g
-    float *s_blu = (float *)(s_slice + 2 * kChunk);    // b
+    float4 *s_col = s_slice + kS;                      // 0.5c, opacity, r, g
+    float *s_blu = (float *)(s_slice + 2 * kS);        // b
+    unsigned short *s_gm = reinterpret_cast<unsigned short *>(s_slice + 2 * kS + kS4);
+    unsigned char *s_list = reinterpret_cast<unsigned char *>(s_slice + 2 * kS + kS4 + kChunk / 8);
+    static_assert(2 * kS + kS4 + kChunk / 8 + kChunk <= kSlice, "sparse LDS layout");
     const int lane = threadIdx.x & 63;
+    if (lane == 0) {
+        // sigma = +inf at every pixel: alpha = 0 fails the test, no change
+        s_geo[kChunk] = make_float4(0.0f, 1e30f, 0.0f, 0.0f);
+        s_col[kChunk] = make_float4(1e30f, 1.0f, 0.0f, 0.0f);
+        s_blu[kChunk] = 0.0f;
+    }
+    const int grp = ((lane >> 4) << 2) | (lane & 3);  // the lane's 4x4 block of the tile
     const int ty = tile / A.tbx, tx = tile - ty * A.tbx;
     const int pi = ty * kTile + (lane >> 2);
     const int pj = tx * kTile + ((lane & 3) << 2);
     const float py = (float)pi;
+    const float tx0f = (float)(tx * kTile), ty0f = (float)(ty * kTile);
     const float px0 = (float)pj, px1 = (float)(pj + 1), px2 = (float)(pj + 2), px3 = (float)(pj + 3);
     v2f ar01 = {init.x, init.x}, ag01 = {init.y, init.y}, ab01 = {init.z, init.z};
     v2f ar23 = ar01, ag23 = ag01, ab23 = ab01;
     const v2f px01 = {px0, px1}, px23 = {px2, px3};
     int l0 = 0, l1 = 0, l2 = 0, l3 = 0;
+    if (seg_rec) {
+        // <= 64 slab records in fill order: staged at their rank by id, before
+        // the chunk loop (the speculative records die here)
+        const int cnt = n;
+            // <= 64 slab records in fill order: staged at their rank by id
+        float4 geo = spec0, col = spec1, bx = spec2;
+        if (lane >= A.spec_slots && lane < cnt) {
+            const float4 *r = slot_rec(seg_head, seg_rec, lane);
+            geo = r[0];
+            col = r[1];
+            bx = r[2];
+        }
+        const int id = lane < cnt ? __float_as_int(bx.y) : 0x7fffffff;
+        const int rank = rank_below(id, cnt);
+        if (lane < cnt) {
+            s_geo[rank] = geo;
+            s_col[rank] = col;
+            s_blu[rank] = bx.x;
+            s_gm[rank] = (unsigned short)ellipse_blocks<16>(
+                geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, tx0f, ty0f);
+        }
+    }
     for (int base = 0; base < n; base += kChunk) {
         const int cnt = min(kChunk, n - base);
-        if (seg_rec) {
-            // <= 64 slab records in fill order: staged at their rank by id
-            float4 geo = spec0, col = spec1, bx = spec2;
-            if (lane >= A.spec_slots && lane < cnt) {
-                const float4 *r = slot_rec(seg_head, seg_rec, lane);
-                geo = r[0];
-                col = r[1];
-                bx = r[2];
-            }
-            const int id = lane < cnt ? __float_as_int(bx.y) : 0x7fffffff;
-            const int rank = rank_below(id, cnt);
-            if (lane < cnt) {
-                s_geo[rank] = geo;
-                s_col[rank] = col;
-                s_blu[rank] = bx.x;
-            }
-        } else if (lane < cnt) {
+        if (!seg_rec && lane < cnt) {  // (seg_rec: staged above, n <= 64: one chunk)
             float4 geo, col;
             float blu;
             const int j = base + lane;
@@ -283,11 +312,32 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
             s_geo[lane] = geo;
             s_col[lane] = col;
             s_blu[lane] = blu;
+            s_gm[lane] = (unsigned short)ellipse_blocks<16>(
+                geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, tx0f, ty0f);
+        }
+        wave_lds_sync();
+        // each 4x4 block's lanes walk, in order, only the staged entries
+        // reaching the block (the band path's argument: the pairs skipped
+        // contribute nothing); lists padded with the sentinel
+        const unsigned gmt = lane < cnt ? s_gm[lane] : 0u;
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        *reinterpret_cast<uint4 *>(s_list + 16 * lane) =
+            make_uint4(0x40404040u, 0x40404040u, 0x40404040u, 0x40404040u);
+        __builtin_amdgcn_wave_barrier();
+        int maxlen = 0;
+#pragma unroll 1
+        for (int g = 0; g < 16; ++g) {
+            const bool in = (gmt >> g) & 1u;
+            const unsigned long long mg = __ballot(in);
+            if (in) s_list[16 * __popcll(mg & lt) + g] = (unsigned char)lane;
+            maxlen = max(maxlen, __popcll(mg));
         }
         wave_lds_sync();
         if (kMode == kModeSparseStamp && base == 0 && lane == 0) A.stamps[4 * (size_t)tile + 1] = stamp();
         const int k0 = range.x + base;
-        for (int t = 0; t < cnt; ++t) {
+        const unsigned char *ml = s_list + grp;
+        for (int it = 0; it < maxlen; ++it) {
+            const int t = ml[16 * it];
             const float4 G = s_geo[t];
             const float4 C = s_col[t];
             const float bl = s_blu[t];
@@ -373,8 +423,7 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
     unsigned char *s_list = s_gm + kChunk;
     static_assert(2 * kS + 2 * kS4 + (kChunk + 8 * kChunk) / 16 <= kSlice, "band LDS layout");
     const int lane = threadIdx.x & 63;
-    const bool grouped = A.grouped != 0;
-    if (grouped && lane == 0) {
+    if (lane == 0) {
         // sigma = +inf at every pixel: alpha = 0 fails the test, no change
         s_geo[kChunk] = make_float4(0.0f, 1e30f, 0.0f, 0.0f);
         s_col[kChunk] = make_float4(1e30f, 1.0f, 0.0f, 0.0f);
@@ -417,13 +466,8 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
                 load_splat(A, ids_in_lds ? s_ids[j] : A.ids[range.x + j], geo, col, blu);
             }
             // 2 * (a/2) == a except for subnormal a, where culling is off anyway
-            if (grouped) {
-                gm = ellipse_band_blocks(geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, bx0, by0);
-                keep = gm != 0u;
-            } else {
-                keep = ellipse_hits_rect(geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, bx0,
-                                         bx0 + 15.0f, by0, by0 + 7.0f);
-            }
+            gm = ellipse_blocks<8>(geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, bx0, by0);
+            keep = gm != 0u;
         }
         const unsigned long long m = __ballot(keep);
         if (seg_rec) {
@@ -451,37 +495,23 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
         }
         const int cnt = __popcll(m);
         wave_lds_sync();
-        if (grouped) {
-            // each group walks, in order, only the staged entries reaching its
-            // block; its list is padded with the sentinel to the longest
-            const unsigned gmt = lane < cnt ? s_gm[lane] : 0u;
-            *reinterpret_cast<unsigned long long *>(s_list + 8 * lane) = 0x4040404040404040ull;
-            __builtin_amdgcn_wave_barrier();
-            int maxlen = 0;
-#pragma unroll
-            for (int g = 0; g < 8; ++g) {
-                const bool in = (gmt >> g) & 1u;
-                const unsigned long long mg = __ballot(in);
-                if (in) s_list[8 * __popcll(mg & lt) + g] = (unsigned char)lane;
-                maxlen = max(maxlen, __popcll(mg));
-            }
-            wave_lds_sync();
-            const unsigned char *ml = s_list + grp;
-            for (int it = 0; it < maxlen; ++it) {
-                const int t = ml[8 * it];
-                const float4 G = s_geo[t];
-                const float4 C = s_col[t];
-                const float bl = s_blu[t];
-                const int k = kIdx ? s_k[t] : 0;
-                const float dy = G.y - py;
-                const float cq = (C.x * dy) * dy;
-                const float bdy = G.w * dy;
-                blend_pair<kIdx>(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, pxv, k, ar, ag, ab, l0, l1);
-            }
-            wave_lds_sync();
-            continue;
+        // each group walks, in order, only the staged entries reaching its
+        // block; its list is padded with the sentinel to the longest
+        const unsigned gmt = lane < cnt ? s_gm[lane] : 0u;
+        *reinterpret_cast<unsigned long long *>(s_list + 8 * lane) = 0x4040404040404040ull;
+        __builtin_amdgcn_wave_barrier();
+        int maxlen = 0;
+#pragma unroll 1
+        for (int g = 0; g < 8; ++g) {
+            const bool in = (gmt >> g) & 1u;
+            const unsigned long long mg = __ballot(in);
+            if (in) s_list[8 * __popcll(mg & lt) + g] = (unsigned char)lane;
+            maxlen = max(maxlen, __popcll(mg));
         }
-        for (int t = 0; t < cnt; ++t) {
+        wave_lds_sync();
+        const unsigned char *ml = s_list + grp;
+        for (int it = 0; it < maxlen; ++it) {
+            const int t = ml[8 * it];
             const float4 G = s_geo[t];
             const float4 C = s_col[t];
             const float bl = s_blu[t];
@@ -791,7 +821,6 @@ void sum_fwd_args_init(SumFwdArgs &A) {
     A.sparse_max = g_knobs[3] > 0 ? g_knobs[3] : 8;
     // A/B knob 10: speculative slab records per tile (default all kHeadSlots)
     A.spec_slots = g_knobs[10] > 0 && g_knobs[10] < kHeadSlots ? g_knobs[10] : kHeadSlots;
-    A.grouped = g_knobs[15] != 1;
     A.layout = kLayoutHWC;
     A.frames = 1;
 }

@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--splats", type=int, nargs="+", default=[10000, 50000])
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--chol-scale", type=float, default=1.0)
+    ap.add_argument("--trained", type=int, default=0,
+                    help="render the bench's frame model after this many training iterations "
+                         "(trained density) instead of random splats")
     ap.add_argument("--modes", type=int, nargs="+", default=[0],
                     help="rasterizer modes (gsvc_debug_set(0)); 0 = automatic")
     ap.add_argument("--knob", type=int, nargs=2, action="append", default=[],
@@ -49,6 +52,17 @@ def main():
         chol = (torch.rand(n, 3, generator=g) * args.chol_scale).to(dev)
         feat = torch.rand(n, 3, generator=g).to(dev)
         bound = torch.tensor([0.5, 0.0, 0.5], device=dev)
+        if args.trained > 0:
+            from gsvc_amd.frame import make_frame_model, synthetic_gt
+            model = make_frame_model(H, W, n, dev, seed=1000)
+            gt = synthetic_gt(H, W, 8, "cpu").to(dev)
+            for it in range(1, args.trained + 1):
+                model.train_iter(gt, it)
+            torch.cuda.synchronize()
+            xyz = model._xyz.detach().clone()
+            chol = model._cholesky.detach().clone()
+            feat = model.get_features.detach().clone()
+            del model
         bg = torch.ones(3, device=dev)
         ws_bytes = L.size("gsvc_render_frame_workspace_bytes", n, H, W)
         ws = torch.zeros((ws_bytes,), dtype=torch.uint8, device=dev)

@@ -33,6 +33,14 @@ SHAPES = {
     "8 groups 4x4": [(r, r + 3, c, c + 3) for r in (0, 4) for c in (0, 4, 8, 12)],
     "8 groups 2x8": [(r, r + 1, c, c + 7) for r in (0, 2, 4, 6) for c in (0, 8)],
 }
+# one wave over the whole 16x16 tile (the sparse composite, 4 pixels per lane)
+TILE_SHAPES = {
+    "tile 16x16 (sparse, current)": [(0, 15, 0, 15)],
+    "tile: 16 groups 4x4": [(r, r + 3, c, c + 3) for r in (0, 4, 8, 12) for c in (0, 4, 8, 12)],
+    "tile: 8 groups 4x8": [(r, r + 3, c, c + 7) for r in (0, 4, 8, 12) for c in (0, 8)],
+    "tile: 8 groups 8x4": [(r, r + 7, c, c + 3) for r in (0, 8) for c in (0, 4, 8, 12)],
+    "tile: 4 groups 8x8": [(r, r + 7, c, c + 7) for r in (0, 8) for c in (0, 8)],
+}
 
 
 def main():
@@ -48,6 +56,7 @@ def main():
     ntiles = tb[0] * tb[1]
     step = a.tiles if a.tiles > 0 else 1
     iters = {k: 0 for k in SHAPES}
+    titers = {k: 0 for k in TILE_SHAPES}
     inside = 0
     for t in range(0, ntiles, step):
         lo, hi = bins[t]
@@ -56,6 +65,12 @@ def main():
             continue
         ty, tx = divmod(t, tb[0])
         x0, x1, y0, y1, ok = rects(xys, conics, ids, tx * 16.0, ty * 16.0)
+        for k, groups in TILE_SHAPES.items():
+            best = 0
+            for (r0, r1, c0, c1) in groups:
+                hit = ok & (y0 <= r1) & (y1 >= r0) & (x0 <= c1) & (x1 >= c0)
+                best = max(best, int(hit.sum()))
+            titers[k] += best
         for band in (0, 1):
             b0 = 8 * band
             for k, groups in SHAPES.items():
@@ -72,6 +87,10 @@ def main():
     for k, v in iters.items():
         print(f"{k:22s} wave iterations {v * step / 1e3:8.1f} k  pairs evaluated "
               f"{v * step * 128 / 1e6:6.2f} M  ({100 * (v / base - 1):+.1f} %)")
+    tb0 = titers["tile 16x16 (sparse, current)"]
+    for k, v in titers.items():
+        print(f"{k:28s} wave iterations {v * step / 1e3:8.1f} k  pairs evaluated "
+              f"{v * step * 256 / 1e6:6.2f} M  ({100 * (v / tb0 - 1):+.1f} %)")
 
 
 if __name__ == "__main__":
