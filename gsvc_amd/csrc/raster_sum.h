@@ -17,6 +17,7 @@ struct SumFwdArgs {
     bool vec_chw;  // CHW: W % 4 == 0, H*W % 4 == 0, 16-byte aligned
     int store_policy;  // CHW plane stores: kStore* (gsvc_debug_set(7) selects)
     int spec_slots;    // frame path: slab records loaded with the count (<= kHeadSlots)
+    int group_min;     // sparse chunks of <= this many entries skip the lane-group lists
     const int *m_dev;  // device num_intersects (NULL: > 0); 0 -> background
     const float *bg;
     const int *ids;

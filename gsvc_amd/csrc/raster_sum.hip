@@ -74,6 +74,9 @@ enum { kModeAdaptive = 6, kModeSparse = 1, kModeBanded = 2, kModeStamp = 3, kMod
 // sparse wins from 3 to 62 entries per tile (trained 50k, 28 per tile: 43.0 vs 48.0 us per
 // frame; 62 per tile: 82.1 vs 93.8) and ties at 107 (138.4 vs 137.2).
 constexpr int kDenseEntriesPerTile = 96;
+// A sparse tile's chunk of at most this many entries is blended by every lane
+// without the lane-group lists (A/B knob 15 = v > 0 sets it to v - 1).
+constexpr int kGroupMinDefault = 24;
 
 // Diagnostic only (kModeStamp): s_memrealtime (100 MHz) stamps per tile,
 // written to the final_Ts slot reinterpreted as int64[ntiles][4].
@@ -152,14 +155,17 @@ __device__ __forceinline__ unsigned ellipse_blocks(float x, float y, float a, fl
     const float S2 = 2.0f * (lg * 1.001f + 0.01f);
     const float ex = sqrtf(S2 * c / det) * 1.001f + 0.01f;
     const float ey = sqrtf(S2 * a / det) * 1.001f + 0.01f;
+    // in strip coordinates, so the block bounds are literals (the origin
+    // shift rounds by < 2^-12 px at 1080p, far inside the 0.01 px margin)
+    const float u = x - bx0, v = y - by0;
     unsigned cols = 0u;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-        cols |= ((x + ex >= bx0 + 4.0f * k) && (x - ex <= bx0 + 4.0f * k + 3.0f)) ? 1u << k : 0u;
+        cols |= ((u + ex >= 4.0f * k) && (u - ex <= 4.0f * k + 3.0f)) ? 1u << k : 0u;
     unsigned m = 0u;
 #pragma unroll
     for (int r = 0; r < kRows / 4; ++r)
-        m |= ((y + ey >= by0 + 4.0f * r) && (y - ey <= by0 + 4.0f * r + 3.0f)) ? cols << (4 * r) : 0u;
+        m |= ((v + ey >= 4.0f * r) && (v - ey <= 4.0f * r + 3.0f)) ? cols << (4 * r) : 0u;
     return m;
 }
 
@@ -204,6 +210,15 @@ __device__ __forceinline__ void st_f2(float *p, float a, float b, int policy) {
 __device__ __forceinline__ float clamp01(float x) {
     // torch.clamp(x, 0, 1): NaN stays NaN
     return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x);
+}
+
+// A tile's first pixel coordinate as a float, converted where it is used (the
+// asm keeps the compiler from hoisting the conversion to the kernel entry and
+// holding -- and, at 64 VGPRs, spilling -- the value across the blend loops).
+__device__ __forceinline__ float tile_origin(int t) {
+    int v = t * kTile;
+    asm volatile("" : "+s"(v));
+    return (float)v;
 }
 
 // Gather splat g: geo = {x, y, a/2, b}, col = {c/2, opacity, r, g}, blu = b.
@@ -269,12 +284,11 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         s_col[kChunk] = make_float4(1e30f, 1.0f, 0.0f, 0.0f);
         s_blu[kChunk] = 0.0f;
     }
-    const int grp = ((lane >> 4) << 2) | (lane & 3);  // the lane's 4x4 block of the tile
+    const int kGroupMin = A.group_min;
     const int ty = tile / A.tbx, tx = tile - ty * A.tbx;
     const int pi = ty * kTile + (lane >> 2);
     const int pj = tx * kTile + ((lane & 3) << 2);
     const float py = (float)pi;
-    const float tx0f = (float)(tx * kTile), ty0f = (float)(ty * kTile);
     const float px0 = (float)pj, px1 = (float)(pj + 1), px2 = (float)(pj + 2), px3 = (float)(pj + 3);
     v2f ar01 = {init.x, init.x}, ag01 = {init.y, init.y}, ab01 = {init.z, init.z};
     v2f ar23 = ar01, ag23 = ag01, ab23 = ab01;
@@ -298,8 +312,9 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
             s_geo[rank] = geo;
             s_col[rank] = col;
             s_blu[rank] = bx.x;
-            s_gm[rank] = (unsigned short)ellipse_blocks<16>(
-                geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, tx0f, ty0f);
+            if (n > kGroupMin)
+                s_gm[rank] = (unsigned short)ellipse_blocks<16>(
+                    geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, tile_origin(tx), tile_origin(ty));
         }
     }
     for (int base = 0; base < n; base += kChunk) {
@@ -312,13 +327,30 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
             s_geo[lane] = geo;
             s_col[lane] = col;
             s_blu[lane] = blu;
-            s_gm[lane] = (unsigned short)ellipse_blocks<16>(
-                geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, tx0f, ty0f);
+            if (cnt > kGroupMin)
+                s_gm[lane] = (unsigned short)ellipse_blocks<16>(
+                    geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, tile_origin(tx), tile_origin(ty));
         }
         wave_lds_sync();
-        // each 4x4 block's lanes walk, in order, only the staged entries
-        // reaching the block (the band path's argument: the pairs skipped
-        // contribute nothing); lists padded with the sentinel
+        const int k0 = range.x + base;
+        if (cnt <= kGroupMin) {
+            // a few entries: every lane walks them all (the lists would cost
+            // more than the pairs they skip)
+            if (kMode == kModeSparseStamp && base == 0 && lane == 0) A.stamps[4 * (size_t)tile + 1] = stamp();
+            for (int t = 0; t < cnt; ++t) {
+                const float4 G = s_geo[t];
+                const float4 C = s_col[t];
+                const float bl = s_blu[t];
+                const float dy = G.y - py;
+                const float cq = (C.x * dy) * dy;
+                const float bdy = G.w * dy;
+                const int k = k0 + t;
+                blend_pair<kIdx>(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, px01, k, ar01, ag01, ab01, l0, l1);
+                blend_pair<kIdx>(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, px23, k, ar23, ag23, ab23, l2, l3);
+            }
+            wave_lds_sync();
+            continue;
+        }
         const unsigned gmt = lane < cnt ? s_gm[lane] : 0u;
         const unsigned long long lt = (1ull << lane) - 1ull;
         *reinterpret_cast<uint4 *>(s_list + 16 * lane) =
@@ -334,8 +366,8 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         }
         wave_lds_sync();
         if (kMode == kModeSparseStamp && base == 0 && lane == 0) A.stamps[4 * (size_t)tile + 1] = stamp();
-        const int k0 = range.x + base;
-        const unsigned char *ml = s_list + grp;
+        // the lane's 4x4 block of the tile
+        const unsigned char *ml = s_list + (((lane >> 4) << 2) | (lane & 3));
         for (int it = 0; it < maxlen; ++it) {
             const int t = ml[16 * it];
             const float4 G = s_geo[t];
@@ -821,6 +853,7 @@ void sum_fwd_args_init(SumFwdArgs &A) {
     A.sparse_max = g_knobs[3] > 0 ? g_knobs[3] : 8;
     // A/B knob 10: speculative slab records per tile (default all kHeadSlots)
     A.spec_slots = g_knobs[10] > 0 && g_knobs[10] < kHeadSlots ? g_knobs[10] : kHeadSlots;
+    A.group_min = g_knobs[15] > 0 ? g_knobs[15] - 1 : kGroupMinDefault;
     A.layout = kLayoutHWC;
     A.frames = 1;
 }
