@@ -188,7 +188,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_ordered_kernel(
     __shared__ int s_box[4][kProjThreads / 64];
     const int tid = threadIdx.x, lane = tid & 63;
     const int t = blockIdx.x * blockDim.x + tid;
-    long long *st = kStamp ? stamps + 4 * (size_t)(t >> 6) : nullptr;
+    long long *st = kStamp ? stamps + 8 * (size_t)(t >> 6) : nullptr;
     if (kStamp && lane == 0) st[0] = proj_stamp();
     if (blockIdx.x == 0 && tid == 0) *m_clear = 0;  // the next frame's slot
     const int i = t < n ? (order ? order[t] : t) : n;  // order NULL: identity
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_ordered_kernel(
         if (S.P.rad > 0) tile_bbox(S.P.xy.x, S.P.xy.y, (float)S.P.rad, tbx, tby, x0, y0, x1, y1);
     }
     if (kStamp && lane == 0) st[1] = proj_stamp();
-    const int hits = slab_insert_window(S, x0, y0, x1, y1, tbx, tby, counts, slab, s_cnt, s_box);
+    const int hits = slab_insert_window(S, x0, y0, x1, y1, tbx, tby, counts, slab, s_cnt, s_box, st);
     if (kStamp) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) st[2] = proj_stamp();

@@ -178,8 +178,18 @@ __device__ __forceinline__ int slab_insert_window(const SplatOut &S, unsigned x0
                                                   unsigned x1, unsigned y1, int tbx, int tby,
                                                   unsigned *__restrict__ counts,
                                                   float4 *__restrict__ slab, unsigned *s_cnt,
-                                                  int (*s_box)[kProjThreads / 64]) {
+                                                  int (*s_box)[kProjThreads / 64],
+                                                  long long *st = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // diagnostic (st != NULL): s_memrealtime per wave after each phase
+    auto mark = [&](int k) {
+        if (st) {
+            long long t;
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memrealtime %0\n\ts_waitcnt lgkmcnt(0)"
+                         : "=s"(t)::"memory");
+            if (lane == 0) st[k] = t;
+        }
+    };
     const bool vis = x1 > x0 && y1 > y0;
     const bool small = vis && (x1 - x0) * (y1 - y0) <= (unsigned)kAggArea;
     // the window of the block's small bboxes
@@ -208,6 +218,7 @@ __device__ __forceinline__ int slab_insert_window(const SplatOut &S, unsigned x0
     }
     const int ww = bx1 - bx0, wh = by1 - by0;
     const bool agg = ww > 0 && wh > 0 && ww * wh <= kAggWin;  // block-uniform
+    mark(4);
     int hits = 0;
     if (vis && !(agg && small))
         hits = slab_insert_pairs<8>(S.P.xy.x, S.P.xy.y, S.P.rad, tbx, tby, S.r0, S.r1, S.r2,
@@ -222,6 +233,7 @@ __device__ __forceinline__ int slab_insert_window(const SplatOut &S, unsigned x0
                     atomicAdd(&s_cnt[((int)y - by0) * ww + ((int)x - bx0)], 1u);
         }
         __syncthreads();
+        mark(5);
         // one device-scope atomic per touched tile: the window's base slots
         for (int c = tid; c < cells; c += kProjThreads) {
             const unsigned v = s_cnt[c];
@@ -231,6 +243,7 @@ __device__ __forceinline__ int slab_insert_window(const SplatOut &S, unsigned x0
             }
         }
         __syncthreads();
+        mark(6);
         if (small) {
             const int ntiles = tbx * tby;
             for (unsigned y = y0; y < y1; ++y)
@@ -246,6 +259,7 @@ __device__ __forceinline__ int slab_insert_window(const SplatOut &S, unsigned x0
             hits += (int)((x1 - x0) * (y1 - y0));
         }
     }
+    mark(7);
     return hits;
 }
 

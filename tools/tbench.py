@@ -129,7 +129,7 @@ def main():
         import numpy as np
         from gsvc_amd import _lib as L
         lib = L.load()
-        st = torch.zeros(((a.splats + 63) // 64, 4), dtype=torch.int64, device=dev)
+        st = torch.zeros(((a.splats + 63) // 64, 8), dtype=torch.int64, device=dev)
         lib.gsvc_debug_set_ptr(ctypes.c_void_p(st.data_ptr()))
         lib.gsvc_debug_set(5, 1)
         model.train_iter(gt, a.warmup + a.iters + 300)
@@ -143,6 +143,11 @@ def main():
         print(json.dumps(dict(proj_stamps="percentiles 0/10/50/90/100 (us)", waves=int(len(t)),
                               start=q(t[:, 0] - t0), project=q(t[:, 1] - t[:, 0]),
                               insert=q(t[:, 2] - t[:, 1]), reduce=q(t[:, 3] - t[:, 2]),
+                              window=q(t[:, 4] - t[:, 1]),
+                              lds_count=q((t[:, 5] - t[:, 4])[t[:, 6] > 0]),
+                              base_atomics=q((t[:, 6] - t[:, 5])[t[:, 6] > 0]),
+                              slab_stores=q((t[:, 7] - t[:, 6])[t[:, 6] > 0]),
+                              windowed_waves=int((t[:, 6] > 0).sum()),
                               end=q(t[:, 3] - t0))), flush=True)
     if a.stamps:
         import ctypes
