@@ -28,7 +28,6 @@
 #include "adan.h"
 #include "binning.h"
 #include "frame.h"
-#include "frame_dev.h"
 #include "tile_ids.h"
 
 namespace gsvc {
@@ -1077,18 +1076,6 @@ struct TrainSplatArgs {
     const float2 *err;
     float *loss;         // [2]: mean squared error, mean absolute error
     unsigned loss_seq;   // non-zero: stored into word 2 of ``loss`` after the losses
-    // project != 0 (update only): the next frame's projection, fused -- lane t
-    // updates splat order[t] (NULL: t) and projects it from the parameters it
-    // has just written, as frame_project_ordered_kernel would (frame_dev.h)
-    int project, tbx, tby;
-    const int *order;
-    float2 *xys;
-    unsigned *counts;
-    float4 *slab;
-    int *m_acc, *m_clear;
-    unsigned *key;       // optional: strip keys and ids for the next order
-    int *key_id;
-    unsigned key_invisible;
 };
 
 // The loss workgroup's loads per round: 16 tile pairs per thread in flight, so
@@ -1096,9 +1083,8 @@ struct TrainSplatArgs {
 constexpr int kLossBatch = 16;
 
 // One splat's step: the projection VJP, activation VJPs and the Adan update of
-// its elements (update == 0: the gradients into grads_out); np receives the
-// parameters as stored (xyz 2, chol 3, feat 3, rgb_W).
-__device__ __forceinline__ void splat_step(const TrainSplatArgs &A, int i, float (&np)[9]) {
+// its elements (update == 0: the gradients into grads_out).
+__device__ __forceinline__ void splat_step(const TrainSplatArgs &A, int i) {
     // Every operand is loaded up front, before any arithmetic: one round trip
     // per lane instead of three (gradient + radius -> record -> Adan state).
     // rec is written for every splat by the projection, so its load needs no
@@ -1112,7 +1098,6 @@ __device__ __forceinline__ void splat_step(const TrainSplatArgs &A, int i, float
     const float f0 = A.feat[3 * i], f1 = A.feat[3 * i + 1], f2 = A.feat[3 * i + 2];
     const float w = A.rgbw ? A.rgbw[i] : 1.0f;
     const bool upd = A.update != 0;
-    np[8] = w;  // rgb_W when it is not trained
     float m[9], v[9], df[9], npg[9];
 #pragma unroll
     for (int e = 0; e < 9; ++e) {
@@ -1184,7 +1169,6 @@ __device__ __forceinline__ void splat_step(const TrainSplatArgs &A, int i, float
                                                   : (q == 2 ? 3 * (size_t)i + (e - 5) : (size_t)i));
         float *param = q == 0 ? A.xyz : (q == 1 ? A.chol : (q == 2 ? A.feat : A.rgbw));
         param[j] = pv;
-        np[e] = pv;
         A.state[q][0][j] = m[e];
         A.state[q][1][j] = v[e];
         A.state[q][2][j] = df[e];
@@ -1193,9 +1177,6 @@ __device__ __forceinline__ void splat_step(const TrainSplatArgs &A, int i, float
 }
 
 __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
-    __shared__ int s_hits[kProjThreads / 64];
-    __shared__ unsigned s_cnt[kAggWin];
-    __shared__ int s_box[4][kProjThreads / 64];
     if (blockIdx.x == 0) {
         // the first workgroup (no splats): the loss, the tiles' error sums in a
         // fixed order, in double; dispatched first so it runs beside the splats
@@ -1246,52 +1227,7 @@ __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
         return;
     }
     const int t = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
-    float np[9];
-    if (!A.project) {
-        if (t < A.n) splat_step(A, t, np);
-        return;
-    }
-    // the fused projection of the next frame (frame_project_ordered_kernel's
-    // sequence on the stored parameters: the same records, slots and M)
-    if (blockIdx.x == 1 && threadIdx.x == 0) *A.m_clear = 0;  // the frame after's slot
-    const int i = t < A.n ? (A.order ? A.order[t] : t) : A.n;
-    const bool have = i < A.n;
-    SplatOut S;
-    S.P.rad = 0;
-    unsigned x0 = 0, y0 = 0, x1 = 0, y1 = 0;
-    if (have) {
-        splat_step(A, i, np);
-        // activations (GaussianSplats_Represent.py:57-70) as load_project
-        const float mx = tanhf(np[0]), my = tanhf(np[1]);
-        float l11 = np[2], l21 = np[3], l22 = np[4];
-        if (A.chol_bound) {
-            l11 = l11 + A.chol_bound[0];
-            l21 = l21 + A.chol_bound[1];
-            l22 = l22 + A.chol_bound[2];
-        }
-        float r = np[5], g = np[6], b = np[7];
-        if (A.rgbw) {
-            r = r * np[8];
-            g = g * np[8];
-            b = b * np[8];
-        }
-        S = splat_out(i, mx, my, l11, l21, l22, r, g, b, 1.0f, A.hw, A.hh, A.tbx, A.tby);
-        A.rec[3 * i] = S.r0;
-        A.rec[3 * i + 1] = S.r1;
-        A.rec[3 * i + 2] = S.r2;
-        A.xys[i] = S.P.xy;
-        A.radii[i] = S.P.rad;
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) A.grad[4 * i + q] = z;  // the next step's atomics
-        if (A.key) {
-            A.key[i] = strip_key(S.P.xy.x, S.P.xy.y, S.P.rad, A.tbx, A.tby, A.key_invisible);
-            A.key_id[i] = i;
-        }
-        if (S.P.rad > 0) tile_bbox(S.P.xy.x, S.P.xy.y, (float)S.P.rad, A.tbx, A.tby, x0, y0, x1, y1);
-    }
-    const int hits = slab_insert_window(S, x0, y0, x1, y1, A.tbx, A.tby, A.counts, A.slab, s_cnt, s_box);
-    add_hits(hits, s_hits, A.m_acc);
+    if (t < A.n) splat_step(A, t);
 }
 
 struct TrainWs {
@@ -1473,27 +1409,6 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     // GSVC_TRAIN_LOSS_SEQ: ``loss`` is coherent host memory of 3 words; word 2
     // receives the call's sequence number (frame_index + 1, never 0)
     P.loss_seq = (adan_flags & GSVC_TRAIN_LOSS_SEQ) ? ((unsigned)frame_index + 1u) | 0x80000000u : 0u;
-    // PROJECT_NEXT: a separate projection launch after the splat kernel; A/B
-    // knob 14 = 2: the splat kernel projects the next frame itself, lane t
-    // updating splat order[t] -- measured slower (38.6 us vs 8.1 + 13.9 at
-    // trained 1080p/50k: the Adan state of spatially ordered splats is
-    // gathered, 36 scattered 4-byte loads and stores per splat)
-    const bool fuse = next && g_knobs[14] == 2;
-    if (fuse) {
-        const FrameSlots fn = frame_slots(w.f, ntiles, frame_index + 1);
-        P.project = 1;
-        P.tbx = tbx;
-        P.tby = tby;
-        P.order = use_order ? w.f.order : nullptr;
-        P.xys = w.f.xys;
-        P.counts = fn.counts;
-        P.slab = w.f.slab;
-        P.m_acc = fn.m_acc;
-        P.m_clear = fn.m_clear;
-        P.key = refresh ? w.f.okey : nullptr;
-        P.key_id = refresh ? w.f.okey_id : nullptr;
-        P.key_invisible = strip_key_invisible(tbx, tby);
-    }
     // one extra (first) workgroup sums the loss, beside the splat workgroups
     const int blocks = (num_points > 0 ? ceil_div(num_points, 256) : 0) + 1;
     hipEvent_t tev[2];
@@ -1502,7 +1417,6 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     timing_end(s, tslot, kTimingTrainSplat);
     rc = check_launch("train_step_sum: splats");
     if (rc) return rc;
-    if (fuse) return refresh ? splat_order_sort(w.f, num_points, tbx, tby, s) : GSVC_OK;
     if (next) return project(frame_slots(w.f, ntiles, frame_index + 1));
     if (!projected && refresh) return splat_order_sort(w.f, num_points, tbx, tby, s);
     return GSVC_OK;
