@@ -212,6 +212,25 @@ def roofline(kernel, nbytes, times_ms, prof=None, prof_key=None, timing=None):
     return r
 
 
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 2  # G wave64 VALU instructions/s (2 cycles each per SIMD)
+
+
+def valu_roofline(kernel_key, avg_us):
+    """The compute-side bound of a tile kernel: its PMC VALU wave-instructions
+    per launch (profiles/pmc_valu.json, committed rocprofv3 pass) over the
+    measured launch time, against the chip's VALU issue rate."""
+    try:
+        with open(os.path.join(REPO, "profiles", "pmc_valu.json")) as f:
+            d = json.load(f)[kernel_key]
+    except (OSError, ValueError, KeyError):
+        return None
+    insts = d["SQ_INSTS_VALU"]
+    achieved = insts / (avg_us * 1e-6) / 1e9
+    return {"bound": "valu", "insts_per_launch": insts, "achieved": round(achieved, 1),
+            "peak": VALU_PEAK_GINST, "unit": "G wave-instructions/s",
+            "frac": round(achieved / VALU_PEAK_GINST, 4), "source": "profiles/pmc_valu.json"}
+
+
 def cpu_baseline(n_splats, seconds):
     """The CPU restatement of the same training iteration (oracle/oracle.py
     train_iter_sum: project + bin + sum-raster + clamp + L2 + raster and
@@ -421,6 +440,11 @@ def main():
     prof = load_profile(f"train_{args.splats}")
     roof = roofline("train_tile_kernel", train_tile_bytes(shape), kt["train_tile"], prof,
                     "train_tile")
+    # the tile kernel is VALU/latency bound at trained density:
+    # its VALU issue fraction beside the HBM roofline
+    vr = valu_roofline("train_tile", roof.get("trace_avg_kernel_us") or roof["avg_kernel_us"])
+    if vr:
+        roof["valu"] = vr
     kernels = {
         "train_tile": roof,
         "frame_project": roofline("frame_project_ordered_kernel", project_bytes(shape, args.splats),
