@@ -50,7 +50,7 @@ struct TrainTileArgs {
     float2 *err;      // [ntiles]: sum of squared, sum of absolute errors
     int brun;         // band kernel: a rectangle row wider than this is two work items
     int spec;         // band kernel: slab records loaded with the count
-    int grouped;      // band kernel forward: lane-group entry lists (A/B knob 15 = 1: off)
+    int grouped;      // band kernel forward: lane-group entry lists (A/B knob 14 = 1: off)
     int diag;         // diagnostic knob 13 (timing experiments only; wrong results):
                       // bits 2 no backward, 4 no forward
                       // blending, 8 no backward pixel work, 16 no run sums, 32 no atomics;
@@ -1360,7 +1360,7 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     // A/B knob 12: speculative slab records per tile (default kBSpec)
     T.spec = g_knobs[12] > 0 && g_knobs[12] <= 64 ? g_knobs[12] : kBSpec;
     T.diag = g_knobs[13];
-    T.grouped = g_knobs[15] != 1;
+    T.grouped = g_knobs[14] != 1;
     if (g_knobs[5] == 2 && g_debug_ptr) {  // diagnostic: per-tile stamps
         T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
         auto kfn = train_tile_kernel<true>;

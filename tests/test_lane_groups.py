@@ -1,0 +1,97 @@
+"""The lane-group entry lists: each group of lanes walks
+only the entries whose alpha >= 1/255 rectangle reaches its 4x4-pixel block.
+Skipped pairs contribute nothing in the reference, so every variant must be
+bit-identical: lists always on / the default threshold / never, the sparse
+and banded composites, and the fused training step's forward with and
+without its lists (A/B knobs 15 and 14), at random-init and trained-like
+densities (3 to ~60 entries per tile)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+H, W = 1080, 1920
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _tb(h, w):
+    return ((w + 15) // 16, (h + 15) // 16, 1)
+
+
+def _knobs(lib, pairs):
+    return [(k, lib.gsvc_debug_set(k, v)) for k, v in pairs]
+
+
+def _restore(lib, olds):
+    for k, v in reversed(olds):
+        lib.gsvc_debug_set(k, v)
+
+
+@pytest.mark.parametrize("n,chol", [(10000, 1.0), (50000, 1.0), (50000, 3.0), (20000, 8.0)])
+def test_composite_lists_bit_identical(cuda, oracle, n, chol):
+    from gsvc_amd import _lib
+    from gsvc_amd.render import render_sum_frame
+    lib = _lib.load()
+    means, L, colors, opac = oracle.synthetic_frame(n, seed=n + 17, rgb_w=2.0, chol_scale=chol)
+    bg = torch.ones(3, device="cuda")
+    outs = {}
+    # mode 1 sparse / 2 banded; knob 15 = 1: lists on every chunk, 65: never
+    for mode in (1, 2):
+        for lists in (0, 1, 65):
+            olds = _knobs(lib, [(0, mode), (15, lists)])
+            try:
+                outs[(mode, lists)] = render_sum_frame(T(means), T(L), T(colors), T(opac), H, W,
+                                                       _tb(H, W), bg)
+            finally:
+                _restore(lib, olds)
+    ref = outs[(1, 65)]
+    for key, out in outs.items():
+        assert torch.equal(out, ref), key
+
+
+def test_composite_lists_match_oracle_dense(cuda, oracle):
+    """Trained-like density (~35 entries per tile, lists on by default) against
+    the C oracle."""
+    from gsvc_amd.render import render_sum_frame
+    n = 30000
+    means, L, colors, opac = oracle.synthetic_frame(n, seed=5, rgb_w=2.0, chol_scale=3.0)
+    fast = render_sum_frame(T(means), T(L), T(colors), T(opac), H, W, _tb(H, W),
+                            torch.ones(3, device="cuda"))
+    ref = oracle.render_sum(means, L, colors, opac, H, W)["out"]
+    ref = np.clip(ref, 0, 1).reshape(H, W, 3).transpose(2, 0, 1)[None]
+    np.testing.assert_allclose(fast.cpu().numpy(), ref, rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("chol", [1.0, 4.0])
+def test_train_forward_lists_bit_identical(cuda, chol):
+    """The fused step's render with the band kernel's lists (default) and
+    without (knob 14 = 1) is the same image; the gradients agree to the float
+    atomics' summation order."""
+    from gsvc_amd import _lib
+    from gsvc_amd.frame import make_frame_model, synthetic_gt
+    lib = _lib.load()
+    gt = synthetic_gt(256, 384, 3, cuda)
+    res = []
+    for knob in (0, 1):
+        model = make_frame_model(256, 384, 6000, cuda, seed=21)
+        with torch.no_grad():
+            model._cholesky.mul_(chol)
+        olds = _knobs(lib, [(14, knob)])
+        try:
+            render = torch.empty(3, 256, 384, device=cuda)
+            g = torch.empty(6000, 9, device=cuda)
+            from gsvc_amd.train import train_step_sum
+            losses = train_step_sum(model._xyz.data, model._cholesky.data, model._features_dc.data,
+                                    model.rgb_W.data, False, model.cholesky_bound, model.background,
+                                    gt.reshape(3, 256, 384).contiguous(), 256, 384, "L2", render_out=render, grads_out=g)
+            torch.cuda.synchronize()
+            res.append((render.clone(), g.clone(), losses.cpu().clone()))
+        finally:
+            _restore(lib, olds)
+    assert torch.equal(res[0][0], res[1][0])
+    torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(res[0][2], res[1][2], rtol=0, atol=0)
