@@ -20,7 +20,7 @@ rank processes itself (``torch.distributed.run`` as a child process; this
 process never touches the GPU) and exits with their status.
 
 Reported beside the primary value:
-  roofline      the dominant kernel of the step (train_tile_kernel): algorithmic
+  roofline      the dominant kernel of the step (train_tile_band_kernel): algorithmic
                 bytes per launch (12 P + 4 T + 48 M_eff + 32 M_eff +
                 12 T) over its average duration from HIP events carried by its
                 own dispatches (on its stream), vs 8 TB/s; ``traffic`` = PMC HBM
@@ -157,7 +157,7 @@ def composite_bytes(shape):
 
 
 def train_tile_bytes(shape):
-    """Algorithmic HBM bytes of one train_tile_kernel launch:
+    """Algorithmic HBM bytes of one train_tile_band_kernel launch:
     gt 12 P + tile counts 4 T + the tiles' splat records 48 M_eff (read);
     gradient sums 32 M_eff (8 floats per (splat, tile), atomics) + per-tile
     error sums 8 T + the next frame's count reset 4 T (written)."""
@@ -438,7 +438,7 @@ def main():
         return
 
     prof = load_profile(f"train_{args.splats}")
-    roof = roofline("train_tile_kernel", train_tile_bytes(shape), kt["train_tile"], prof,
+    roof = roofline("train_tile_band_kernel", train_tile_bytes(shape), kt["train_tile"], prof,
                     "train_tile")
     # the tile kernel is VALU/latency bound at trained density:
     # its VALU issue fraction beside the HBM roofline

@@ -129,7 +129,7 @@ def main():
         import numpy as np
         from gsvc_amd import _lib as L
         lib = L.load()
-        st = torch.zeros(((a.splats + 63) // 64, 8), dtype=torch.int64, device=dev)
+        st = torch.zeros(((a.splats + 63) // 64 + 4096, 8), dtype=torch.int64, device=dev)  # waves of any per-workgroup split
         lib.gsvc_debug_set_ptr(ctypes.c_void_p(st.data_ptr()))
         lib.gsvc_debug_set(5, 1)
         model.train_iter(gt, a.warmup + a.iters + 300)
