@@ -14,10 +14,11 @@
 // Forward: one wave64 per tile, 4 pixels per lane (as the sum forward), the
 // wave leaves the tile when every lane's 4 pixels are done.
 // Backward: the transmittance recursion runs per pixel from the back, so it
-// is PIXEL-parallel: 256 threads = 256 pixels; per entry each wave reduces
-// its 9 partial gradients with shuffles, adds them to an LDS record with LDS
-// float atomics (4 waves), and once per 256-entry chunk the tile's records go
-// to HBM as one 64-byte atomic request per (splat, tile).
+// is PIXEL-parallel: 256 threads = 256 pixels; per entry each wave sums its 9
+// partial gradients per 16-lane row with DPP adds (4 VALU each, no LDS
+// permutes), the rows' last lanes add them to an LDS record with LDS float
+// atomics (16 rows), and once per 256-entry chunk the tile's records go to HBM
+// as one 64-byte atomic request per (splat, tile).
 #include "common.h"
 
 namespace gsvc {
@@ -104,12 +105,26 @@ __global__ __launch_bounds__(64) void raster_alpha_fwd_kernel(
     }
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
+// Sum over each 16-lane row, left in every lane of the row: four DPP adds
+// (quad swaps, half-row and row mirrors), no LDS permutes.
+template <int kCtrl>
+__device__ __forceinline__ float dpp_add(float v) {
+    return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), kCtrl, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float row_sum16(float v) {
+    v = dpp_add<0xb1>(v);   // quad_perm [1, 0, 3, 2]
+    v = dpp_add<0x4e>(v);   // quad_perm [2, 3, 0, 1]
+    v = dpp_add<0x141>(v);  // row_half_mirror
+    return dpp_add<0x140>(v);  // row_mirror
+}
+
+__device__ __forceinline__ float wave_sum_shfl(float v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     return v;
 }
 
+template <bool kDpp>
 __global__ __launch_bounds__(256) void raster_alpha_bwd_kernel(
     int tbx, int img_w, int img_h, int ntiles, const int *__restrict__ ids,
     const int2 *__restrict__ bins, const float2 *__restrict__ xys, const float *__restrict__ conics,
@@ -210,25 +225,26 @@ __global__ __launch_bounds__(256) void raster_alpha_bwd_kernel(
                 g_y = v_sigma * fmaf(G.w, dx, C.x * dy);
                 g_o = vis * v_alpha;
             }
-            g_x = wave_sum(g_x);
-            g_y = wave_sum(g_y);
-            g_c0 = wave_sum(g_c0);
-            g_c1 = wave_sum(g_c1);
-            g_c2 = wave_sum(g_c2);
-            g_r = wave_sum(g_r);
-            g_g = wave_sum(g_g);
-            g_b = wave_sum(g_b);
-            g_o = wave_sum(g_o);
-            if (lane == 0) {
-                atomicAdd(&s_acc[t][0], g_x);
-                atomicAdd(&s_acc[t][1], g_y);
-                atomicAdd(&s_acc[t][2], g_c0);
-                atomicAdd(&s_acc[t][3], g_c1);
-                atomicAdd(&s_acc[t][4], g_c2);
-                atomicAdd(&s_acc[t][5], g_r);
-                atomicAdd(&s_acc[t][6], g_g);
-                atomicAdd(&s_acc[t][7], g_b);
-                atomicAdd(&s_acc[t][8], g_o);
+            // the entry's sums over the wave: per 16-lane row by DPP, then the
+            // last lane of each row adds its row's sums into the entry's LDS
+            // accumulator (the row order of these adds is not fixed: float
+            // atomics, as the reference's warp sums + atomicAdd)
+            if (kDpp) {
+                const float gs[9] = {row_sum16(g_x), row_sum16(g_y), row_sum16(g_c0),
+                                     row_sum16(g_c1), row_sum16(g_c2), row_sum16(g_r),
+                                     row_sum16(g_g), row_sum16(g_b), row_sum16(g_o)};
+                if ((lane & 15) == 15) {
+#pragma unroll
+                    for (int c = 0; c < 9; ++c) atomicAdd(&s_acc[t][c], gs[c]);
+                }
+            } else {  // A/B (knob 9 = 1): butterfly shuffles over the wave
+                const float gs[9] = {wave_sum_shfl(g_x), wave_sum_shfl(g_y), wave_sum_shfl(g_c0),
+                                     wave_sum_shfl(g_c1), wave_sum_shfl(g_c2), wave_sum_shfl(g_r),
+                                     wave_sum_shfl(g_g), wave_sum_shfl(g_b), wave_sum_shfl(g_o)};
+                if (lane == 0) {
+#pragma unroll
+                    for (int c = 0; c < 9; ++c) atomicAdd(&s_acc[t][c], gs[c]);
+                }
             }
         }
         __syncthreads();
@@ -283,7 +299,8 @@ extern "C" int gsvc_rasterize_backward(unsigned img_height, unsigned img_width, 
     const int tbx = ceil_div((int)img_width, kTile), tby = ceil_div((int)img_height, kTile);
     const int ntiles = tbx * tby;
     if (ntiles == 0 || num_points == 0) return GSVC_OK;
-    hipLaunchKernelGGL(raster_alpha_bwd_kernel, dim3(ntiles), dim3(256), 0, s, tbx, (int)img_width,
+    hipLaunchKernelGGL(g_knobs[9] == 1 ? raster_alpha_bwd_kernel<false> : raster_alpha_bwd_kernel<true>,
+                       dim3(ntiles), dim3(256), 0, s, tbx, (int)img_width,
                        (int)img_height, ntiles, gaussian_ids_sorted, (const int2 *)tile_bins,
                        (const float2 *)xys, conics, colors, opacities, background, final_Ts,
                        final_idx, v_output, v_output_alpha, grad_records);

@@ -53,13 +53,21 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--splats", type=int, nargs="+", default=[10000, 50000])
     ap.add_argument("--calls", type=int, default=200)
+    ap.add_argument("--knob", action="append", default=[],
+                    help="K=V: gsvc_debug_set(K, V) first (A/B; knob 9 = 1: shuffle reductions)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
+    if a.knob:
+        from gsvc_amd import _lib as L
+        lib = L.load()
+        for kv in a.knob:
+            k, v = kv.split("=")
+            lib.gsvc_debug_set(int(k), int(v))
     for n in a.splats:
         fwd = run(n, a.calls, dev, False)
         both = run(n, a.calls, dev, True)
         print(json.dumps(dict(path="rasterize_gaussians (alpha)", H=H, W=W, splats=n,
-                              us_forward=round(fwd, 1), us_forward_backward=round(both, 1))),
+                              us_forward=round(fwd, 1), us_forward_backward=round(both, 1), knobs=a.knob)),
               flush=True)
 
 
