@@ -431,6 +431,27 @@ def main():
     kt = time_channels(["train_tile", "project", "train_splat"], one_iter, args.timing_launches)
     shape = frame_shape(model.get_xyz.detach(), model.get_cholesky_elements.detach(),
                         model.tile_bounds)
+    # N > 1: the render half of the metric, weak-scaled like the headline (each
+    # rank renders its own trained frame; barrier-bracketed, max over ranks)
+    render_ranks = None
+    if world > 1 and not args.no_secondary:
+        model.eval()
+        with torch.no_grad():
+            for _ in range(20):
+                model()
+            barrier(world)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(200):
+                model()
+            torch.cuda.synchronize()
+            rel = time.perf_counter() - t1
+        barrier(world)
+        rel = all_max(rel, world, device)
+        render_ranks = {"workload": "GaussianVideoFrame.forward of each rank's trained 1920x1080 "
+                                    f"frame, {args.splats} splats, 200 frames per rank",
+                        "frames_per_s": round(world * 200 / rel, 1),
+                        "ms_per_frame": round(1e3 * rel / 200, 4), "n_gpus": world}
     if rank != 0:
         if world > 1:
             import torch.distributed as dist
@@ -472,6 +493,8 @@ def main():
         "train_iter_path": ("fused: gsvc_train_step_sum" if model.fused_steps else "op by op"),
         "cpu_baseline": None,
     }
+    if render_ranks is not None:
+        line["render"] = render_ranks
     if world == 1 and not args.no_secondary:
         line["psnr_vs_ref"] = psnr_vs_ref(device)
         model.eval()
