@@ -349,7 +349,22 @@ def parse_args(argv=None):
                     help="auto (K_frames.txt, else detect), forced (shard boundaries only), "
                          "or a comma list")
     ap.add_argument("--root", type=str, default="./checkpoints")
+    ap.add_argument("--ranks_per_gpu", type=int, default=1,
+                    help="ranks sharing one GPU (each trains its own GOPs on its own stream; "
+                         "> 1 uses gloo for the metric collectives, RCCL takes one rank per GPU)")
     return ap.parse_args(argv)
+
+
+def rank_device(local: int, ranks_per_gpu: int, use_cuda: bool):
+    """(device, backend) of a rank: GPU local // ranks_per_gpu.  Frames and
+    GOPs are independent, and one frame's training step is a latency chain
+    that leaves most of the GPU idle, so several ranks per GPU overlap their
+    steps; their only collectives are the metric aggregate and the K-frame
+    detector's gathers, so gloo (host) serves them when ranks share a GPU."""
+    rpg = max(1, int(ranks_per_gpu))
+    if not use_cuda:
+        return torch.device("cpu"), "gloo"
+    return torch.device("cuda", local // rpg), ("nccl" if rpg == 1 else "gloo")
 
 
 def main(argv=None):
@@ -358,13 +373,12 @@ def main(argv=None):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_cuda = torch.cuda.is_available()
-    device = torch.device("cuda", local) if use_cuda else torch.device("cpu")
+    device, args.backend = rank_device(local, args.ranks_per_gpu, use_cuda)
     if use_cuda:
         torch.cuda.set_device(device)
-    args.backend = "nccl" if use_cuda else "gloo"
     if world > 1:
         import torch.distributed as dist
-        if use_cuda:
+        if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group("gloo")

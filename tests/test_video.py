@@ -245,3 +245,14 @@ def test_video_driver_reports_ms_ssim(cuda, tmp_path):
     ms = [r["ms_ssim"] for r in res["frames"]]
     assert all(np.isfinite(ms)) and all(0.0 < m <= 1.0 for m in ms)
     assert res["average"]["ms_ssim"] == pytest.approx(float(np.mean(ms)), rel=1e-6)
+
+
+def test_rank_device_mapping():
+    """--ranks_per_gpu: GPU local // R, gloo when ranks share a GPU (RCCL takes
+    one rank per device), nccl otherwise; CPU runs stay on gloo."""
+    import torch
+    from gsvc_amd.video import rank_device
+    assert rank_device(3, 1, True) == (torch.device("cuda", 3), "nccl")
+    assert rank_device(3, 2, True) == (torch.device("cuda", 1), "gloo")
+    assert rank_device(7, 4, True) == (torch.device("cuda", 1), "gloo")
+    assert rank_device(5, 2, False) == (torch.device("cpu"), "gloo")
