@@ -99,6 +99,8 @@ def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("GSVC_BENCH_SHARED_GPU") == "1" and args.backend != "nccl":
+        local = 0  # rehearsal of N ranks on a one-GPU box (gloo): all ranks on cuda:0
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1:
