@@ -21,7 +21,10 @@ detect_outliers_mean_diff :214-229) that runs on the MI355X path:
   the GPU), early stopping as the reference, then PSNR and the eval FPS of
   100 renders (synchronised);
 * the per-frame metrics meet in ONE all_reduce (RCCL over xGMI with the
-  "nccl" backend; gloo on CPU), the only collective of the path.
+  "nccl" backend; gloo on CPU), the only collective of the path (SURVEY §8e);
+* ``--ranks_per_gpu R`` puts R ranks (R GOP shards) on each GPU: one frame's
+  step leaves part of the chip idle, so two concurrent shards train ~1.35x as
+  many iterations per second; their collectives go over gloo.
 
     python -m gsvc_amd.video --synthetic 24 --width 256 --height 256 --num_points 2000 \\
         --iterations 300 --loss_type L2
