@@ -256,3 +256,42 @@ def test_rank_device_mapping():
     assert rank_device(3, 2, True) == (torch.device("cuda", 1), "gloo")
     assert rank_device(7, 4, True) == (torch.device("cuda", 1), "gloo")
     assert rank_device(5, 2, False) == (torch.device("cpu"), "gloo")
+
+
+@pytest.mark.gpu
+def test_video_driver_two_ranks_share_one_gpu(cuda, tmp_path):
+    """--ranks_per_gpu 2 under torchrun on one GPU: two GOP shards train
+    concurrently on cuda:0 over gloo collectives; every frame is trained once,
+    rank 0 gathers one checkpoint, and the per-frame PSNRs agree with the
+    one-rank run of the same video (same seeds per frame; float atomics only)."""
+    import os
+    import subprocess
+    import sys
+    args = ["--synthetic", "6", "--height", "64", "--width", "96", "--num_points", "300",
+            "--iterations", "300", "--k_frames", "1,4"]
+    from gsvc_amd import video as V
+    one = V.main(args + ["--root", str(tmp_path / "one")])
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env["PYTHONPATH"] = repo + os.pathsep + env.get("PYTHONPATH", "")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        "29731", "-m", "gsvc_amd.video", *args, "--ranks_per_gpu", "2",
+                        "--root", str(tmp_path / "two")],
+                       cwd=repo, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([s for s in r.stdout.splitlines() if s.startswith("{")][-1])
+    assert line["ranks"] == 2 and line["frames"] == 6
+    out = tmp_path / "two" / "result" / "Synthetic" / "GaussianVideo_300_300"
+    frames = []
+    for rank in (0, 1):
+        frames += [json.loads(s) for s in (out / f"train_rank{rank}.jsonl").read_text().splitlines()]
+    assert sorted(f["frame"] for f in frames) == list(range(1, 7))
+    psnr_two = {f["frame"]: f["psnr"] for f in frames}
+    psnr_one = {f["frame"]: f["psnr"] for f in one["frames"]}
+    for k in psnr_one:
+        assert psnr_two[k] == pytest.approx(psnr_one[k], abs=0.05), k
+    models = torch.load(tmp_path / "two" / "models" / "Synthetic" / "GaussianVideo_300_300" /
+                        "gmodels_state_dict.pth", weights_only=True)
+    assert sorted(models) == [f"frame_{i}" for i in range(1, 7)]
