@@ -316,11 +316,16 @@ def render_block(model, steps, warmup):
     shape = frame_shape(model.get_xyz.detach(), model.get_cholesky_elements.detach(),
                         model.tile_bounds)
     prof = load_profile(f"render_{model._xyz.shape[0]}")
+    roof = roofline("raster_sum_fwd_kernel (composite)", composite_bytes(shape),
+                    times["composite"], prof, "rasterize_sum_forward")
+    vr = valu_roofline(f"render_{model._xyz.shape[0]}",
+                       roof.get("trace_avg_kernel_us") or roof["avg_kernel_us"])
+    if vr:
+        roof["valu"] = vr
     return {"workload": f"GaussianVideoFrame.forward, 1920x1080, {model._xyz.shape[0]} splats "
                         "(configs[2] render): project + bin + sum-raster + clamp + NCHW",
             "frames_per_s": round(steps / el, 1), "ms_per_frame": round(1e3 * el / steps, 4),
-            "roofline": roofline("raster_sum_fwd_kernel (composite)", composite_bytes(shape),
-                                 times["composite"], prof, "rasterize_sum_forward"),
+            "roofline": roof,
             "project_avg_us": round(_avg(times["project"]) * 1e3, 2), "shape": shape}
 
 
