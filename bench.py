@@ -21,17 +21,18 @@ process never touches the GPU) and exits with their status.
 
 Reported beside the primary value:
   roofline      the dominant kernel of the step (train_tile_band_kernel): algorithmic
-                bytes per launch (12 P + 4 T + 48 M_eff + 32 M_eff +
-                12 T) over its average duration from HIP events carried by its
+                bytes per launch (12 P + 36 N_vis + 4 M_eff + 8 T +
+                36 N) over its average duration from HIP events carried by its
                 own dispatches (on its stream), vs 8 TB/s; ``traffic`` = PMC HBM
-                bytes per launch from the committed rocprofv3 passes (profiles/).
+                bytes per launch from the committed rocprofv3 passes (profiles/),
+                ``traffic_model`` = the bytes the slab design moves.
   kernels       every kernel of the step, event-timed the same way.
   render        configs[2]'s render: GaussianVideoFrame.forward at 50k splats,
                 frames/s and the composite kernel's roofline.
   psnr_vs_ref   the fused trajectory against the reference's own train_iter run
                 on CPU (tests/golden/train_traj_1080p_n50k.npz, make_golden.py).
-  cpu_baseline  the CPU restatement (oracle/oracle.py train_iter_sum, C kernels,
-                1 thread) on a bounded sample of the same iteration.
+  cpu_baseline  the CPU restatement (oracle/oracle.py train_iter_sum, C kernels)
+                on the same settled state, k = 1 and all cores, median of 5.
   render_10k    configs[1] (render only, 10k splats) and ``video_decode``.
 """
 from __future__ import annotations
@@ -53,6 +54,7 @@ METRIC = "1920×1080 frames/sec (render + train-iter) @ N splats; PSNR vs ref"
 H, W = 1080, 1920
 HBM_PEAK_GBS = 8000.0
 TRAJ_FIXTURE = os.path.join(REPO, "tests", "golden", "train_traj_1080p_n50k.npz")
+STATE_FIXTURE = os.path.join(REPO, "tests", "golden", "train_state_1080p_n50k.npz")
 
 
 def parse():
@@ -64,7 +66,6 @@ def parse():
     ap.add_argument("--settle", type=int, default=2000,
                     help="training iterations before the warmup (untimed): the timed steps "
                          "run at a trained splat density, not at random init")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--timing-launches", type=int, default=200,
                     help="launches per kernel timed by HIP events after the timed region")
     ap.add_argument("--no-secondary", action="store_true")
@@ -158,11 +159,21 @@ def composite_bytes(shape):
     return 36 * shape["N_vis"] + 4 * shape["M_eff"] + 8 * shape["T"] + 12 * shape["P"]
 
 
-def train_tile_bytes(shape):
-    """Algorithmic HBM bytes of one train_tile_band_kernel launch:
-    gt 12 P + tile counts 4 T + the tiles' splat records 48 M_eff (read);
-    gradient sums 32 M_eff (8 floats per (splat, tile), atomics) + per-tile
-    error sums 8 T + the next frame's count reset 4 T (written)."""
+def train_tile_bytes(shape, n):
+    """Algorithmic HBM bytes of one fused training tile pass (forward + loss +
+    backward over every tile): the target frame 12 P, the
+    visible splats' geometry and colour 36 N_vis, the tile id lists 4 M_eff and
+    bins 8 T (read); the gradients 36 N (9 floats per splat, written).  The
+    image, final_idx and v_out never leave the chip."""
+    return 12 * shape["P"] + 36 * shape["N_vis"] + 4 * shape["M_eff"] + 8 * shape["T"] + 36 * n
+
+
+def train_tile_traffic_model(shape):
+    """What train_tile_band_kernel's design moves per launch:
+    gt 12 P + tile counts 4 T + the tiles' 48-byte slab records 48 M_eff (read);
+    gradient sums by atomics 32 M_eff (8 floats per (splat, tile)) + per-tile
+    error sums 8 T + the next frame's count reset 4 T (written).  Reported next
+    to the PMC traffic; the excess over train_tile_bytes is the slab design's."""
     return 12 * shape["P"] + 4 * shape["T"] + 48 * shape["M_eff"] + 32 * shape["M_eff"] + 12 * shape["T"]
 
 
@@ -233,34 +244,64 @@ def valu_roofline(kernel_key, avg_us):
             "frac": round(achieved / VALU_PEAK_GINST, 4), "source": "profiles/pmc_valu.json"}
 
 
-def cpu_baseline(n_splats, seconds):
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(n_splats, reps=5, warm=2):
     """The CPU restatement of the same training iteration (oracle/oracle.py
     train_iter_sum: project + bin + sum-raster + clamp + L2 + raster and
-    projection VJPs + Adan; C kernels, numpy glue), 1 thread, timed on a
-    bounded number of iterations of the headline frame on this host."""
+    projection VJPs + Adan; C kernels, OpenMP over tiles, numpy glue) on the
+    SETTLED state the GPU is timed on (tests/golden/train_state_1080p_n50k.npz,
+    the bench's frame after settle + warmup iterations), BASELINE.md §4
+    protocol: k = 1 and k = all cores of this process's affinity, median of
+    ``reps`` iterations after ``warm`` warm-ups each (all cores = the affinity
+    mask, capped by OMP_NUM_THREADS: the GPU box grants 16 CPUs per GPU while
+    its affinity mask shows the whole machine)."""
+    import numpy as np
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     from gsvc_amd.frame import synthetic_gt
+    z = np.load(STATE_FIXTURE)
+    if n_splats != int(z["n"]):
+        return None
+    gt = synthetic_gt(H, W, int(z["gt_seed"]), "cpu").numpy()[0]
+    cores = len(os.sched_getaffinity(0))
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():  # the box's CPU share (16 per GPU)
+        cores = min(cores, max(1, int(os.environ["OMP_NUM_THREADS"])))
+    runs = {}
+    for k in sorted({1, cores}):
+        O.set_threads(k)
+        params = {name: np.array(z["state_" + name], copy=True)
+                  for name in ("_xyz", "_cholesky", "_features_dc")}
+        state = {}
+        step = int(z["iters"])
+        ts = []
+        for i in range(warm + reps):
+            step += 1
+            t0 = time.perf_counter()
+            O.train_iter_sum(params, gt, H, W, state, step)
+            ts.append(time.perf_counter() - t0)
+        ts = sorted(ts[warm:])
+        runs[k] = ts[len(ts) // 2]
     O.set_threads(1)
-    g = torch.Generator().manual_seed(1000)
-    params = dict(_xyz=torch.atanh(2 * (torch.rand(n_splats, 2, generator=g) - 0.5)).numpy(),
-                  _cholesky=torch.rand(n_splats, 3, generator=g).numpy(),
-                  _features_dc=torch.rand(n_splats, 3, generator=g).numpy())
-    gt = synthetic_gt(H, W, 8, "cpu").numpy()[0]
-    state = {}
-    O.train_iter_sum(params, gt, H, W, state, 1)  # warm-up (library load, first step)
-    t0 = time.perf_counter()
-    it = 0
-    while True:
-        it += 1
-        O.train_iter_sum(params, gt, H, W, state, 1 + it)
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": it / el, "unit": "train-iters/s", "cores": 1, "kind": "port",
-            "sample": f"{it} train iterations of one 1920x1080 / {n_splats}-splat frame "
-                      "(oracle/oracle.py train_iter_sum: C project/bin/raster + VJPs, numpy "
-                      f"clamp/L2/Adan), 1 thread, {el:.1f} s"}
+    best = min(runs, key=runs.get)
+    return {"value": 1.0 / runs[best], "unit": "train-iters/s", "cores": best, "kind": "port",
+            "cpu_model": _cpu_model(),
+            "per_cores": {str(k): round(1.0 / v, 4) for k, v in runs.items()},
+            "sample": f"median of {reps} train iterations after {warm} warm-ups, per core count, "
+                      f"of one 1920x1080 / {n_splats}-splat frame at the settled state the GPU "
+                      f"times (after {int(z['iters'])} iterations, M = {int(z['M'])}; "
+                      "oracle/oracle.py train_iter_sum: C project/bin/raster + VJPs with OpenMP "
+                      "over tiles, numpy clamp/L2/Adan)"}
 
 
 def psnr_vs_ref(device):
@@ -466,8 +507,11 @@ def main():
         return
 
     prof = load_profile(f"train_{args.splats}")
-    roof = roofline("train_tile_band_kernel", train_tile_bytes(shape), kt["train_tile"], prof,
-                    "train_tile")
+    roof = roofline("train_tile_band_kernel", train_tile_bytes(shape, args.splats), kt["train_tile"],
+                    prof, "train_tile")
+    roof["traffic_model"] = train_tile_traffic_model(shape)
+    if roof.get("traffic"):
+        roof["traffic_over_algorithmic"] = round(roof["traffic"] / roof["algorithmic_bytes_per_launch"], 3)
     # the tile kernel is VALU/latency bound at trained density:
     # its VALU issue fraction beside the HBM roofline
     vr = valu_roofline("train_tile", roof.get("trace_avg_kernel_us") or roof["avg_kernel_us"])
@@ -510,7 +554,7 @@ def main():
         line["render_10k"] = render_10k(device)
         line["video_decode"] = video_decode(device)
     if world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(args.splats, args.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(args.splats)
     print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -790,6 +790,11 @@ extern "C" int gsvc_bin_tiles_counted(int num_points, const float *xys, const in
     const int ntiles = tbx * tby;
     if (num_points < 0 || tbx <= 0 || tby <= 0 || capacity < 0 || tile_cap < 0)
         return set_error(GSVC_ERR_ARG, "bin_tiles_counted: bad sizes");
+    // the overflow rebuild (tile_overflow_kernel -> wave_brute_ids) writes exactly
+    // kTilePix ids per overfull tile, so a cap is either off or the 256 entries
+    // the rasterizers read (forward.cu:569-571,613)
+    if (tile_cap != 0 && tile_cap != kTilePix)
+        return set_error(GSVC_ERR_ARG, "bin_tiles_counted: tile_cap must be 0 or 256");
     if (tile_cap && !gaussian_ids_sorted)
         return set_error(GSVC_ERR_ARG, "bin_tiles_counted: tile_cap needs gaussian_ids_sorted");
     if (workspace_bytes < gsvc_bin_tiles_counted_workspace_bytes(ntiles))

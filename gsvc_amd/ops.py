@@ -289,8 +289,11 @@ def bin_tiles_counted(num_points, xys, radii, tile_bounds, capacity, tile_cap=0)
     """Sync-free tile binning (gsvc_bin_tiles_counted): returns
     (gaussian_ids_sorted [capacity], tile_bins [#tiles, 2], meta [2] = {M,
     overflow}) with M only on the device.  Valid when every emitting splat has
-    the same depth bits (the order is (tile, splat id)).  tile_cap > 0 keeps
-    each tile's first tile_cap entries only."""
+    the same depth bits (the order is (tile, splat id)).  tile_cap = 256 keeps
+    each tile's first 256 entries only (the rasterizers read no more,
+    forward.cu:569-571,613); 0 keeps all.  Other caps raise ValueError."""
+    if int(tile_cap) not in (0, 256):
+        raise ValueError(f"bin_tiles_counted: tile_cap must be 0 or 256, got {tile_cap}")
     xys = _f32(xys, "xys")
     radii = _i32(radii, "radii")
     tb = _tb(tile_bounds)

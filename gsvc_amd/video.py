@@ -86,11 +86,36 @@ def load_yuv_frames(path: str, width: int, height: int, device, frames: Optional
     return out, total
 
 
-def synthetic_video(num_frames: int, height: int, width: int, seed: int = 0, cut_every: int = 0):
+def synthetic_video(num_frames: int, height: int, width: int, seed: int = 0, cut_every: int = 0,
+                    device=None):
     """A seeded smooth moving RGB pattern (sum of drifting sinusoids per
     channel), with a scene cut (new pattern) every ``cut_every`` frames: the
-    stand-in for the UVG sequences.  Returns a function frame(i) -> CPU
-    [1, 3, H, W] in [0, 1] so ranks materialise only their own frames."""
+    stand-in for the UVG sequences.  Returns a function frame(i) -> [1, 3, H, W]
+    in [0, 1] so ranks materialise only their own frames: on the CPU (numpy)
+    by default, or computed on ``device`` with torch (a 1080p frame is ~36 M
+    sines: ~0.3 s on one host core, microseconds on the GPU; the two agree to
+    float32 rounding of sin)."""
+    if device is not None and torch.device(device).type != "cpu":
+        dev = torch.device(device)
+        yy_t, xx_t = torch.meshgrid(torch.linspace(0, 1, height, device=dev),
+                                    torch.linspace(0, 1, width, device=dev), indexing="ij")
+
+        def frame_dev(i: int) -> torch.Tensor:
+            scene = i // cut_every if cut_every else 0
+            rng = np.random.default_rng(seed * 1000003 + scene)
+            par = rng.uniform(0, 1, (3, 6, 5)).astype(np.float32)
+            t = np.float32(i - (scene * cut_every if cut_every else 0))
+            chans = []
+            for c in range(3):
+                acc = torch.zeros((height, width), device=dev)
+                for k in range(6):
+                    fx, fy, ph, vx, vy = (float(v) for v in par[c, k])
+                    acc += torch.sin(12 * fx * xx_t + 12 * fy * yy_t +
+                                     (6.28 * ph + float(0.08 * t * (vx + vy))))
+                chans.append(0.5 + 0.5 * acc / 6)
+            return torch.stack(chans).clamp(0, 1)[None].contiguous()
+
+        return frame_dev
     yy, xx = np.meshgrid(np.linspace(0, 1, height, dtype=np.float32),
                          np.linspace(0, 1, width, dtype=np.float32), indexing="ij")
 
@@ -401,7 +426,8 @@ def main(argv=None):
             return _cache[i]
     else:
         num_frames = args.synthetic or args.image_length
-        gen = synthetic_video(num_frames, args.height, args.width, int(args.seed), args.cut_every)
+        gen = synthetic_video(num_frames, args.height, args.width, int(args.seed), args.cut_every,
+                              device=device)
 
         def frame_fn(i):
             return gen(i).to(device)

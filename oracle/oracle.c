@@ -292,56 +292,103 @@ void oracle_raster_sum_forward(int tbx, int tby, int img_w, int img_h,
     }
 }
 
-/* backward.cu:696-862.  Gradients are accumulated in double (the GPU sums by
- * tree reduction + atomics; tests compare with a relative tolerance). */
+/* backward.cu:696-862 for the tiles [t0, t1).  Gradients are accumulated in
+ * double (the GPU sums by tree reduction + atomics; tests compare with a
+ * relative tolerance). */
+static void raster_sum_backward_tiles(int t0, int t1, int tbx, int img_w, int img_h,
+                                      const int *ids, const int *bins,
+                                      const float *xys, const float *conics,
+                                      const float *colors, const float *opac,
+                                      const int *final_idx, const float *v_out,
+                                      double *v_xy, double *v_conic, double *v_rgb,
+                                      double *v_opac) {
+    for (int tile = t0; tile < t1; ++tile) {
+        int ty = tile / tbx, tx = tile - ty * tbx;
+        int r0 = bins[2 * tile], r1 = bins[2 * tile + 1];
+        for (int ly = 0; ly < TILE; ++ly)
+            for (int lx = 0; lx < TILE; ++lx) {
+                int i = ty * TILE + ly, j = tx * TILE + lx;
+                if (i >= img_h || j >= img_w) continue;
+                size_t p = (size_t)i * (size_t)img_w + (size_t)j;
+                int bin_final = final_idx[p];
+                float vo0 = v_out[3 * p], vo1 = v_out[3 * p + 1], vo2 = v_out[3 * p + 2];
+                float px = (float)j, py = (float)i;
+                for (int k = r1 - 1; k >= r0; --k) {
+                    if (k > bin_final) continue;
+                    int g = ids[k];
+                    float a = conics[3 * g], b = conics[3 * g + 1], c = conics[3 * g + 2];
+                    float dx = xys[2 * g] - px, dy = xys[2 * g + 1] - py;
+                    float s = splat_sigma(a, b, c, dx, dy);
+                    float vis = exp2f(s * NEG_LOG2E);
+                    float o = opac[g];
+                    float alpha = fminf(1.0f, o * vis);
+                    if (s < 0.0f || alpha < 1.0f / 255.0f) continue;
+                    float r = colors[3 * g], gg = colors[3 * g + 1], bb = colors[3 * g + 2];
+                    float v_alpha = fmaf(bb, vo2, fmaf(gg, vo1, r * vo0));
+                    float v_sigma = (-o * vis) * v_alpha;
+                    v_rgb[3 * g]     += (double)(alpha * vo0);
+                    v_rgb[3 * g + 1] += (double)(alpha * vo1);
+                    v_rgb[3 * g + 2] += (double)(alpha * vo2);
+                    float hs = 0.5f * v_sigma;
+                    v_conic[3 * g]     += (double)((hs * dx) * dx);
+                    v_conic[3 * g + 1] += (double)((hs * dx) * dy);
+                    v_conic[3 * g + 2] += (double)((hs * dy) * dy);
+                    v_xy[2 * g]     += (double)(v_sigma * fmaf(a, dx, b * dy));
+                    v_xy[2 * g + 1] += (double)(v_sigma * fmaf(b, dx, c * dy));
+                    v_opac[g] += (double)(vis * v_alpha);
+                }
+            }
+    }
+}
+
+/* The whole backward.  With one thread the tiles run in order into the
+ * outputs; with more, each thread takes a contiguous tile range (static, so
+ * the split depends only on the thread count) into its own double buffers,
+ * which are then added in thread order: results equal the one-thread sums up
+ * to double rounding (invisible after the float32 cast). */
 void oracle_raster_sum_backward(int tbx, int tby, int img_w, int img_h, int n,
                                 const int *ids, const int *bins,
                                 const float *xys, const float *conics,
                                 const float *colors, const float *opac,
                                 const int *final_idx, const float *v_out,
                                 double *v_xy, double *v_conic, double *v_rgb, double *v_opac) {
-    memset(v_xy, 0, sizeof(double) * 2 * (size_t)n);
-    memset(v_conic, 0, sizeof(double) * 3 * (size_t)n);
-    memset(v_rgb, 0, sizeof(double) * 3 * (size_t)n);
-    memset(v_opac, 0, sizeof(double) * (size_t)n);
-    for (int ty = 0; ty < tby; ++ty)
-        for (int tx = 0; tx < tbx; ++tx) {
-            int tile = ty * tbx + tx;
-            int r0 = bins[2 * tile], r1 = bins[2 * tile + 1];
-            for (int ly = 0; ly < TILE; ++ly)
-                for (int lx = 0; lx < TILE; ++lx) {
-                    int i = ty * TILE + ly, j = tx * TILE + lx;
-                    if (i >= img_h || j >= img_w) continue;
-                    size_t p = (size_t)i * (size_t)img_w + (size_t)j;
-                    int bin_final = final_idx[p];
-                    float vo0 = v_out[3 * p], vo1 = v_out[3 * p + 1], vo2 = v_out[3 * p + 2];
-                    float px = (float)j, py = (float)i;
-                    for (int k = r1 - 1; k >= r0; --k) {
-                        if (k > bin_final) continue;
-                        int g = ids[k];
-                        float a = conics[3 * g], b = conics[3 * g + 1], c = conics[3 * g + 2];
-                        float dx = xys[2 * g] - px, dy = xys[2 * g + 1] - py;
-                        float s = splat_sigma(a, b, c, dx, dy);
-                        float vis = exp2f(s * NEG_LOG2E);
-                        float o = opac[g];
-                        float alpha = fminf(1.0f, o * vis);
-                        if (s < 0.0f || alpha < 1.0f / 255.0f) continue;
-                        float r = colors[3 * g], gg = colors[3 * g + 1], bb = colors[3 * g + 2];
-                        float v_alpha = fmaf(bb, vo2, fmaf(gg, vo1, r * vo0));
-                        float v_sigma = (-o * vis) * v_alpha;
-                        v_rgb[3 * g]     += (double)(alpha * vo0);
-                        v_rgb[3 * g + 1] += (double)(alpha * vo1);
-                        v_rgb[3 * g + 2] += (double)(alpha * vo2);
-                        float hs = 0.5f * v_sigma;
-                        v_conic[3 * g]     += (double)((hs * dx) * dx);
-                        v_conic[3 * g + 1] += (double)((hs * dx) * dy);
-                        v_conic[3 * g + 2] += (double)((hs * dy) * dy);
-                        v_xy[2 * g]     += (double)(v_sigma * fmaf(a, dx, b * dy));
-                        v_xy[2 * g + 1] += (double)(v_sigma * fmaf(b, dx, c * dy));
-                        v_opac[g] += (double)(vis * v_alpha);
-                    }
-                }
-        }
+    size_t nn = (size_t)n;
+    memset(v_xy, 0, sizeof(double) * 2 * nn);
+    memset(v_conic, 0, sizeof(double) * 3 * nn);
+    memset(v_rgb, 0, sizeof(double) * 3 * nn);
+    memset(v_opac, 0, sizeof(double) * nn);
+    int tiles = tbx * tby;
+    int nt = 1;
+#ifdef _OPENMP
+    nt = omp_get_max_threads();
+#endif
+    double *buf = NULL;
+    if (nt > 1 && tiles >= 2 * nt)
+        buf = (double *)calloc((size_t)nt * 9 * nn, sizeof(double));
+    if (!buf) {
+        raster_sum_backward_tiles(0, tiles, tbx, img_w, img_h, ids, bins, xys, conics, colors,
+                                  opac, final_idx, v_out, v_xy, v_conic, v_rgb, v_opac);
+        return;
+    }
+#pragma omp parallel num_threads(nt)
+    {
+        int t = 0;
+#ifdef _OPENMP
+        t = omp_get_thread_num();
+#endif
+        double *b = buf + (size_t)t * 9 * nn;
+        int t0 = (int)((long long)tiles * t / nt), t1 = (int)((long long)tiles * (t + 1) / nt);
+        raster_sum_backward_tiles(t0, t1, tbx, img_w, img_h, ids, bins, xys, conics, colors, opac,
+                                  final_idx, v_out, b, b + 2 * nn, b + 5 * nn, b + 8 * nn);
+    }
+    for (int t = 0; t < nt; ++t) {
+        const double *b = buf + (size_t)t * 9 * nn;
+        for (size_t i = 0; i < 2 * nn; ++i) v_xy[i] += b[i];
+        for (size_t i = 0; i < 3 * nn; ++i) v_conic[i] += b[2 * nn + i];
+        for (size_t i = 0; i < 3 * nn; ++i) v_rgb[i] += b[5 * nn + i];
+        for (size_t i = 0; i < nn; ++i) v_opac[i] += b[8 * nn + i];
+    }
+    free(buf);
 }
 
 /* forward.cu:252-374: front-to-back alpha compositing over ALL entries of the

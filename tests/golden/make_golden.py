@@ -419,6 +419,75 @@ def make_train_trajectory_case(name, H, W, n, seed, gt_seed, iters, keep=4096):
     print(f"{name}: {iters} iters in {time.time() - t0:.1f} s, psnrs={[round(p, 4) for p in psnrs]}")
 
 
+TRAINED_CROPS = ((0, 0), (512, 960), (1064, 1904), (300, 1500), (777, 123))
+
+
+def make_trained_state_case(state_path, name="train_state_1080p_n50k", steps=3, keep=4096):
+    """BASELINE configs[2] at the state bench.py times: the bench's 1080p / 50k
+    frame after its settle + warmup iterations (trained density, M ~ 240k),
+    dumped from the GPU by tools/dump_trained.py and loaded here into the
+    reference model.  Records, from the reference's own Python with the oracle
+    injected (GaussianSplats_Represent.py:83-90,191-207, fresh Adan):
+
+    * the forward's image checksums and five 16x16-aligned crops, M, and the
+      L2 loss / PSNR;
+    * the parameter gradients of that loss (the part of train_iter before Adan);
+    * ``steps`` train_iter steps: loss and PSNR per step, the first ``keep``
+      splats' parameters after the last step, float64 sums of all of them."""
+    import time
+    sys.path.insert(0, REF)
+    import GaussianSplats_Represent as GR
+    st = np.load(state_path)
+    n = int(st["_xyz"].shape[0])
+    H, W = 1080, 1920
+    torch.manual_seed(0)
+    model = GR.GaussianVideo_frame(
+        loss_type="L2", opt_type="adan", num_points=n, max_num_points=n, densification_interval=100,
+        iterations=30000, H=H, W=W, BLOCK_H=16, BLOCK_W=16, device=torch.device("cpu"), lr=1e-3,
+        quantize=False, removal_rate=0.1, isdensity=False, isremoval=False)
+    with torch.no_grad():
+        for k in ("_xyz", "_cholesky", "_features_dc"):
+            getattr(model, k).copy_(torch.from_numpy(st[k]))
+        assert np.all(st["rgb_W"] == 1.0)
+    gt_seed = int(st["gt_seed"])
+    gt = synthetic_gt_np(H, W, gt_seed)
+    t0 = time.time()
+    img = model.forward()["render"]
+    loss0 = GR.loss_fn(img.squeeze(0), gt.squeeze(0), "L2", lambda_value=0)
+    loss0.backward()
+    grads = {k: _np(p.grad).copy() for k, p in model.named_parameters() if p.grad is not None}
+    model.optimizer.zero_grad(set_to_none=True)
+    im = _np(img)[0].astype(np.float64)
+    from gsplat.utils import compute_cumulative_intersects
+    with torch.no_grad():
+        _, _, _, _, nth = GR.project_gaussians_2d(model.get_xyz, model.get_cholesky_elements, H, W,
+                                                  model.tile_bounds)
+        M, _ = compute_cumulative_intersects(nth)
+    rec = dict(H=H, W=W, n=n, gt_seed=gt_seed, iters=int(st["iters"]), seed=int(st["seed"]),
+               M=np.int64(M), loss0=np.float64(loss0.item()),
+               render_sum=im.sum(axis=(1, 2)), render_sq=(im ** 2).sum(axis=(1, 2)),
+               crops=np.array(TRAINED_CROPS, np.int32),
+               render_crops=np.stack([_np(img)[0][:, y:y + 16, x:x + 16] for y, x in TRAINED_CROPS]),
+               gt_sum=np.float64(gt.double().sum()))
+    for k in ("_xyz", "_cholesky", "_features_dc"):
+        rec["state_" + k] = st[k]
+        rec["grad_" + k] = grads[k]
+    losses, psnrs = [], []
+    for it in range(int(st["iters"]) + 1, int(st["iters"]) + 1 + steps):
+        loss, psnr = model.train_iter(gt, it)
+        losses.append(float(loss.item()))
+        psnrs.append(float(psnr))
+    rec["losses"] = np.array(losses)
+    rec["psnrs"] = np.array(psnrs)
+    for k in ("_xyz", "_cholesky", "_features_dc"):
+        a = _np(getattr(model, k))
+        rec["final_" + k] = a[:keep].copy()
+        rec["sum_" + k] = np.float64(a.astype(np.float64).sum())
+        rec["abssum_" + k] = np.float64(np.abs(a.astype(np.float64)).sum())
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **rec)
+    print(f"{name}: N={n} M={M} loss0={float(loss0):.6g} psnrs={psnrs} ({time.time() - t0:.1f} s)")
+
+
 def make_prune_cases():
     """removal_control / adaptive_control (GaussianSplats_Represent.py:98-172)
     of the reference model on CPU, torch.sort made stable (the GPU's radix
@@ -475,6 +544,10 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "alpha":
         gs = _import_reference()
         make_alpha_dense_cases(gs)
+        return
+    if len(sys.argv) > 2 and sys.argv[1] == "trained":
+        _import_reference()
+        make_trained_state_case(sys.argv[2])
         return
     if len(sys.argv) > 1 and sys.argv[1] == "trajectory":
         _import_reference()

@@ -51,6 +51,21 @@ def test_argument_errors_are_reported_without_launch():
     assert b"16x16" in lib.gsvc_last_error()
 
 
+def test_bin_tiles_counted_rejects_partial_caps():
+    """The overflow rebuild writes 256 ids per overfull tile, so the only caps
+    are 0 (keep all) and 256 (what the rasterizers read); anything else is an
+    argument error before any HIP call (C ABI) or a ValueError (ops)."""
+    from gsvc_amd import _lib, ops
+    lib = _lib.load()
+    for cap in (1, 100, 255, 257, 1024):
+        rc = lib.gsvc_bin_tiles_counted(10, None, None, 2, 2, 1024, cap, None, None, None, None,
+                                        None, 0, None)
+        assert rc == 1 and b"tile_cap" in lib.gsvc_last_error(), cap
+        with pytest.raises(ValueError, match="tile_cap"):
+            ops.bin_tiles_counted(10, torch.zeros(10, 2), torch.zeros(10, dtype=torch.int32),
+                                  (2, 2, 1), 1024, cap)
+
+
 def test_prune_and_timing_argument_errors():
     """gsvc_prune_lowest / gsvc_timing_enable check their arguments before any
     HIP call; a prune that keeps nothing launches nothing."""
