@@ -270,6 +270,8 @@ def cpu_baseline(n_splats, reps=5, warm=2):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     from gsvc_amd.frame import synthetic_gt
+    if not os.path.exists(STATE_FIXTURE):
+        return None
     z = np.load(STATE_FIXTURE)
     if n_splats != int(z["n"]):
         return None

@@ -65,6 +65,10 @@ _SIGS = {
     "gsvc_render_frame_sum_ex": [_I, _P, _I, _P, _P, _P, _P, _P, _P, _U, _U, _I, _I, _P, _P, _SZ,
                                  _P, _P, _I],
     "gsvc_train_step_workspace_bytes": [_I, _U, _U],
+    "gsvc_train_step_det_workspace_bytes": [_I, ctypes.c_longlong],
+    "gsvc_rasterize_sum_backward_det_workspace_bytes": [_I, ctypes.c_longlong],
+    "gsvc_rasterize_sum_backward_det": [_U, _U, _U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                        _P, _P, _SZ, ctypes.c_longlong, _P, _P],
     "gsvc_train_step_sum_args": [_P],
     "gsvc_train_step_sum": [_I, _P, _P, _P, _P, _P, _I, _P, _P, _U, _U, _I, _I, _P, _P, _I, _P, _P,
                             _P, _P, _SZ, _P],
@@ -99,6 +103,8 @@ _RESTYPE = {
     "gsvc_render_frame_workspace_bytes": _SZ,
     "gsvc_render_frame_zeroed_bytes": _SZ,
     "gsvc_train_step_workspace_bytes": _SZ,
+    "gsvc_train_step_det_workspace_bytes": _SZ,
+    "gsvc_rasterize_sum_backward_det_workspace_bytes": _SZ,
     "gsvc_render_frames_workspace_bytes": _SZ,
     "gsvc_render_frames_zeroed_bytes": _SZ,
     "gsvc_ssim_workspace_bytes": _SZ,

@@ -38,6 +38,7 @@
 // request per entry instead of the reference's 9 per warp).
 #include <hip/hip_ext.h>
 
+#include "det.h"
 #include "frame.h"
 #include "raster_sum.h"
 #include "tile_ids.h"
@@ -710,12 +711,16 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
 
 __device__ __forceinline__ int ceil_log2(int n) { return n <= 1 ? 0 : 32 - __clz(n - 1); }
 
+// det_off (deterministic backward, det.h): each (splat, tile) sum goes to
+// det_part[9 * slot ...] instead of the record's atomics (slots past det_cap:
+// atomics); det_radii: the splats' radii for the slot's bbox.
 __global__ __launch_bounds__(256) void raster_sum_bwd_kernel(
     int tbx, int img_w, int img_h, int ntiles, const int *__restrict__ ids,
     const int2 *__restrict__ bins, const float2 *__restrict__ xys, const float *__restrict__ conics,
     const float *__restrict__ colors, const float *__restrict__ opac,
     const int *__restrict__ final_idx, const float *__restrict__ v_out,
-    float *__restrict__ grad) {
+    float *__restrict__ grad, const int *__restrict__ det_off, const int *__restrict__ det_radii,
+    float *__restrict__ det_part, long long det_cap) {
     __shared__ float4 s_pix[kTilePix];  // v_out rgb, final_idx bits
     __shared__ float4 s_geo[kTilePix];  // x, y, a, b
     __shared__ float4 s_col[kTilePix];  // c, opacity, r, g
@@ -833,10 +838,39 @@ __global__ __launch_bounds__(256) void raster_sum_bwd_kernel(
         // 64-byte gradient record: one memory request per (splat, tile).
         for (int q = tid; q < n * 16; q += kTilePix) {
             const int e2 = q >> 4, c = q & 15;
-            if (c < 9) unsafeAtomicAdd(grad + (size_t)s_gid[e2] * 16 + c, s_red[c][e2]);
+            if (c >= 9) continue;
+            if (det_off) {
+                const int tby = (img_h + kTile - 1) / kTile;
+                const long long slot = det_slot(det_off, xys, det_radii, s_gid[e2], tx, ty, tbx, tby);
+                if (slot < det_cap) {
+                    det_part[9 * slot + c] = s_red[c][e2];
+                    continue;
+                }
+            }
+            unsafeAtomicAdd(grad + (size_t)s_gid[e2] * 16 + c, s_red[c][e2]);
         }
         __syncthreads();
     }
+}
+
+// Deterministic backward: splat i's record = its slots summed in bbox order +
+// the atomics of slots past det_cap (zero unless the capacity was short).
+__global__ __launch_bounds__(256) void det_gather_kernel(int n, const int *__restrict__ off,
+                                                         const float *__restrict__ part,
+                                                         long long cap, float *__restrict__ grad) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const long long b = off[i], e = min((long long)off[i + 1], cap);
+    float s[9];
+#pragma unroll
+    for (int c = 0; c < 9; ++c) s[c] = 0.0f;
+    for (long long k = b; k < e; ++k) {
+#pragma unroll
+        for (int c = 0; c < 9; ++c) s[c] += part[9 * k + c];
+    }
+    float *g = grad + 16 * (size_t)i;
+#pragma unroll
+    for (int c = 0; c < 9; ++c) g[c] = s[c] + g[c];
 }
 
 static int check_tiles(const char *what, int bx, int by, int tbx, int tby, unsigned w, unsigned h) {
@@ -1005,6 +1039,53 @@ extern "C" int gsvc_rasterize_sum_backward(unsigned img_height, unsigned img_wid
     hipLaunchKernelGGL(raster_sum_bwd_kernel, dim3(ntiles), dim3(256), 0, s, tbx, (int)img_width,
                        (int)img_height, ntiles, gaussian_ids_sorted, (const int2 *)tile_bins,
                        (const float2 *)xys, conics, colors, opacities, final_idx, v_output,
-                       grad_records);
+                       grad_records, nullptr, nullptr, nullptr, 0ll);
     return check_launch("rasterize_sum_backward");
+}
+
+extern "C" size_t gsvc_rasterize_sum_backward_det_workspace_bytes(int num_points,
+                                                                  long long det_capacity) {
+    const size_t nn = (size_t)(num_points > 0 ? num_points : 0);
+    const size_t cap = (size_t)(det_capacity > 0 ? det_capacity : 0);
+    return 256 * ((sizeof(int) * (nn + 1) + 255) / 256) + sizeof(float) * 9 * cap;
+}
+
+extern "C" int gsvc_rasterize_sum_backward_det(
+    unsigned img_height, unsigned img_width, unsigned block_h, unsigned block_w, int num_points,
+    const int *gaussian_ids_sorted, const int *tile_bins, const float *xys, const float *conics,
+    const float *colors, const float *opacities, const int *radii, const int *final_idx,
+    const float *v_output, float *grad_records, void *det_workspace, size_t det_workspace_bytes,
+    long long det_capacity, int *pairs_out, void *stream) {
+    const int tbx = ceil_div((int)img_width, (int)block_w), tby = ceil_div((int)img_height, (int)block_h);
+    int rc = check_tiles("rasterize_sum_backward_det", (int)block_w, (int)block_h, tbx, tby,
+                         img_width, img_height);
+    if (rc) return rc;
+    if (num_points < 0 || det_capacity < 0)
+        return set_error(GSVC_ERR_ARG, "rasterize_sum_backward_det: bad sizes");
+    if (!radii || !det_workspace ||
+        det_workspace_bytes < gsvc_rasterize_sum_backward_det_workspace_bytes(num_points, det_capacity))
+        return set_error(GSVC_ERR_WORKSPACE, "rasterize_sum_backward_det: missing radii or workspace");
+    hipStream_t s = (hipStream_t)stream;
+    if (num_points > 0 &&
+        hipMemsetAsync(grad_records, 0, sizeof(float) * 16 * (size_t)num_points, s) != hipSuccess)
+        return set_error(GSVC_ERR_HIP, "rasterize_sum_backward_det: memset failed");
+    const int ntiles = tbx * tby;
+    if (ntiles == 0 || num_points == 0) return GSVC_OK;
+    int *off = (int *)det_workspace;
+    float *part = (float *)((char *)det_workspace + 256 * ((sizeof(int) * ((size_t)num_points + 1) + 255) / 256));
+    hipLaunchKernelGGL(det_offsets_kernel, dim3(1), dim3(kDetScanThreads), 0, s, num_points,
+                       (const float2 *)xys, radii, tbx, tby, off);
+    if (det_capacity > 0 &&
+        hipMemsetAsync(part, 0, sizeof(float) * 9 * (size_t)det_capacity, s) != hipSuccess)
+        return set_error(GSVC_ERR_HIP, "rasterize_sum_backward_det: memset failed");
+    hipLaunchKernelGGL(raster_sum_bwd_kernel, dim3(ntiles), dim3(256), 0, s, tbx, (int)img_width,
+                       (int)img_height, ntiles, gaussian_ids_sorted, (const int2 *)tile_bins,
+                       (const float2 *)xys, conics, colors, opacities, final_idx, v_output,
+                       grad_records, off, radii, part, det_capacity);
+    hipLaunchKernelGGL(det_gather_kernel, dim3(ceil_div(num_points, 256)), dim3(256), 0, s,
+                       num_points, off, part, det_capacity, grad_records);
+    if (pairs_out &&
+        hipMemcpyAsync(pairs_out, off + num_points, sizeof(int), hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return set_error(GSVC_ERR_HIP, "rasterize_sum_backward_det: copy failed");
+    return check_launch("rasterize_sum_backward_det");
 }

@@ -28,6 +28,7 @@
 #include "adan.h"
 #include "binning.h"
 #include "frame.h"
+#include "det.h"
 #include "tile_ids.h"
 
 namespace gsvc {
@@ -57,6 +58,13 @@ struct TrainTileArgs {
                       // 64 (A/B, exact): items in entry order, not longest first
     float *out;       // optional [3, H, W] clamped render
     long long *stamps;  // diagnostic: int64[ntiles][8]
+    // GSVC_TRAIN_DETERMINISTIC (band kernel): the (splat, tile) sums go to
+    // det_part[det_off[g] + k] (k = the tile's row-major index in the splat's
+    // tile bbox, 8 floats) instead of atomics; slots past det_cap fall back to
+    // the atomics
+    const int *det_off;
+    float4 *det_part;
+    long long det_cap;
 };
 
 __device__ __forceinline__ float clamp_unit(float x) {
@@ -1046,11 +1054,28 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
         __syncthreads();
         // 8 lanes per entry add the entry's sums (band 0 + band 1) into the
         // splat's gradient record
-        for (int q = tid; q < gn * 8 && !(A.diag & 32); q += kBThreads) {  // diag 32: no atomics
-            const int e = q >> 3, c = q & 7;
-            const float *ea = &S.part[0][0];
-            unsafeAtomicAdd(A.grad + (size_t)S.gid[e] * 16 + c,
-                            ea[c * kBChunk + e] + ea[8 * kBChunk + c * kBChunk + e]);
+        if (A.det_off) {
+            // deterministic: one 32-byte partial per (splat, tile) at the tile's
+            // place in the splat's bbox; the splat kernel sums them in bbox order
+            for (int q = tid; q < gn * 8; q += kBThreads) {
+                const int e = q >> 3, c = q & 7;
+                const float *ea = &S.part[0][0];
+                const float v = ea[c * kBChunk + e] + ea[8 * kBChunk + c * kBChunk + e];
+                const int g = S.gid[e];
+                const long long slot = det_slot(A.det_off, A.xys, A.radii, g, tx, ty, A.tbx,
+                                                (A.img_h + kTile - 1) / kTile);
+                if (slot < A.det_cap)
+                    reinterpret_cast<float *>(A.det_part)[8 * slot + c] = v;
+                else
+                    unsafeAtomicAdd(A.grad + (size_t)g * 16 + c, v);
+            }
+        } else {
+            for (int q = tid; q < gn * 8 && !(A.diag & 32); q += kBThreads) {  // diag 32: no atomics
+                const int e = q >> 3, c = q & 7;
+                const float *ea = &S.part[0][0];
+                unsafeAtomicAdd(A.grad + (size_t)S.gid[e] * 16 + c,
+                                ea[c * kBChunk + e] + ea[8 * kBChunk + c * kBChunk + e]);
+            }
         }
     }
     if (kStamp && tid == 0) {
@@ -1076,6 +1101,12 @@ struct TrainSplatArgs {
     const float2 *err;
     float *loss;         // [2]: mean squared error, mean absolute error
     unsigned loss_seq;   // non-zero: stored into word 2 of ``loss`` after the losses
+    // GSVC_TRAIN_DETERMINISTIC: splat i's gradient = its partials
+    // det_part[det_off[i] .. det_off[i + 1]) summed in order (+ the record's
+    // atomics of slots past det_cap, zero otherwise)
+    const int *det_off;
+    const float4 *det_part;
+    long long det_cap;
 };
 
 // The loss workgroup's loads per round: 16 tile pairs per thread in flight, so
@@ -1089,8 +1120,21 @@ __device__ __forceinline__ void splat_step(const TrainSplatArgs &A, int i) {
     // per lane instead of three (gradient + radius -> record -> Adan state).
     // rec is written for every splat by the projection, so its load needs no
     // radius test; a first step's neg_pre_grad is loaded and ignored.
-    const float4 g0 = A.grad[4 * i];      // v_xy.x, v_xy.y, v_conic 0, v_conic 1
-    const float4 g1 = A.grad[4 * i + 1];  // v_conic 2, v_colors r g b
+    float4 g0 = A.grad[4 * i];      // v_xy.x, v_xy.y, v_conic 0, v_conic 1
+    float4 g1 = A.grad[4 * i + 1];  // v_conic 2, v_colors r g b
+    if (A.det_off) {
+        // the splat's (splat, tile) partials in bbox row-major order, then the
+        // overflow atomics (zero unless det_cap was too small)
+        const long long b = A.det_off[i], e = min((long long)A.det_off[i + 1], A.det_cap);
+        float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+        for (long long k = b; k < e; ++k) {
+            const float4 p0 = A.det_part[2 * k], p1 = A.det_part[2 * k + 1];
+            s0.x += p0.x; s0.y += p0.y; s0.z += p0.z; s0.w += p0.w;
+            s1.x += p1.x; s1.y += p1.y; s1.z += p1.z; s1.w += p1.w;
+        }
+        g0 = make_float4(s0.x + g0.x, s0.y + g0.y, s0.z + g0.z, s0.w + g0.w);
+        g1 = make_float4(s1.x + g1.x, s1.y + g1.y, s1.z + g1.z, s1.w + g1.w);
+    }
     const float4 r0 = A.rec[3 * i], r2 = A.rec[3 * i + 2];
     const int rad = A.radii[i];
     const float c0 = A.chol[3 * i], c1 = A.chol[3 * i + 1], c2 = A.chol[3 * i + 2];
@@ -1217,6 +1261,10 @@ __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
         if (threadIdx.x == 0) {
             A.loss[0] = (float)(((s_l[0][0] + s_l[0][1]) + (s_l[0][2] + s_l[0][3])) * A.inv_count);
             A.loss[1] = (float)(((s_l[1][0] + s_l[1][1]) + (s_l[1][2] + s_l[1][3])) * A.inv_count);
+            // deterministic mode: this frame's (splat, tile) pair count, so
+            // the caller can size det_capacity (word 3, before the release)
+            if (A.loss_seq && A.det_off)
+                reinterpret_cast<unsigned *>(A.loss)[3] = (unsigned)A.det_off[A.n];
             // coherent host memory: the host stops waiting here, while the
             // splat workgroups still run (later work on the stream is ordered
             // after them anyway)
@@ -1262,14 +1310,21 @@ extern "C" size_t gsvc_train_step_workspace_bytes(int num_points, unsigned img_h
     return train_ws(nullptr, num_points, tiles_of(img_height, img_width)).bytes;
 }
 
-extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
-                                   const float *cholesky_bound, float *features, float *rgb_w,
-                                   int rgb_w_trainable, const float *background, const float *gt,
-                                   unsigned img_height, unsigned img_width, int loss_kind,
-                                   int frame_index, float *const *adan_state,
-                                   const double *adan_hparams, int adan_flags, float *loss,
-                                   float *render_out, float *grads_out, void *workspace,
-                                   size_t workspace_bytes, void *stream) {
+extern "C" size_t gsvc_train_step_det_workspace_bytes(int num_points, long long det_capacity) {
+    const size_t nn = (size_t)(num_points > 0 ? num_points : 0);
+    const size_t cap = (size_t)(det_capacity > 0 ? det_capacity : 0);
+    return ws_align(sizeof(int) * (nn + 1)) + sizeof(float4) * 2 * cap;
+}
+
+static int train_step_impl(int num_points, float *xyz, float *cholesky,
+                           const float *cholesky_bound, float *features, float *rgb_w,
+                           int rgb_w_trainable, const float *background, const float *gt,
+                           unsigned img_height, unsigned img_width, int loss_kind,
+                           int frame_index, float *const *adan_state,
+                           const double *adan_hparams, int adan_flags, float *loss,
+                           float *render_out, float *grads_out, void *workspace,
+                           size_t workspace_bytes, void *stream, void *det_workspace,
+                           size_t det_workspace_bytes, long long det_capacity) {
     if (num_points < 0 || img_height == 0 || img_width == 0)
         return set_error(GSVC_ERR_ARG, "train_step_sum: bad sizes");
     if (!xyz || !cholesky || !features || !background || !gt || !loss || !adan_hparams)
@@ -1317,6 +1372,17 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
                                        "projection flags; PROJECT_NEXT needs PROJECTED");
     if (next && !update)
         return set_error(GSVC_ERR_ARG, "train_step_sum: PROJECT_NEXT needs the Adan update");
+    const bool det = (adan_flags & GSVC_TRAIN_DETERMINISTIC) != 0;
+    int *det_off = nullptr;
+    float4 *det_part = nullptr;
+    if (det) {
+        if (!det_workspace || det_capacity < 0 ||
+            det_workspace_bytes < gsvc_train_step_det_workspace_bytes(num_points, det_capacity))
+            return set_error(GSVC_ERR_WORKSPACE, "train_step_sum: GSVC_TRAIN_DETERMINISTIC needs a "
+                                                 "det_workspace of gsvc_train_step_det_workspace_bytes");
+        det_off = (int *)det_workspace;
+        det_part = (float4 *)((char *)det_workspace + ws_align(sizeof(int) * ((size_t)num_points + 1)));
+    }
     auto project = [&](const FrameSlots &fs) {
         int r = frame_project_launch(num_points, xyz, 1, cholesky, cholesky_bound, features, rgb_w,
                                      nullptr, img_height, img_width, w.f, fs, w.grad, s, 1,
@@ -1334,6 +1400,16 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
         if (only) return refresh ? splat_order_sort(w.f, num_points, tbx, tby, s) : GSVC_OK;
     }
 
+    if (det) {
+        // this frame's (splat, tile) slot offsets, from the projection's xys / radii
+        hipLaunchKernelGGL(det_offsets_kernel, dim3(1), dim3(kDetScanThreads), 0, s, num_points,
+                           (const float2 *)w.f.xys, w.f.radii, tbx, tby, det_off);
+        if (det_capacity > 0 &&
+            hipMemsetAsync(det_part, 0, sizeof(float4) * 2 * (size_t)det_capacity, s) != hipSuccess)
+            return set_error(GSVC_ERR_HIP, "train_step_sum: memset failed");
+        rc = check_launch("train_step_sum: det offsets");
+        if (rc) return rc;
+    }
     const double count = 3.0 * (double)img_height * (double)img_width;  // numel of [3, H, W]
     TrainTileArgs T{};
     T.tbx = tbx;
@@ -1361,6 +1437,9 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     T.spec = g_knobs[12] > 0 && g_knobs[12] <= 64 ? g_knobs[12] : kBSpec;
     T.diag = g_knobs[13];
     T.grouped = g_knobs[14] != 1;
+    T.det_off = det_off;
+    T.det_part = det_part;
+    T.det_cap = det_capacity;
     if (g_knobs[5] == 2 && g_debug_ptr) {  // diagnostic: per-tile stamps
         T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
         auto kfn = train_tile_kernel<true>;
@@ -1369,10 +1448,10 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
         T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
         hipLaunchKernelGGL(train_tile_band_kernel<true>, dim3(ntiles), dim3(kBThreads), 0, s, T);
     } else {
-        // knob 8 = 1: the 256-thread workgroup-per-tile kernel (A/B)
+        // knob 8 = 1: the 256-thread workgroup-per-tile kernel (A/B; atomics only)
         hipEvent_t tev[2];
         const int tslot = timing_begin(s, tev, kTimingTrainTile);
-        if (g_knobs[8] == 1)
+        if (g_knobs[8] == 1 && !det)
             launch_timed(train_tile_kernel<false>, dim3(ntiles), dim3(kT), 0, s, tev, T);
         else
             launch_timed(train_tile_band_kernel<false>, dim3(ntiles), dim3(kBThreads), 0, s, tev, T);
@@ -1404,6 +1483,9 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     const double *h = adan_hparams;
     P.S = adan_scalars(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], adan_flags & 1, h[9]);
     P.grads_out = grads_out;
+    P.det_off = det_off;
+    P.det_part = det_part;
+    P.det_cap = det_capacity;
     P.err = w.err;
     P.loss = loss;
     // GSVC_TRAIN_LOSS_SEQ: ``loss`` is coherent host memory of 3 words; word 2
@@ -1422,11 +1504,26 @@ extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
     return GSVC_OK;
 }
 
+extern "C" int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
+                                   const float *cholesky_bound, float *features, float *rgb_w,
+                                   int rgb_w_trainable, const float *background, const float *gt,
+                                   unsigned img_height, unsigned img_width, int loss_kind,
+                                   int frame_index, float *const *adan_state,
+                                   const double *adan_hparams, int adan_flags, float *loss,
+                                   float *render_out, float *grads_out, void *workspace,
+                                   size_t workspace_bytes, void *stream) {
+    return train_step_impl(num_points, xyz, cholesky, cholesky_bound, features, rgb_w,
+                           rgb_w_trainable, background, gt, img_height, img_width, loss_kind,
+                           frame_index, adan_state, adan_hparams, adan_flags, loss, render_out,
+                           grads_out, workspace, workspace_bytes, stream, nullptr, 0, 0);
+}
+
 extern "C" int gsvc_train_step_sum_args(const gsvc_train_step_args *a) {
     if (!a) return set_error(GSVC_ERR_ARG, "train_step_sum_args: null");
-    return gsvc_train_step_sum(a->num_points, a->xyz, a->cholesky, a->cholesky_bound, a->features,
-                               a->rgb_w, a->rgb_w_trainable, a->background, a->gt, a->img_height,
-                               a->img_width, a->loss_kind, a->frame_index, a->adan_state,
-                               a->adan_hparams, a->adan_flags, a->loss, a->render_out,
-                               a->grads_out, a->workspace, a->workspace_bytes, a->stream);
+    return train_step_impl(a->num_points, a->xyz, a->cholesky, a->cholesky_bound, a->features,
+                           a->rgb_w, a->rgb_w_trainable, a->background, a->gt, a->img_height,
+                           a->img_width, a->loss_kind, a->frame_index, a->adan_state,
+                           a->adan_hparams, a->adan_flags, a->loss, a->render_out, a->grads_out,
+                           a->workspace, a->workspace_bytes, a->stream, a->det_workspace,
+                           a->det_workspace_bytes, a->det_capacity);
 }

@@ -442,10 +442,58 @@ def _raster_bwd(sym, img_height, img_width, BLOCK_H, BLOCK_W, gaussian_ids_sorte
 
 def rasterize_sum_backward(img_height, img_width, BLOCK_H, BLOCK_W, gaussian_ids_sorted, tile_bins,
                            xys, conics, colors, opacities, background, final_Ts, final_idx,
-                           v_output, v_output_alpha):
+                           v_output, v_output_alpha, radii=None):
+    """bindings.cu:706-779.  Under torch.use_deterministic_algorithms(True)
+    and with the splats' ``radii`` (the autograd Function passes them), the
+    bitwise reproducible variant (gsvc_rasterize_sum_backward_det)."""
+    if radii is not None and torch.are_deterministic_algorithms_enabled():
+        return _raster_sum_bwd_det(img_height, img_width, BLOCK_H, BLOCK_W, gaussian_ids_sorted,
+                                   tile_bins, xys, conics, colors, opacities, radii, final_idx,
+                                   v_output)
     return _raster_bwd("gsvc_rasterize_sum_backward", img_height, img_width, BLOCK_H, BLOCK_W,
                        gaussian_ids_sorted, tile_bins, xys, conics, colors, opacities, background,
                        final_Ts, final_idx, v_output, v_output_alpha)
+
+
+DET_PAIRS_PER_SPLAT = 16  # the deterministic backward's first slot capacity per splat
+_det_ws = {}  # device index -> [workspace, capacity, pair count of the last call (device int)]
+
+
+def _raster_sum_bwd_det(img_height, img_width, BLOCK_H, BLOCK_W, gaussian_ids_sorted, tile_bins,
+                        xys, conics, colors, opacities, radii, final_idx, v_output):
+    xys = _f32(xys, "xys")
+    colors = _f32(colors, "colors")
+    if xys.dim() != 2 or xys.shape[1] != 2:
+        raise RuntimeError("xys must have dimensions (num_points, 2)")
+    if colors.dim() != 2 or colors.shape[1] != 3:
+        raise RuntimeError("colors must have 2 dimensions")
+    h, w = int(img_height), int(img_width)
+    tb = ((w + int(BLOCK_W) - 1) // int(BLOCK_W), (h + int(BLOCK_H) - 1) // int(BLOCK_H))
+    gids = _i32(gaussian_ids_sorted, "gaussian_ids_sorted")
+    bins = _bins_for(tile_bins, tb[0] * tb[1])
+    conics = _f32(conics, "conics")
+    opacities = _f32(opacities, "opacities")
+    radii = _i32(radii, "radii")
+    final_idx = _i32(final_idx, "final_idx")
+    v_output = _f32(v_output, "v_output")
+    n = xys.shape[0]
+    dev = xys.device
+    st = _det_ws.get(dev.index)
+    cap = DET_PAIRS_PER_SPLAT * n
+    if st is not None:
+        # grow past the pair count an earlier call reported (a short capacity
+        # falls back to atomics for the pairs past it: correct, not reproducible)
+        cap = max(cap, st[1], int(st[2]) * 3 // 2)
+    need = L.size("gsvc_rasterize_sum_backward_det_workspace_bytes", n, cap)
+    if st is None or st[0].numel() < need or st[1] != cap:
+        st = _det_ws[dev.index] = [torch.empty((need,), dtype=torch.uint8, device=dev), cap,
+                                   torch.zeros((1,), dtype=torch.int32, device=dev)]
+    rec = torch.empty((n, 16), dtype=torch.float32, device=dev)
+    _timed_call("gsvc_rasterize_sum_backward_det", h, w, int(BLOCK_H), int(BLOCK_W), n,
+                L.ptr(gids), L.ptr(bins), L.ptr(xys), L.ptr(conics), L.ptr(colors),
+                L.ptr(opacities), L.ptr(radii), L.ptr(final_idx), L.ptr(v_output), L.ptr(rec),
+                L.ptr(st[0]), st[0].numel(), cap, L.ptr(st[2]), L.stream(dev))
+    return split_grad_records(rec)
 
 
 def rasterize_backward(img_height, img_width, BLOCK_H, BLOCK_W, gaussian_ids_sorted, tile_bins,

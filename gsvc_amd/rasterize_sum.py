@@ -114,8 +114,9 @@ class _RasterizeGaussiansSum(Function):
         ctx.BLOCK_H = BLOCK_H
         ctx.BLOCK_W = BLOCK_W
         ctx.num_intersects = num_intersects
+        # (radii only for the deterministic backward's slot layout)
         ctx.save_for_backward(gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
-                              background, final_idx)
+                              background, final_idx, radii)
 
         if return_alpha:
             if final_Ts is None:
@@ -138,7 +139,7 @@ class _RasterizeGaussiansSum(Function):
             v_out_alpha = torch.zeros_like(v_out_img[..., 0])
 
         (gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
-         final_idx) = ctx.saved_tensors
+         final_idx, radii) = ctx.saved_tensors
 
         if num_intersects is not None and num_intersects < 1:
             v_xy = torch.zeros_like(xys)
@@ -149,7 +150,7 @@ class _RasterizeGaussiansSum(Function):
             v_xy, v_conic, v_colors, v_opacity = _C.rasterize_sum_backward(
                 img_height, img_width, ctx.BLOCK_H, ctx.BLOCK_W, gaussian_ids_sorted, tile_bins,
                 xys, conics, colors, opacity, background, None, final_idx, v_out_img,
-                v_out_alpha)
+                v_out_alpha, radii=radii)
             v_opacity = v_opacity.reshape(opacity.shape) if opacity.dim() != 2 else v_opacity
 
         return (

@@ -13,6 +13,7 @@ learning rate, so fused and op-by-op iterations interleave freely.
 from __future__ import annotations
 
 import ctypes
+import weakref
 from typing import Optional, Sequence
 
 import torch
@@ -28,6 +29,8 @@ ORDER_REFRESH_EVERY = 64  # fused steps between splat-order sorts (0: no order)
 TRAIN_PROJECT_ONLY = 0x800  # GSVC_TRAIN_PROJECT_ONLY
 TRAIN_PROJECTED = 0x1000  # GSVC_TRAIN_PROJECTED
 TRAIN_PROJECT_NEXT = 0x2000  # GSVC_TRAIN_PROJECT_NEXT
+TRAIN_DETERMINISTIC = 0x4000  # GSVC_TRAIN_DETERMINISTIC
+DET_CAPACITY_PER_SPLAT = 8  # first det_capacity guess: M / N is ~2.5 at init, ~5 trained
 PROJECT_AHEAD = True  # a bound step enqueues the next step's projection after itself
 
 # A step's projection of the NEXT frame is used only if nothing could have
@@ -56,7 +59,22 @@ class _TrainWorkspace:
         self.shape = None
         self.order_for = None  # (n, H, W) the workspace's splat order was sorted for
         self.order_age = 0     # steps since it was sorted
-        self.pending = None    # the projection a bound step enqueued ahead (BoundStep.launch)
+        self.pending = None    # the projection a bound step enqueued ahead (BoundStep.launch):
+        #                        (weakref to the step, frame, launch count, epoch, versions)
+        self.det_buf = None    # GSVC_TRAIN_DETERMINISTIC workspace
+        self.det_cap = 0
+
+    def det_workspace(self, dev: torch.device, n: int, pairs: int = 0):
+        """The deterministic mode's slot buffer for n splats, with room for at
+        least ``pairs`` (splat, tile) pairs (grown by half again when short)."""
+        cap = max(self.det_cap, DET_CAPACITY_PER_SPLAT * n)
+        if pairs > cap:
+            cap = pairs + pairs // 2
+        need = L.size("gsvc_train_step_det_workspace_bytes", n, cap)
+        if self.det_buf is None or self.det_buf.numel() < need or cap != self.det_cap:
+            self.det_buf = torch.empty((need,), dtype=torch.uint8, device=dev)
+            self.det_cap = cap
+        return self.det_buf, cap
 
     def order_flags(self) -> int:
         return order_flags(self)
@@ -133,7 +151,8 @@ class _StepArgs(ctypes.Structure):
                 ("adan_flags", ctypes.c_int), ("loss", ctypes.c_void_p),
                 ("render_out", ctypes.c_void_p), ("grads_out", ctypes.c_void_p),
                 ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_size_t),
-                ("stream", ctypes.c_void_p)]
+                ("stream", ctypes.c_void_p), ("det_workspace", ctypes.c_void_p),
+                ("det_workspace_bytes", ctypes.c_size_t), ("det_capacity", ctypes.c_longlong)]
 
 
 class BoundStep:
@@ -175,9 +194,12 @@ class BoundStep:
         a.adan_hparams = ctypes.addressof(self.hp)
         self.args_ref = ctypes.byref(a)
         self.fn = L.load().gsvc_train_step_sum_args
-        self.host = None  # coherent host words: mse, l1, sequence
+        self.host = None  # coherent host words: mse, l1, sequence, (det) pairs
         self.seq = 0
         self.stream = None
+        self.det = False        # this step runs GSVC_TRAIN_DETERMINISTIC
+        self.det_pairs = 0      # the (splat, tile) pairs its last det step reported
+        self.det_overflows = 0  # det steps whose capacity was short (those fell back to atomics)
         self.params = tuple(t for t in (xyz, cholesky, features, rgb_w) if t is not None)
 
     def __del__(self):
@@ -216,13 +238,26 @@ class BoundStep:
             if not self.host:
                 raise RuntimeError(lib.gsvc_last_error().decode(errors="replace"))
             self.host_f = (ctypes.c_float * 4).from_address(self.host)
+            self.host_u = (ctypes.c_uint * 4).from_address(self.host)
             a.loss = self.host
+        # a stale sequence word must not satisfy this step's wait (a workspace on
+        # another stream counts its frames from 0 again)
+        self.host_u[2] = 0
         self.stream = _raw_stream(self.dev.index)
         flags = int(adan_flags) | TRAIN_LOSS_SEQ
+        # torch.use_deterministic_algorithms(True): bitwise reproducible gradients
+        self.det = torch.are_deterministic_algorithms_enabled()
+        if self.det:
+            buf, cap = ws.det_workspace(self.dev, self.n, self.det_pairs)
+            a.det_workspace, a.det_workspace_bytes, a.det_capacity = buf.data_ptr(), buf.numel(), cap
+            flags |= TRAIN_DETERMINISTIC
+            adan_flags = int(adan_flags) | TRAIN_DETERMINISTIC
+        else:
+            a.det_workspace, a.det_workspace_bytes, a.det_capacity = None, 0, 0
         if PROJECT_AHEAD:
             versions = tuple(t._version for t in self.params)
             pend = ws.pending
-            ahead = (pend is not None and pend[0] is self and pend[1] == ws.frame
+            ahead = (pend is not None and pend[0]() is self and pend[1] == ws.frame
                      and pend[2] == _launch_count[0] and pend[3] == _param_epoch[0]
                      and pend[4] == versions)
             if pend is not None and not ahead:
@@ -237,7 +272,8 @@ class BoundStep:
         self._call(ws, lib, gt, flags | ws.order_flags())
         _launch_count[0] += 1
         if PROJECT_AHEAD:
-            ws.pending = (self, ws.frame + 1, _launch_count[0], _param_epoch[0], versions)
+            ws.pending = (weakref.ref(self), ws.frame + 1, _launch_count[0], _param_epoch[0],
+                          versions)
         ws.frame += 1
 
     def _call(self, ws, lib, gt, flags):
@@ -259,6 +295,12 @@ class BoundStep:
         waits for its sequence word (the reference's PSNR ``.item()``); after
         50 ms of spinning, for the whole stream, which reports a failed kernel."""
         L.call("gsvc_wait_host_seq", self.host + 8, self.seq, self.stream, 50000)
+        if self.det:
+            pairs = int(self.host_u[3])
+            ws = _workspace(self.dev, self.n, self.H, self.W)
+            if pairs > ws.det_cap:
+                self.det_overflows += 1
+            self.det_pairs = pairs
         return self.host_f[0], self.host_f[1]
 
 
@@ -305,10 +347,22 @@ def train_step_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, rgb_w: Optio
         ws = _workspace(dev, n, H, W)
     _launch_count[0] += 1
     loss = torch.empty((2,), dtype=torch.float32, device=dev)
-    rc = L.load().gsvc_train_step_sum(
-        n, p_xyz, p_chol, p_bound, p_feat, p_rgbw, 1 if rgb_w_trainable else 0, p_bg, p_gt, H, W,
-        LOSS_KIND[loss_type], ws.frame, state, hp, int(adan_flags), loss.data_ptr(), p_render,
-        p_grads, ws.buf_ptr, ws.buf.numel(), _raw_stream(dev.index))
+    a = _StepArgs()
+    a.num_points, a.xyz, a.cholesky, a.cholesky_bound = n, p_xyz, p_chol, p_bound
+    a.features, a.rgb_w, a.rgb_w_trainable = p_feat, p_rgbw, 1 if rgb_w_trainable else 0
+    a.background, a.gt, a.img_height, a.img_width = p_bg, p_gt, H, W
+    a.loss_kind, a.frame_index = LOSS_KIND[loss_type], ws.frame
+    a.adan_state, a.adan_hparams = ctypes.addressof(state), ctypes.addressof(hp)
+    flags = int(adan_flags)
+    if torch.are_deterministic_algorithms_enabled():
+        # no pair count comes back without GSVC_TRAIN_LOSS_SEQ: room for 16 per
+        # splat (pairs past it fall back to the atomics)
+        buf, cap = ws.det_workspace(dev, n, 16 * n)
+        a.det_workspace, a.det_workspace_bytes, a.det_capacity = buf.data_ptr(), buf.numel(), cap
+        flags |= TRAIN_DETERMINISTIC
+    a.adan_flags, a.loss, a.render_out, a.grads_out = flags, loss.data_ptr(), p_render, p_grads
+    a.workspace, a.workspace_bytes, a.stream = ws.buf_ptr, ws.buf.numel(), _raw_stream(dev.index)
+    rc = L.load().gsvc_train_step_sum_args(ctypes.byref(a))
     if rc != 0:
         ws.dirty = True
         msg = L.load().gsvc_last_error().decode(errors="replace")

@@ -353,6 +353,20 @@ int gsvc_render_frame_sum_ex(int num_points, const float *xyz, int xyz_tanh,
 #define GSVC_TRAIN_PROJECT_ONLY 0x800
 #define GSVC_TRAIN_PROJECTED 0x1000
 #define GSVC_TRAIN_PROJECT_NEXT 0x2000
+/* GSVC_TRAIN_DETERMINISTIC (gsvc_train_step_sum_args only): bitwise
+ * reproducible gradients.  The tile kernel writes each (splat, tile) gradient
+ * sum -- itself formed in a fixed order -- to its own slot instead of adding
+ * it with float atomics (backward.cu:843-859 uses atomics, so the reference
+ * is not reproducible run to run), and the splat kernel adds a splat's slots
+ * in tile-bbox row-major order.  Needs det_workspace of
+ * gsvc_train_step_det_workspace_bytes(num_points, det_capacity) bytes;
+ * det_capacity (>= the frame's M, the (splat, tile) pairs) slots of 32 B.
+ * Pairs past the capacity fall back to the atomics (correct, not
+ * reproducible).  With GSVC_TRAIN_LOSS_SEQ, ``loss`` then holds 4 words and
+ * word 3 receives the frame's M (before the sequence word), so the caller can
+ * grow det_capacity. */
+#define GSVC_TRAIN_DETERMINISTIC 0x4000
+size_t gsvc_train_step_det_workspace_bytes(int num_points, long long det_capacity);
 size_t gsvc_train_step_workspace_bytes(int num_points, unsigned img_height,
                                        unsigned img_width);
 int gsvc_train_step_sum(int num_points, float *xyz, float *cholesky,
@@ -383,6 +397,10 @@ typedef struct gsvc_train_step_args {
     void *workspace;
     size_t workspace_bytes;
     void *stream;
+    /* GSVC_TRAIN_DETERMINISTIC only (else NULL / 0) */
+    void *det_workspace;
+    size_t det_workspace_bytes;
+    long long det_capacity;
 } gsvc_train_step_args;
 int gsvc_train_step_sum_args(const gsvc_train_step_args *args);
 
@@ -420,6 +438,24 @@ int gsvc_rasterize_sum_backward(
     const float *opacities, const float *background, const float *final_Ts,
     const int *final_idx, const float *v_output, const float *v_output_alpha,
     float *grad_records, void *stream);
+
+/* The same backward with bitwise reproducible sums (the op path under
+ * torch.use_deterministic_algorithms; not part of the reference, whose
+ * backward.cu:843-859 adds with float atomics): each (splat, tile) sum is
+ * stored to its own slot -- det_off[splat] + the tile's row-major index in the
+ * splat's tile bbox, from xys and radii -- and every splat then adds its slots
+ * in that order.  det_workspace of
+ * gsvc_rasterize_sum_backward_det_workspace_bytes(num_points, det_capacity)
+ * bytes; pairs past det_capacity fall back to the atomics.  pairs_out
+ * (optional, device int): the (splat, tile) pair count, to size the capacity. */
+size_t gsvc_rasterize_sum_backward_det_workspace_bytes(int num_points, long long det_capacity);
+int gsvc_rasterize_sum_backward_det(
+    unsigned img_height, unsigned img_width, unsigned block_h, unsigned block_w,
+    int num_points, const int *gaussian_ids_sorted, const int *tile_bins,
+    const float *xys, const float *conics, const float *colors,
+    const float *opacities, const int *radii, const int *final_idx,
+    const float *v_output, float *grad_records, void *det_workspace,
+    size_t det_workspace_bytes, long long det_capacity, int *pairs_out, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Alpha-compositing rasterizer (rasterize.py; north_star's front-to-back path).

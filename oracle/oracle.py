@@ -417,21 +417,15 @@ def adan_step(p, grad, st, step, lr=1e-3, betas=(0.98, 0.92, 0.99), eps=1e-8, we
     return p
 
 
-def train_iter_sum(params, gt, H, W, state, step, lr=1e-3):
-    """GaussianVideo_frame.train_iter (GaussianSplats_Represent.py:191-207) for
-    the L2 loss, no prune / densify, on CPU: activations (:57-70), the sum-path
-    forward (render_sum), clamp, F.mse_loss against ``gt`` [3, H, W], its
-    gradient through the clamp (torch clamp passes where 0 <= out <= 1), the
-    rasterizer and projection VJPs, the activation VJPs and one Adan step of
-    _xyz, _cholesky, _features_dc (rgb_W fixed at ones).  ``params``: dict of
-    float32 arrays ``_xyz`` [N,2], ``_cholesky`` [N,3], ``_features_dc`` [N,3],
-    updated in place; ``state``: dict of per-parameter Adan state dicts.
-    Returns (loss, psnr)."""
-    xyz, chol, feat = params["_xyz"], params["_cholesky"], params["_features_dc"]
-    n = xyz.shape[0]
-    means = np.tanh(xyz).astype(F32)
-    L = (chol + np.array([0.5, 0.0, 0.5], F32)).astype(F32)
-    colors = feat.astype(F32)
+def train_grads_sum(means, L, colors, gt, H, W):
+    """The part of GaussianVideo_frame.train_iter (GaussianSplats_Represent.py:
+    191-195) before Adan, from ACTIVATED inputs (means2d = tanh(_xyz), L,
+    colors; opacity 1): the sum-path forward, clamp, F.mse_loss against ``gt``
+    [3, H, W], its gradient through the clamp (torch clamp passes where 0 <=
+    out <= 1), the rasterizer and projection VJPs.  Returns (loss, render
+    [3, H, W] clamped, v_means2d [N,2], v_L [N,3], v_colors [N,3]) in float32
+    (loss float64)."""
+    n = means.shape[0]
     opac = np.ones((n, 1), F32)
     r = render_sum(means, L, colors, opac, H, W)
     out = r["out"]
@@ -441,21 +435,35 @@ def train_iter_sum(params, gt, H, W, state, step, lr=1e-3):
     numel = 3 * H * W
     loss = float(np.mean(d.astype(F64) ** 2))
     if r["m"] < 1:
-        grads = [np.zeros_like(xyz), np.zeros_like(chol), np.zeros_like(feat)]
-    else:
-        v_img = (np.float32(2.0 / numel) * d).astype(F32)
-        v_img[(img < 0.0) | (img > 1.0)] = 0.0  # (never: img is clamped; kept for the rule)
-        o_chw = out.transpose(2, 0, 1)
-        v_img[(o_chw < 0.0) | (o_chw > 1.0)] = 0.0
-        v_out = np.ascontiguousarray(v_img.transpose(1, 2, 0))
-        tb = r["tb"]
-        v_xy, v_conic, v_rgb, _ = raster_sum_backward(tb, H, W, r["gids_sorted"], r["bins"], r["xys"],
-                                                      r["conics"], colors, opac, r["final_idx"],
-                                                      v_out)
-        _, v_mean2d, v_L = project_2d_backward(L, H, W, r["radii"], r["conics"],
-                                               v_xy.astype(F32), v_conic.astype(F32))
-        d_xyz = (v_mean2d * (1.0 - means * means)).astype(F32)
-        grads = [d_xyz, v_L.astype(F32), v_rgb.astype(F32)]
+        z2, z3 = np.zeros((n, 2), F32), np.zeros((n, 3), F32)
+        return loss, img, z2, z3, z3.copy()
+    v_img = (np.float32(2.0 / numel) * d).astype(F32)
+    v_img[(img < 0.0) | (img > 1.0)] = 0.0  # (never: img is clamped; kept for the rule)
+    o_chw = out.transpose(2, 0, 1)
+    v_img[(o_chw < 0.0) | (o_chw > 1.0)] = 0.0
+    v_out = np.ascontiguousarray(v_img.transpose(1, 2, 0))
+    tb = r["tb"]
+    v_xy, v_conic, v_rgb, _ = raster_sum_backward(tb, H, W, r["gids_sorted"], r["bins"], r["xys"],
+                                                  r["conics"], colors, opac, r["final_idx"], v_out)
+    _, v_mean2d, v_L = project_2d_backward(L, H, W, r["radii"], r["conics"], v_xy.astype(F32),
+                                           v_conic.astype(F32))
+    return loss, img, v_mean2d, v_L.astype(F32), v_rgb.astype(F32)
+
+
+def train_iter_sum(params, gt, H, W, state, step, lr=1e-3):
+    """GaussianVideo_frame.train_iter (GaussianSplats_Represent.py:191-207) for
+    the L2 loss, no prune / densify, on CPU: activations (:57-70),
+    train_grads_sum, the activation VJPs and one Adan step of _xyz, _cholesky,
+    _features_dc (rgb_W fixed at ones).  ``params``: dict of float32 arrays
+    ``_xyz`` [N,2], ``_cholesky`` [N,3], ``_features_dc`` [N,3], updated in
+    place; ``state``: dict of per-parameter Adan state dicts.
+    Returns (loss, psnr)."""
+    xyz, chol, feat = params["_xyz"], params["_cholesky"], params["_features_dc"]
+    means = np.tanh(xyz).astype(F32)
+    L = (chol + np.array([0.5, 0.0, 0.5], F32)).astype(F32)
+    loss, _, v_mean2d, v_L, v_rgb = train_grads_sum(means, L, feat.astype(F32), gt, H, W)
+    d_xyz = (v_mean2d * (1.0 - means * means)).astype(F32)
+    grads = [d_xyz, v_L, v_rgb]
     for name, p, g in zip(("_xyz", "_cholesky", "_features_dc"), (xyz, chol, feat), grads):
         adan_step(p, g, state.setdefault(name, {}), step, lr=lr)
     return loss, 10.0 * math.log10(1.0 / loss)

@@ -4,7 +4,7 @@
 
 This script imports the reference Python from /root/reference (read-only) and
 is never run by the tests or on the GPU box; only its outputs (.npz data) are
-committed.  Four kinds of fixtures are produced:
+committed.  Five kinds of fixtures are produced:
 
 1. ``sum_*.npz`` / ``alpha_*.npz``: the reference's own autograd glue
    (gsplat/project_gaussians_2d.py:59-141, rasterize_sum.py:14-254,
@@ -21,7 +21,12 @@ committed.  Four kinds of fixtures are produced:
 3. ``train_iter_*.npz``: one and two ``GaussianVideo_frame.train_iter`` steps
    (GaussianSplats_Represent.py:191-207, L2 loss, Adan optimizer.py:39-362) of
    the reference model on CPU, oracle injected.
-4. ``prune_controls.npz``: ``removal_control`` / ``adaptive_control``
+4. ``train_state_1080p_n50k.npz`` (``make_golden.py trained STATE.npz``): the
+   state bench.py times -- its 1080p / 50k frame after 2020 training
+   iterations, trained on the CPU by the oracle (tools/train_oracle_state.py)
+   -- and the reference's own forward / backward / three train_iter steps
+   from it (make_trained_state_case).
+5. ``prune_controls.npz``: ``removal_control`` / ``adaptive_control``
    (GaussianSplats_Represent.py:98-172) of the reference model on CPU with a
    stable torch.sort, on rgb_W with tie groups, NaN, +-0 and underflowing
    squares (``python tests/golden/make_golden.py prune`` remakes only this).
@@ -424,8 +429,9 @@ TRAINED_CROPS = ((0, 0), (512, 960), (1064, 1904), (300, 1500), (777, 123))
 
 def make_trained_state_case(state_path, name="train_state_1080p_n50k", steps=3, keep=4096):
     """BASELINE configs[2] at the state bench.py times: the bench's 1080p / 50k
-    frame after its settle + warmup iterations (trained density, M ~ 240k),
-    dumped from the GPU by tools/dump_trained.py and loaded here into the
+    frame (seed 1000, target seed 8) after its settle + warmup iterations
+    (trained density, M ~ 230-240k), trained on the CPU by the oracle's
+    train_iter_sum (tools/train_oracle_state.py), loaded here into the
     reference model.  Records, from the reference's own Python with the oracle
     injected (GaussianSplats_Represent.py:83-90,191-207, fresh Adan):
 
