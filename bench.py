@@ -285,12 +285,10 @@ def cpu_baseline(n_splats, reps=5, warm=2):
         params = {name: np.array(z["state_" + name], copy=True)
                   for name in ("_xyz", "_cholesky", "_features_dc")}
         state = {}
-        step = int(z["iters"])
         ts = []
         for i in range(warm + reps):
-            step += 1
             t0 = time.perf_counter()
-            O.train_iter_sum(params, gt, H, W, state, step)
+            O.train_iter_sum(params, gt, H, W, state, i + 1)  # Adan's own step count
             ts.append(time.perf_counter() - t0)
         ts = sorted(ts[warm:])
         runs[k] = ts[len(ts) // 2]

@@ -456,8 +456,9 @@ def train_iter_sum(params, gt, H, W, state, step, lr=1e-3):
     train_grads_sum, the activation VJPs and one Adan step of _xyz, _cholesky,
     _features_dc (rgb_W fixed at ones).  ``params``: dict of float32 arrays
     ``_xyz`` [N,2], ``_cholesky`` [N,3], ``_features_dc`` [N,3], updated in
-    place; ``state``: dict of per-parameter Adan state dicts.
-    Returns (loss, psnr)."""
+    place; ``state``: dict of per-parameter Adan state dicts; ``step``: the
+    optimizer's own step count (1 for a fresh Adan, as optimizer.py:171-173
+    counts it -- not the training iteration).  Returns (loss, psnr)."""
     xyz, chol, feat = params["_xyz"], params["_cholesky"], params["_features_dc"]
     means = np.tanh(xyz).astype(F32)
     L = (chol + np.array([0.5, 0.0, 0.5], F32)).astype(F32)

@@ -29,9 +29,10 @@ same inputs:
   trained density);
 * the op path's rasterize_sum_backward against oracle.raster_sum_backward at
   full size, v_out ~ N(0, 1), same tolerance;
-* three train_iter steps: losses / PSNRs as above, parameters by the
-  trajectory test's quantile bars (Adan normalises near-zero gradient sums,
-  tests/test_train_trajectory.py).
+* three train_iter steps (a fresh Adan, as a P-frame's): step 1 as above;
+  steps 2-3 within STEP_PSNR_TOL, the envelope the reference's own arithmetic
+  shows under a 1-ulp tanh change; parameters by the trajectory test's
+  quantile bars (Adan normalises near-zero gradient sums).
 """
 import numpy as np
 import pytest
@@ -41,6 +42,12 @@ from conftest import load_golden
 
 FIX = "train_state_1080p_n50k"
 H, W = 1080, 1920
+# PSNR bar for train_iter steps 2 and 3 from the fixture (step 1 is held to
+# 1e-4 dB): a fresh Adan moves every element by ~lr * sign(gradient), so an
+# element whose gradient sign flips with a last-bit change of the inputs moves
+# the other way; with the reference's own arithmetic and numpy's tanh in place
+# of torch's the PSNR moves by 1.5e-4 and 9.5e-4 dB (test_oracle_reproduces_fixture)
+STEP_PSNR_TOL = 2e-3
 
 
 def _z():
@@ -109,9 +116,16 @@ def test_oracle_reproduces_fixture(oracle):
                                    rtol=2e-6)
         gt = _gt(z, "cpu").numpy()[0]
         state = {}
-        loss, psnr = oracle.train_iter_sum(params, gt, H, W, state, int(z["iters"]) + 1)
-        assert abs(loss - z["losses"][0]) <= 2e-6 * z["losses"][0]
-        assert abs(psnr - z["psnrs"][0]) <= 1e-4
+        # the fixture's optimizer is fresh: Adan steps 1, 2, 3 (its own count)
+        out = [oracle.train_iter_sum(params, gt, H, W, state, k + 1) for k in range(3)]
+        losses, psnrs = np.array([o[0] for o in out]), np.array([o[1] for o in out])
+        assert abs(losses[0] - z["losses"][0]) <= 2e-6 * z["losses"][0]
+        assert abs(psnrs[0] - z["psnrs"][0]) <= 1e-4
+        # the envelope of STEP_PSNR_TOL: numpy's tanh differs from torch's by an
+        # ulp in a third of the centres; the fresh Adan's sign-normalised first
+        # steps then move the PSNR by ~1e-3 dB (measured 1.5e-4, 9.5e-4)
+        d = np.abs(psnrs - z["psnrs"])
+        assert d[1:].max() <= STEP_PSNR_TOL, d
     finally:
         oracle.set_threads(1)
 
@@ -295,6 +309,8 @@ def test_trained_train_iter_steps_match_reference(cuda, fused):
         losses.append(float(loss))
         psnrs.append(psnr)
     assert m.fused_steps == (len(losses) if fused else 0)
-    np.testing.assert_allclose(psnrs, z["psnrs"], rtol=0, atol=1e-4)
-    np.testing.assert_allclose(losses, z["losses"], rtol=2e-5, atol=0)
+    assert abs(psnrs[0] - z["psnrs"][0]) <= 1e-4
+    assert abs(losses[0] - z["losses"][0]) <= 2e-6 * z["losses"][0]
+    np.testing.assert_allclose(psnrs[1:], z["psnrs"][1:], rtol=0, atol=STEP_PSNR_TOL)
+    np.testing.assert_allclose(losses[1:], z["losses"][1:], rtol=1e-3, atol=0)
     _check_params(m, z)

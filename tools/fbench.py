@@ -41,6 +41,8 @@ def main():
                     metavar=("KEY", "VALUE"), help="extra gsvc_debug_set for a second pass")
     ap.add_argument("--stamps", action="store_true",
                     help="also run the timestamped one-wave kernel (mode 7) and print phases")
+    ap.add_argument("--stamps-out", default=None,
+                    help="with --stamps: save the raw per-tile stamps (us) and entry counts (npz)")
     ap.add_argument("--proj-stamps", action="store_true",
                     help="also stamp the projection kernel's waves (knob 5) and print phases")
     args = ap.parse_args()
@@ -156,6 +158,19 @@ def main():
                                   start=q(t[:, 0] - t0), staged=q(t[:, 1] - t[:, 0]),
                                   blend=q(t[:, 2] - t[:, 1]), stores_drained=q(t[:, 3] - t[:, 2]),
                                   end=q(t[:, 3] - t0))), flush=True)
+            if args.stamps_out:
+                from gsvc_amd import ops
+                from gsvc_amd.utils import bin_and_sort_for_raster
+                tbs = ((W + 15) // 16, (H + 15) // 16, 1)
+                with torch.no_grad():
+                    means = torch.tanh(xyz)
+                    L_ = chol + bound
+                    xys, depths, radii, conics, nth = ops.project_gaussians_2d_forward(
+                        n, means, L_, H, W, tbs, 0.01)
+                    _, _, bins = bin_and_sort_for_raster(n, xys, depths, radii, nth, tbs)
+                counts = (bins[:, 1] - bins[:, 0]).clamp(min=0).cpu().numpy()
+                np.savez_compressed(args.stamps_out, stamps_us=t - t0, counts=counts,
+                                    tbx=tbs[0], tby=tbs[1])
         if args.proj_stamps:
             import numpy as np
             waves = (n + 63) // 64

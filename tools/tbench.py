@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--knob-after", action="append", default=[],
                     help="knob K=V set only after the warmup (diagnostic variants that change "
                          "results must not steer the training state being measured)")
+    ap.add_argument("--stamps-out", default=None,
+                    help="with --stamps: save the raw per-tile stamps (us, tile order) as npz")
     ap.add_argument("--proj-stamps", action="store_true",
                     help="also stamp the projection kernel's waves (start, projected, inserted, end)")
     ap.add_argument("--order-every", type=int, default=None,
@@ -163,6 +165,10 @@ def main():
         lib.gsvc_debug_set(5, 0)
         lib.gsvc_debug_set_ptr(None)
         t = st.cpu().numpy().astype(np.float64) * 0.01
+        if a.stamps_out:
+            raw = st.cpu().numpy()
+            np.savez_compressed(a.stamps_out, stamps_us=raw[:, :6] * 0.01 - t[t[:, 5] > 0][:, 0].min(),
+                                counts=raw[:, 6], tbx=(W + 15) // 16, tby=(H + 15) // 16)
         t = t[t[:, 5] > 0]
         t0 = t[:, 0].min()
         q = lambda x: [round(float(np.percentile(x, p)), 2) for p in (0, 10, 50, 90, 100)]  # noqa
