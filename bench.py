@@ -411,7 +411,8 @@ def video_decode(device, frames=8, splats=10000, steps=50, warmup=5):
     return {"workload": f"GOP of {frames} distinct 1920x1080 frame models x {splats} splats, one "
                         "gsvc_render_frames_sum call per step",
             "frames_per_s": round(frames * steps / el, 1), "ms_per_call": round(1e3 * el / steps, 4),
-            "roofline": roofline("raster_sum_fwd_kernel (frames x tiles)", nbytes, kt)}
+            "roofline": roofline("raster_sum_fwd_kernel (frames x tiles)", nbytes, kt,
+                                 load_profile("video_decode"), "rasterize_sum_forward")}
 
 
 def dry_run(args, world, rank):

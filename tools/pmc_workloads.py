@@ -4,7 +4,9 @@
   train50k   GaussianVideoFrame at 1920x1080 / 50k splats: --settle training
              iterations, then --iters more (the bench's trained state), then
              --iters renders of the trained model (configs[2] render);
-  render10k  --iters renders of a random-init 10k-splat frame (configs[1]).
+  render10k  --iters renders of a random-init 10k-splat frame (configs[1]);
+  decode8    --iters batched renders of a GOP of 8 distinct 10k-splat frame
+             models (bench.py ``video_decode``: one gsvc_render_frames_sum call).
 
 Summaries take each kernel's last --iters dispatches (tools/prof_summary.py
 --last), i.e. the trained state.
@@ -21,13 +23,27 @@ import torch  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["train50k", "render10k"])
+    ap.add_argument("mode", choices=["train50k", "render10k", "decode8"])
     ap.add_argument("--settle", type=int, default=2000)
     ap.add_argument("--iters", type=int, default=50)
     a = ap.parse_args()
     from gsvc_amd.frame import make_frame_model, synthetic_gt
     dev = torch.device("cuda:0")
     H, W = 1080, 1920
+    if a.mode == "decode8":
+        from gsvc_amd.render import render_frames_sum
+        frames, splats = 8, 10000
+        g = torch.Generator().manual_seed(4242)  # bench.py video_decode's inputs
+        xyz = torch.atanh(2 * (torch.rand(frames * splats, 2, generator=g) - 0.5)).to(dev)
+        chol = torch.rand(frames * splats, 3, generator=g).to(dev)
+        feat = torch.rand(frames * splats, 3, generator=g).to(dev)
+        bound = torch.tensor([0.5, 0.0, 0.5], device=dev)
+        bg = torch.ones(3, device=dev)
+        for _ in range(a.iters + 5):
+            render_frames_sum(xyz, chol, feat, [splats] * frames, H, W, bg, cholesky_bound=bound)
+        torch.cuda.synchronize()
+        print("done", a.mode, flush=True)
+        return
     if a.mode == "train50k":
         model = make_frame_model(H, W, 50000, dev, seed=1000)
         gt = synthetic_gt(H, W, 8, "cpu").to(dev)
