@@ -22,7 +22,7 @@ constexpr float kAlphaMin = 1.0f / 255.0f;
 // Host-side error plumbing -------------------------------------------------
 int set_error(int code, const char *fmt, ...);
 int check_launch(const char *what);
-constexpr int kKnobs = 16;
+constexpr int kKnobs = 24;
 extern int g_knobs[kKnobs];  // gsvc_debug_set(); knob 0 = sum-forward variant, 8 = training tile kernel
 extern void *g_debug_ptr;  // gsvc_debug_set_ptr(): diagnostic output buffer
 // timing.hip: slot, or -1 when not recording; dispatch_ev[2] = the events the

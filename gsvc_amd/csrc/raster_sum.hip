@@ -69,7 +69,9 @@ constexpr int kSlice = 220;  // float4s of LDS per wave (3.4 KB; sum_fwd_sparse'
 // mode: a 128-thread workgroup whose second wave exits at once still halves
 // the dispatch rate of sparse tiles.
 enum { kModeAdaptive = 6, kModeSparse = 1, kModeBanded = 2, kModeStamp = 3, kModeNoBlend = 4,
-       kModeNoStore = 5, kModeSparseStamp = 7 };
+       kModeNoStore = 5, kModeSparseStamp = 7, kModeSparsePrio = 8 };
+// kModeSparsePrio: kModeSparse with the wave priority raised over the staging
+// (s_setprio 3 until the blend; A/B knob 17 = 1 selects it for the sparse launches)
 // Banded (two waves per tile) only past this many entries per tile on average.
 // Measured with the lane-group lists (1080p, tools/fbench.py, profiles/r02/composite_modes/):
 // sparse wins from 3 to 62 entries per tile (trained 50k, 28 per tile: 43.0 vs 48.0 us per
@@ -335,6 +337,7 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         wave_lds_sync();
         const int k0 = range.x + base;
         if (cnt <= kGroupMin) {
+            if (kMode == kModeSparsePrio) __builtin_amdgcn_s_setprio(0);
             // a few entries: every lane walks them all (the lists would cost
             // more than the pairs they skip)
             if (kMode == kModeSparseStamp && base == 0 && lane == 0) A.stamps[4 * (size_t)tile + 1] = stamp();
@@ -366,6 +369,7 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
             maxlen = max(maxlen, __popcll(mg));
         }
         wave_lds_sync();
+        if (kMode == kModeSparsePrio) __builtin_amdgcn_s_setprio(0);
         if (kMode == kModeSparseStamp && base == 0 && lane == 0) A.stamps[4 * (size_t)tile + 1] = stamp();
         // the lane's 4x4 block of the tile
         const unsigned char *ml = s_list + (((lane >> 4) << 2) | (lane & 3));
@@ -613,11 +617,15 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
 // kIdx: final_idx is written (the autograd forward); the render paths launch
 // the kIdx = false instance, which tracks no indices.
 template <int kMode, bool kIdx>
-__global__ __launch_bounds__(kMode == kModeSparse || kMode == kModeSparseStamp ? 64 : 128, 8) void
+__global__ __launch_bounds__(kMode == kModeSparse || kMode == kModeSparseStamp || kMode == kModeSparsePrio ? 64 : 128, 8) void
 raster_sum_fwd_kernel(SumFwdArgs A) {
-    constexpr bool kOneWave = kMode == kModeSparse || kMode == kModeSparseStamp;
+    constexpr bool kOneWave = kMode == kModeSparse || kMode == kModeSparseStamp || kMode == kModeSparsePrio;
     __shared__ float4 s_buf[kOneWave ? 1 : 2][kSlice];
     __shared__ int s_ids[kOneWave ? 1 : 2][kTilePix];
+    // raised wave priority over the staging (loads, ranking, lists): the
+    // arbiter favours older waves, so a young wave would otherwise wait behind
+    // its elders' blending to issue its round trips (train.hip, same reason)
+    if (kMode == kModeSparsePrio) __builtin_amdgcn_s_setprio(3);
     const int w = kOneWave ? 0 : (threadIdx.x >> 6);
     int tile = xcd_remap(blockIdx.x, A.ntiles * A.frames);
     if (A.frames > 1) {  // batched frames: this block's frame and tile
@@ -681,7 +689,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
     }
     const int ty = tile / A.tbx;
     if (kMode == kModeSparseStamp && threadIdx.x == 0) A.stamps[4 * (size_t)tile] = t0;
-    const bool sparse = kMode == kModeSparse || kMode == kModeSparseStamp ||
+    const bool sparse = kMode == kModeSparse || kMode == kModeSparseStamp || kMode == kModeSparsePrio ||
                         ((kMode == kModeAdaptive || kMode == kModeStamp) && n <= A.sparse_max);
     if (n == 0) seg_rec = nullptr;
     const bool by_ids = A.sort_ids && !seg_rec;  // ids sorted into s_ids first
@@ -923,8 +931,14 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
     const dim3 grid(ntiles * A.frames);
     switch (mode) {
         case kModeSparse:
-            launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeSparse, true> : raster_sum_fwd_kernel<kModeSparse, false>, grid,
-                       dim3(64), s, tev, A);
+            if (g_knobs[17] == 1)
+                launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeSparsePrio, true>
+                                       : raster_sum_fwd_kernel<kModeSparsePrio, false>,
+                           grid, dim3(64), s, tev, A);
+            else
+                launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeSparse, true>
+                                       : raster_sum_fwd_kernel<kModeSparse, false>,
+                           grid, dim3(64), s, tev, A);
             break;
         case kModeBanded:
             launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeBanded, true> : raster_sum_fwd_kernel<kModeBanded, false>, grid,

@@ -65,6 +65,7 @@ struct TrainTileArgs {
     const int *det_off;
     float4 *det_part;
     long long det_cap;
+    int prio;  // A/B knob 16: raise the wave priority over the order phase (s_setprio)
 };
 
 __device__ __forceinline__ float clamp_unit(float x) {
@@ -611,9 +612,19 @@ struct BandLds {
     int misc[4];   // the waves' error sums
 };
 
-template <bool kStamp>
+// kDet: GSVC_TRAIN_DETERMINISTIC's slot stores in place of the atomics (its
+// own instantiation: the slot arithmetic in the flush would cost the atomic
+// kernel two spilled VGPRs)
+template <bool kStamp, bool kDet = false>
 __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTileArgs A) {
     __shared__ BandLds S;
+    // Wave issue priority: the arbiter favours older waves, so without it a
+    // workgroup dispatched late onto a busy CU waits behind its elders' blending
+    // before it can even issue its loads and ranking (stamps: the order phase
+    // grows from 2.6 us for the first workgroups of a CU to 11.7 us for its
+    // 13th-16th, profiles/r03/stamps).  Raised over the order phase, a young
+    // tile gets its round trips going while its elders compute.
+    if (A.prio) __builtin_amdgcn_s_setprio(3);
     const int tile = xcd_remap(blockIdx.x, A.ntiles);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     long long *st = kStamp ? A.stamps + 8 * (size_t)tile : nullptr;
@@ -699,6 +710,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
         }
     }
     __syncthreads();
+    if (A.prio) __builtin_amdgcn_s_setprio(0);
     if (kStamp && tid == 0) st[1] = tstamp();
 
     // 2. forward: this wave's band against the entries that can reach it
@@ -1054,7 +1066,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
         __syncthreads();
         // 8 lanes per entry add the entry's sums (band 0 + band 1) into the
         // splat's gradient record
-        if (A.det_off) {
+        if (kDet) {
             // deterministic: one 32-byte partial per (splat, tile) at the tile's
             // place in the splat's bbox; the splat kernel sums them in bbox order
             for (int q = tid; q < gn * 8; q += kBThreads) {
@@ -1437,6 +1449,7 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     T.spec = g_knobs[12] > 0 && g_knobs[12] <= 64 ? g_knobs[12] : kBSpec;
     T.diag = g_knobs[13];
     T.grouped = g_knobs[14] != 1;
+    T.prio = g_knobs[16] >= 0 && g_knobs[16] <= 3 ? g_knobs[16] : 0;
     T.det_off = det_off;
     T.det_part = det_part;
     T.det_cap = det_capacity;
@@ -1453,6 +1466,8 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
         const int tslot = timing_begin(s, tev, kTimingTrainTile);
         if (g_knobs[8] == 1 && !det)
             launch_timed(train_tile_kernel<false>, dim3(ntiles), dim3(kT), 0, s, tev, T);
+        else if (det)
+            launch_timed(train_tile_band_kernel<false, true>, dim3(ntiles), dim3(kBThreads), 0, s, tev, T);
         else
             launch_timed(train_tile_band_kernel<false>, dim3(ntiles), dim3(kBThreads), 0, s, tev, T);
         timing_end(s, tslot, kTimingTrainTile);
