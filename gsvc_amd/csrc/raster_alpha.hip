@@ -12,7 +12,8 @@
 // entry of the tile is visited (no 256 cap); out = acc + T * background.
 //
 // Forward: one wave64 per tile, 4 pixels per lane (as the sum forward), the
-// wave leaves the tile when every lane's 4 pixels are done.
+// wave leaves the tile when every lane's 4 pixels are done; chunks of more
+// than 24 entries are walked through lane-group lists (cull.h).
 // Backward: the transmittance recursion runs per pixel from the back, so it
 // is PIXEL-parallel: 256 threads = 256 pixels; per entry each wave sums its 9
 // partial gradients per 16-lane row with DPP adds (4 VALU each, no LDS
@@ -20,27 +21,75 @@
 // atomics (16 rows), and once per 256-entry chunk the tile's records go to HBM
 // as one 64-byte atomic request per (splat, tile).
 #include "common.h"
+#include "cull.h"
 
 namespace gsvc {
 
 constexpr int kAChunk = 64;
+// A chunk of more than this many entries is walked through lane-group lists
+// (as the sum composite's sparse path, raster_sum.hip): each group of 4 lanes
+// owns a 4x4-pixel block and visits, in order, only the entries whose
+// alpha >= 1/255 ellipse box reaches it (cull.h ellipse_blocks); fewer entries
+// are walked by every lane (the lists would cost more than they skip).
+constexpr int kAGroupMin = 24;
+
+// One entry against a lane's 4 pixels: forward.cu:323-357 (front to back,
+// alpha clamped at 0.999, stop at next_T <= 1e-4 without blending that entry).
+__device__ __forceinline__ void alpha_blend4(float4 G, float4 C, float blu, float py, int pj, int k,
+                                             float (&T)[4], float (&ar)[4], float (&ag)[4],
+                                             float (&ab)[4], int (&last)[4], bool (&done)[4]) {
+    const float dy = G.y - py;
+    const float cq = (C.x * dy) * dy;
+    const float bdy = G.w * dy;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (done[q]) continue;
+        const float dx = G.x - (float)(pj + q);
+        const float s = fmaf(fmaf(G.z, dx, bdy), dx, cq);
+        const float al = fminf(0.999f, C.y * exp_neg(s));
+        if (s < 0.0f || al < kAlphaMin) continue;
+        const float next_T = T[q] * (1.0f - al);
+        if (next_T <= 1e-4f) {
+            done[q] = true;
+            continue;
+        }
+        const float vis = al * T[q];
+        ar[q] = fmaf(C.z, vis, ar[q]);
+        ag[q] = fmaf(C.w, vis, ag[q]);
+        ab[q] = fmaf(blu, vis, ab[q]);
+        T[q] = next_T;
+        last[q] = k;
+    }
+}
 
 __global__ __launch_bounds__(64) void raster_alpha_fwd_kernel(
     int tbx, int img_w, int img_h, int ntiles, const int *__restrict__ ids,
     const int2 *__restrict__ bins, const float2 *__restrict__ xys, const float *__restrict__ conics,
     const float *__restrict__ colors, const float *__restrict__ opac, const float *__restrict__ bg,
-    float *__restrict__ out, float *__restrict__ final_Ts, int *__restrict__ final_idx) {
-    __shared__ float4 s_geo[kAChunk];  // x, y, 0.5a, b
-    __shared__ float4 s_col[kAChunk];  // 0.5c, opacity, r, g
-    __shared__ float s_blu[kAChunk];
+    float *__restrict__ out, float *__restrict__ final_Ts, int *__restrict__ final_idx,
+    int group_min) {
+    // staged entries (slot kAChunk: the lists' no-op sentinel, sigma = +inf),
+    // their 4x4 blocks and the 16 groups' lists [iteration][group]
+    __shared__ float4 s_geo[kAChunk + 1];  // x, y, 0.5a, b
+    __shared__ float4 s_col[kAChunk + 1];  // 0.5c, opacity, r, g
+    __shared__ float s_blu[kAChunk + 1];
+    __shared__ unsigned short s_gm[kAChunk];
+    __shared__ uint4 s_list4[kAChunk];     // 16 bytes per iteration
+    unsigned char *s_list = reinterpret_cast<unsigned char *>(s_list4);
     const int tile = xcd_remap(blockIdx.x, ntiles);
     const int ty = tile / tbx, tx = tile - ty * tbx;
     const int lane = threadIdx.x;
     const int pi = ty * kTile + (lane >> 2);
     const int pj = tx * kTile + ((lane & 3) << 2);
     const float py = (float)pi;
+    const float ox = (float)(tx * kTile), oy = (float)(ty * kTile);
     const int2 range = bins[tile];
     const int n = max(range.y - range.x, 0);
+    if (lane == 0) {
+        s_geo[kAChunk] = make_float4(0.0f, 1e30f, 0.0f, 0.0f);
+        s_col[kAChunk] = make_float4(1e30f, 1.0f, 0.0f, 0.0f);
+        s_blu[kAChunk] = 0.0f;
+    }
 
     float T[4] = {1.f, 1.f, 1.f, 1.f};
     float ar[4] = {0.f, 0.f, 0.f, 0.f}, ag[4] = {0.f, 0.f, 0.f, 0.f}, ab[4] = {0.f, 0.f, 0.f, 0.f};
@@ -52,41 +101,43 @@ __global__ __launch_bounds__(64) void raster_alpha_fwd_kernel(
     for (int base = 0; base < n; base += kAChunk) {
         if (__all(done[0] && done[1] && done[2] && done[3])) break;
         const int cnt = min(kAChunk, n - base);
+        const bool grouped = cnt > group_min;
         if (lane < cnt) {
             const int g = ids[range.x + base + lane];
             const float2 xy = xys[g];
             const float a = conics[3 * g], b = conics[3 * g + 1], c = conics[3 * g + 2];
+            const float o = opac[g];
             s_geo[lane] = make_float4(xy.x, xy.y, 0.5f * a, b);
-            s_col[lane] = make_float4(0.5f * c, opac[g], colors[3 * g], colors[3 * g + 1]);
+            s_col[lane] = make_float4(0.5f * c, o, colors[3 * g], colors[3 * g + 1]);
             s_blu[lane] = colors[3 * g + 2];
+            if (grouped) s_gm[lane] = (unsigned short)ellipse_blocks<16>(xy.x, xy.y, a, b, c, o, ox, oy);
         }
         __syncthreads();
-        for (int t = 0; t < cnt; ++t) {
-            const float4 G = s_geo[t];
-            const float4 C = s_col[t];
-            const float dy = G.y - py;
-            const float cq = (C.x * dy) * dy;
-            const float bdy = G.w * dy;
-            const int k = range.x + base + t;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (done[q]) continue;
-                const float dx = G.x - (float)(pj + q);
-                const float s = fmaf(fmaf(G.z, dx, bdy), dx, cq);
-                const float al = fminf(0.999f, C.y * exp_neg(s));
-                if (s < 0.0f || al < kAlphaMin) continue;
-                const float next_T = T[q] * (1.0f - al);
-                if (next_T <= 1e-4f) {
-                    done[q] = true;
-                    continue;
-                }
-                const float vis = al * T[q];
-                ar[q] = fmaf(C.z, vis, ar[q]);
-                ag[q] = fmaf(C.w, vis, ag[q]);
-                ab[q] = fmaf(s_blu[t], vis, ab[q]);
-                T[q] = next_T;
-                last[q] = k;
-            }
+        const int k0 = range.x + base;
+        if (!grouped) {
+            for (int t = 0; t < cnt; ++t)
+                alpha_blend4(s_geo[t], s_col[t], s_blu[t], py, pj, k0 + t, T, ar, ag, ab, last, done);
+            __syncthreads();
+            continue;
+        }
+        // lists: row `it` of the 16 groups' lists, padded with the sentinel
+        const unsigned gmt = lane < cnt ? s_gm[lane] : 0u;
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        s_list4[lane] = make_uint4(0x40404040u, 0x40404040u, 0x40404040u, 0x40404040u);
+        __syncthreads();
+        int maxlen = 0;
+#pragma unroll 1
+        for (int gr = 0; gr < 16; ++gr) {
+            const bool in = (gmt >> gr) & 1u;
+            const unsigned long long mg = __ballot(in);
+            if (in) s_list[16 * __popcll(mg & lt) + gr] = (unsigned char)lane;
+            maxlen = max(maxlen, __popcll(mg));
+        }
+        __syncthreads();
+        const unsigned char *ml = s_list + (((lane >> 4) << 2) | (lane & 3));
+        for (int it = 0; it < maxlen; ++it) {
+            const int t = ml[16 * it];
+            alpha_blend4(s_geo[t], s_col[t], s_blu[t], py, pj, k0 + t, T, ar, ag, ab, last, done);
         }
         __syncthreads();
     }
@@ -277,7 +328,9 @@ extern "C" int gsvc_rasterize_forward(int tbx, int tby, int tbz, int block_x, in
     hipLaunchKernelGGL(raster_alpha_fwd_kernel, dim3(ntiles), dim3(64), 0, (hipStream_t)stream, tbx,
                        (int)img_width, (int)img_height, ntiles, gaussian_ids_sorted,
                        (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacities,
-                       background, out_img, final_Ts, final_idx);
+                       background, out_img, final_Ts, final_idx,
+                       // A/B knob 18 = v > 0: list threshold v - 1
+                       g_knobs[18] > 0 ? g_knobs[18] - 1 : kAGroupMin);
     return check_launch("rasterize_forward");
 }
 

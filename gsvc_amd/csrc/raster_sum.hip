@@ -38,6 +38,7 @@
 // request per entry instead of the reference's 9 per warp).
 #include <hip/hip_ext.h>
 
+#include "cull.h"
 #include "det.h"
 #include "frame.h"
 #include "raster_sum.h"
@@ -138,38 +139,6 @@ __device__ __forceinline__ bool ellipse_hits_rect(float x, float y, float a, flo
     const float ex = sqrtf(S2 * c / det) * 1.001f + 0.01f;
     const float ey = sqrtf(S2 * a / det) * 1.001f + 0.01f;
     return (x + ex >= x0) && (x - ex <= x1) && (y + ey >= y0) && (y - ey <= y1);
-}
-
-// The 4x4-pixel blocks of the kRows-row strip at (bx0, by0) (bit 4 * r + c:
-// rows by0 + 4r .. + 3, columns bx0 + 4c .. + 3) that splat (x, y, conic, o)
-// can reach with alpha >= 1/255 -- ellipse_hits_rect's test per block, so a
-// block left out holds no contributing pixel centre.  kRows = 8: a band, 16:
-// the whole tile.
-template <int kRows>
-__device__ __forceinline__ unsigned ellipse_blocks(float x, float y, float a, float b, float c,
-                                                   float o, float bx0, float by0) {
-    constexpr unsigned kAll = (1u << kRows) - 1u;  // kRows / 4 row blocks x 4 column blocks
-    if (!(o > 0.0f)) return (o <= 0.0f) ? 0u : kAll;  // o <= 0: never valid; NaN: keep
-    const float det = a * c - b * b;
-    if (!(a > 0.0f) || !(det > 0.0f) || !(o < 3.0e38f) || !(fabsf(x) < 1e30f) || !(fabsf(y) < 1e30f))
-        return kAll;  // not positive definite / non-finite: no culling
-    const float lg = __logf(255.0f * o);
-    if (lg < -0.01f) return 0u;  // o < e^-0.01 / 255: alpha < 1/255 everywhere
-    const float S2 = 2.0f * (lg * 1.001f + 0.01f);
-    const float ex = sqrtf(S2 * c / det) * 1.001f + 0.01f;
-    const float ey = sqrtf(S2 * a / det) * 1.001f + 0.01f;
-    // in strip coordinates, so the block bounds are literals (the origin
-    // shift rounds by < 2^-12 px at 1080p, far inside the 0.01 px margin)
-    const float u = x - bx0, v = y - by0;
-    unsigned cols = 0u;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        cols |= ((u + ex >= 4.0f * k) && (u - ex <= 4.0f * k + 3.0f)) ? 1u << k : 0u;
-    unsigned m = 0u;
-#pragma unroll
-    for (int r = 0; r < kRows / 4; ++r)
-        m |= ((v + ey >= 4.0f * r) && (v - ey <= 4.0f * r + 3.0f)) ? cols << (4 * r) : 0u;
-    return m;
 }
 
 typedef float v4f __attribute__((ext_vector_type(4)));

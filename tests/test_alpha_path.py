@@ -82,13 +82,14 @@ def test_alpha_dense_golden(cuda, name):
         assert N(Ts).min() > 0.4
 
 
-@pytest.mark.parametrize("n", [10000])
-def test_alpha_1080p_oracle(cuda, oracle, n):
-    """Full 1080p frame against the C restatement, forward and backward."""
+@pytest.mark.parametrize("n,chol", [(10000, 1.0), (30000, 4.0)])
+def test_alpha_1080p_oracle(cuda, oracle, n, chol):
+    """Full 1080p frame against the C restatement, forward and backward; the
+    dense case (~40-60 entries per tile) walks the forward's lane-group lists."""
     from gsvc_amd import ops
     H, W = 1080, 1920
     tb = _tb(H, W)
-    means, L, colors, _ = oracle.synthetic_frame(n, seed=n + 17)
+    means, L, colors, _ = oracle.synthetic_frame(n, seed=n + 17, chol_scale=chol)
     opac = np.random.default_rng(n).uniform(0.2, 1.0, (n, 1)).astype(np.float32)
     bg = np.array([0.1, 0.4, 0.7], np.float32)
     ref = oracle.render_sum(means, L, colors, opac, H, W)  # projection + sorted bins
@@ -96,6 +97,9 @@ def test_alpha_1080p_oracle(cuda, oracle, n):
                                                                       0.01)
     gids, bins, _ = ops.bin_and_sort_tiles(n, ref["m"], xys, depths, radii, T(ref["cum"]), tb)
     np.testing.assert_array_equal(N(gids), ref["gids_sorted"])
+    counts = ref["bins"][: tb[0] * tb[1], 1] - ref["bins"][: tb[0] * tb[1], 0]
+    if chol > 1.0:
+        assert (counts > 24).mean() > 0.5  # most tiles take the grouped lists
     out, Ts, idx = ops.rasterize_forward(tb, (16, 16, 1), (W, H, 1), gids, bins, xys, conics,
                                          T(colors), T(opac), T(bg))
     r_out, r_Ts, r_idx = oracle.raster_forward(tb, H, W, ref["gids_sorted"], ref["bins"], ref["xys"],
