@@ -500,7 +500,7 @@ def main():
         render_ranks = {"workload": "GaussianVideoFrame.forward of each rank's trained 1920x1080 "
                                     f"frame, {args.splats} splats, 200 frames per rank",
                         "frames_per_s": round(world * 200 / rel, 1),
-                        "ms_per_frame": round(1e3 * rel / 200, 4), "n_gpus": world}
+                        "ms_per_frame": round(1e3 * rel / 200, 4), "ranks": world}
     if rank != 0:
         if world > 1:
             import torch.distributed as dist
@@ -525,8 +525,12 @@ def main():
         "train_splat": roofline("train_splat_kernel", train_splat_bytes(args.splats),
                                 kt["train_splat"], prof, "train_splat"),
     }
+    # GSVC_BENCH_SHARED_GPU (a rehearsal of N ranks on one GPU): the devices
+    # used, not the ranks, are the GPU count
+    shared = os.environ.get("GSVC_BENCH_SHARED_GPU") == "1" and args.backend != "nccl"
+    n_gpus = 1 if shared else world
     line = {
-        "metric": METRIC, "value": round(value, 2), "unit": "train-iters/s", "n_gpus": world,
+        "metric": METRIC, "value": round(value, 2), "unit": "train-iters/s", "n_gpus": n_gpus,
         "steps": args.steps, "warmup": args.warmup, "settle_iters": args.settle,
         "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
@@ -537,7 +541,9 @@ def main():
                                f"{args.splats} splats (GaussianVideoFrame.train_iter = forward + "
                                "L2 + backward + PSNR .item() + Adan + zero_grad + StepLR)",
                    "H": H, "W": W, "splats": args.splats,
-                   "parallelism": f"one frame per rank, {world} rank(s), no data-path collective"},
+                   "parallelism": f"one frame per rank, {world} rank(s), no data-path collective"
+                                  + (f", all ranks sharing one GPU" if shared else "")},
+        "ranks_per_gpu": world if shared else 1,
         "roofline": roof,
         "kernels": kernels,
         "shape": shape,

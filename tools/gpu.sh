@@ -12,6 +12,7 @@
 #                                      (tools/pmc_workloads.py) -> pmc_traffic.json
 #   pmc_valu TAG                       VALU / LDS / SALU / VMEM instruction counts of
 #                                      the trained composite and training tile kernel
+#   pmc_sq TAG                         SQ busy / wait / LDS-conflict cycles of the same
 #   ablate TAG "bits" [tbench args]    training tile kernel diagnostic bits (knob 13)
 #                                      on frozen trained-density steps
 #   fbench_ab TAG [fbench args]        composite A/B by fbench + kernel trace
@@ -82,6 +83,22 @@ for r in csv.DictReader(open(f)):
         if key in r["Kernel_Name"]:
             by[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
 print(json.dumps({k: {c: round(sum(v[-50:]) / len(v[-50:])) for c, v in d.items()} for k, d in by.items()}))
+PY
+  ;;
+pmc_sq)
+  # where the tile kernels' cycles go: two SQ passes over the trained workload
+  pmc sqa SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES -- python3 tools/pmc_workloads.py train50k
+  pmc sqb SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INSTS_SMEM -- python3 tools/pmc_workloads.py train50k
+  python3 - "$OUT" <<'PY'
+import csv, glob, sys, json, collections
+by = collections.defaultdict(lambda: collections.defaultdict(list))
+for sub in ("sqa", "sqb"):
+    f = glob.glob(f"{sys.argv[1]}/{sub}/**/*counter_collection.csv", recursive=True)[0]
+    for r in csv.DictReader(open(f)):
+        for key in ("raster_sum_fwd", "train_tile_band", "frame_project", "train_splat"):
+            if key in r["Kernel_Name"]:
+                by[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+print(json.dumps({k: {c: round(sum(v[-50:]) / len(v[-50:])) for c, v in d.items()} for k, d in by.items()}, indent=1))
 PY
   ;;
 ablate)
