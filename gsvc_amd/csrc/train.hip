@@ -65,7 +65,7 @@ struct TrainTileArgs {
     const int *det_off;
     float4 *det_part;
     long long det_cap;
-    int prio;  // A/B knob 16: raise the wave priority over the order phase (s_setprio)
+    int prio;  // raise the wave priority over the order phase (s_setprio; knob 16 = 1 off)
 };
 
 __device__ __forceinline__ float clamp_unit(float x) {
@@ -1449,7 +1449,7 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     T.spec = g_knobs[12] > 0 && g_knobs[12] <= 64 ? g_knobs[12] : kBSpec;
     T.diag = g_knobs[13];
     T.grouped = g_knobs[14] != 1;
-    T.prio = g_knobs[16] >= 0 && g_knobs[16] <= 3 ? g_knobs[16] : 0;
+    T.prio = g_knobs[16] != 1;  // A/B knob 16 = 1: no raised priority
     T.det_off = det_off;
     T.det_part = det_part;
     T.det_cap = det_capacity;

@@ -34,13 +34,21 @@ DET_CAPACITY_PER_SPLAT = 8  # first det_capacity guess: M / N is ~2.5 at init, ~
 PROJECT_AHEAD = True  # a bound step enqueues the next step's projection after itself
 
 # A step's projection of the NEXT frame is used only if nothing could have
-# changed the parameters since: no other fused launch anywhere (_launch_count),
-# no optimizer step or control of ours (_param_epoch, bump_param_epoch), no
-# in-place op through the bound Parameters (their _version), the same bound
-# step and workspace frame.  (In-place writes through ``.data`` bypass
-# _version; call bump_param_epoch() after such writes.)
-_launch_count = [0]
+# changed the parameters since: no other fused launch on the same parameters
+# (_param_launches, keyed by the xyz storage: another model's launches on
+# another stream no longer void it), no optimizer step or control of ours
+# (_param_epoch, bump_param_epoch), no in-place op through the bound Parameters
+# (their _version), the same bound step and workspace frame (a launch of any
+# model on the same workspace advances its frame).  (In-place writes through
+# ``.data`` bypass _version; call bump_param_epoch() after such writes.)
+_param_launches = {}
 _param_epoch = [0]
+
+
+def _note_launch(xyz_ptr: int) -> int:
+    n = _param_launches.get(xyz_ptr, 0) + 1
+    _param_launches[xyz_ptr] = n
+    return n
 
 
 def bump_param_epoch() -> None:
@@ -258,7 +266,7 @@ class BoundStep:
             versions = tuple(t._version for t in self.params)
             pend = ws.pending
             ahead = (pend is not None and pend[0]() is self and pend[1] == ws.frame
-                     and pend[2] == _launch_count[0] and pend[3] == _param_epoch[0]
+                     and pend[2] == _param_launches.get(a.xyz, 0) and pend[3] == _param_epoch[0]
                      and pend[4] == versions)
             if pend is not None and not ahead:
                 # an enqueued projection that cannot be used: its counts are in
@@ -270,10 +278,9 @@ class BoundStep:
             flags |= TRAIN_PROJECTED | TRAIN_PROJECT_NEXT
         self.seq = ((ws.frame + 1) & 0xFFFFFFFF) | 0x80000000
         self._call(ws, lib, gt, flags | ws.order_flags())
-        _launch_count[0] += 1
+        launches = _note_launch(a.xyz)
         if PROJECT_AHEAD:
-            ws.pending = (weakref.ref(self), ws.frame + 1, _launch_count[0], _param_epoch[0],
-                          versions)
+            ws.pending = (weakref.ref(self), ws.frame + 1, launches, _param_epoch[0], versions)
         ws.frame += 1
 
     def _call(self, ws, lib, gt, flags):
@@ -345,7 +352,7 @@ def train_step_sum(xyz: Tensor, cholesky: Tensor, features: Tensor, rgb_w: Optio
     if ws.pending is not None:  # a bound step's projection ahead: not for this call
         ws.dirty = True
         ws = _workspace(dev, n, H, W)
-    _launch_count[0] += 1
+    _note_launch(p_xyz)
     loss = torch.empty((2,), dtype=torch.float32, device=dev)
     a = _StepArgs()
     a.num_points, a.xyz, a.cholesky, a.cholesky_bound = n, p_xyz, p_chol, p_bound
