@@ -68,6 +68,8 @@ def parse():
                          "run at a trained splat density, not at random init")
     ap.add_argument("--timing-launches", type=int, default=200,
                     help="launches per kernel timed by HIP events after the timed region")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="torch.use_deterministic_algorithms(True): the bitwise reproducible backward")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--knob", action="append", default=[],
@@ -448,6 +450,8 @@ def main():
             k, v = kv.split("=")
             _lib.load().gsvc_debug_set(int(k), int(v))
 
+    if args.deterministic:
+        torch.use_deterministic_algorithms(True, warn_only=True)
     # ---- headline: configs[2] training iterations, one frame per rank
     model = make_frame_model(H, W, args.splats, device, seed=1000 + rank)
     gt = synthetic_gt(H, W, 8 + rank, "cpu").to(device)
@@ -541,6 +545,7 @@ def main():
                                f"{args.splats} splats (GaussianVideoFrame.train_iter = forward + "
                                "L2 + backward + PSNR .item() + Adan + zero_grad + StepLR)",
                    "H": H, "W": W, "splats": args.splats,
+                   "deterministic_backward": bool(args.deterministic),
                    "parallelism": f"one frame per rank, {world} rank(s), no data-path collective"
                                   + (f", all ranks sharing one GPU" if shared else "")},
         "ranks_per_gpu": world if shared else 1,

@@ -68,10 +68,17 @@ FrameSlots frame_slots(const FrameWs &w, int ntiles, int frame_index);
 // identity) and the workgroup aggregates its slot atomics per tile (the same
 // entries per tile); ord->key / key_id (optional): every splat's strip key and
 // id, the input of the next order's sort (frame.hip strip_key).
+// carry_ids (optional, the training step's carried bins, train.hip): the
+// insertion writes splat ids into carry_ids[T][256] counted in carry_counts
+// instead of records into the slab, and every splat's tile box into
+// carry_box and carry_hull.
 struct SplatOrder {
     const int *order = nullptr;
     unsigned *key = nullptr;
     int *key_id = nullptr;
+    int *carry_ids = nullptr;
+    unsigned *carry_counts = nullptr;
+    uint2 *carry_box = nullptr, *carry_hull = nullptr;
 };
 int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *chol,
                          const float *chol_bound, const float *feat, const float *rgb_w,

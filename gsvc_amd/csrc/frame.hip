@@ -182,7 +182,8 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_ordered_kernel(
     float2 *__restrict__ xys, int *__restrict__ radii, float4 *__restrict__ rec,
     unsigned *__restrict__ counts, float4 *__restrict__ slab, int *__restrict__ m_acc,
     int *__restrict__ m_clear, float4 *__restrict__ grad_zero, unsigned *__restrict__ key,
-    int *__restrict__ key_id, unsigned key_invisible, long long *stamps) {
+    int *__restrict__ key_id, unsigned key_invisible, long long *stamps,
+    int *__restrict__ carry_ids, uint2 *__restrict__ carry_box, uint2 *__restrict__ carry_hull) {
     __shared__ int s_hits[kProjThreads / 64];
     __shared__ unsigned s_cnt[kAggWin];
     __shared__ int s_box[4][kProjThreads / 64];
@@ -213,9 +214,11 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_ordered_kernel(
             key_id[i] = i;
         }
         if (S.P.rad > 0) tile_bbox(S.P.xy.x, S.P.xy.y, (float)S.P.rad, tbx, tby, x0, y0, x1, y1);
+        if (carry_ids) carry_box[i] = carry_hull[i] = pack_box(x0, y0, x1, y1);
     }
     if (kStamp && lane == 0) st[1] = proj_stamp();
-    const int hits = slab_insert_window(S, x0, y0, x1, y1, tbx, tby, counts, slab, s_cnt, s_box, st);
+    const int hits = slab_insert_window(S, x0, y0, x1, y1, tbx, tby, counts, slab, s_cnt, s_box, st,
+                                        carry_ids);
     if (kStamp) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) st[2] = proj_stamp();
@@ -302,17 +305,21 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
         if (g_knobs[5] == 1 && g_debug_ptr) {  // diagnostic: per-wave stamps
             hipLaunchKernelGGL(frame_project_ordered_kernel<true>, grid, dim3(kProjThreads), 0, s, n,
                                ord->order, xyz, xyz_tanh, chol, chol_bound, feat, rgb_w, opac, hw,
-                               hh, tbx, tby, w.xys, w.radii, w.rec, f.counts, w.slab, f.m_acc,
+                               hh, tbx, tby, w.xys, w.radii, w.rec,
+                               ord->carry_ids ? ord->carry_counts : f.counts, w.slab, f.m_acc,
                                f.m_clear, grad_zero, ord->key, ord->key_id, strip_key_invisible(tbx, tby),
-                               reinterpret_cast<long long *>(g_debug_ptr));
+                               reinterpret_cast<long long *>(g_debug_ptr), ord->carry_ids,
+                               ord->carry_box, ord->carry_hull);
             return check_launch("frame projection (ordered)");
         }
         hipEvent_t tev[2];
         const int tslot = timing_begin(s, tev, kTimingProject);
         launch_timed(frame_project_ordered_kernel<false>, grid, dim3(kProjThreads), 0, s, tev, n,
                      ord->order, xyz, xyz_tanh, chol, chol_bound, feat, rgb_w, opac, hw, hh, tbx,
-                     tby, w.xys, w.radii, w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero,
-                     ord->key, ord->key_id, strip_key_invisible(tbx, tby), (long long *)nullptr);
+                     tby, w.xys, w.radii, w.rec, ord->carry_ids ? ord->carry_counts : f.counts,
+                     w.slab, f.m_acc, f.m_clear, grad_zero, ord->key, ord->key_id,
+                     strip_key_invisible(tbx, tby), (long long *)nullptr, ord->carry_ids,
+                     ord->carry_box, ord->carry_hull);
         timing_end(s, tslot, kTimingProject);
         return check_launch("frame projection (ordered)");
     }

@@ -18,11 +18,14 @@ constexpr int kProjThreads = 256;
 // (trained-like 1080p / 50k splats: 794k insertions).  kB slot atomics are
 // generated (unrolled, register-resident), issued, and only then waited for:
 // one round trip per kB of them.
+// ``ids`` (optional, the training step's carried bins): the splat's id into
+// ids[tile][slot] instead of its record into the slab.
 template <int kB>
 __device__ __forceinline__ int slab_insert_pairs(float cx, float cy, int r, int tbx, int tby,
                                                  float4 r0, float4 r1, float4 r2,
                                                  unsigned *__restrict__ counts,
-                                                 float4 *__restrict__ slab, int wt) {
+                                                 float4 *__restrict__ slab, int wt,
+                                                 int *__restrict__ ids = nullptr) {
     unsigned x0, y0, x1, y1;
     tile_bbox(cx, cy, (float)r, tbx, tby, x0, y0, x1, y1);
     if (x1 <= x0 || y1 <= y0) return 0;
@@ -30,7 +33,9 @@ __device__ __forceinline__ int slab_insert_pairs(float cx, float cy, int r, int 
     const bool wide = x1 - x0 >= 3;  // narrow rows: single atomics (measured faster at 10k)
     const int ntiles = tbx * tby;
     auto put = [&](unsigned t, unsigned sl) {
-        if (sl < (unsigned)kTilePix) {
+        if (sl < (unsigned)kTilePix && ids) {
+            ids[(size_t)t * kTilePix + sl] = __float_as_int(r2.y);
+        } else if (sl < (unsigned)kTilePix) {
             float4 *d = slab_rec(slab, ntiles, (int)t, (int)sl);
             d[0] = r0;
             d[1] = r1;
@@ -82,6 +87,15 @@ __device__ __forceinline__ int slab_insert_pairs(float cx, float cy, int r, int 
         }
     }
     return hits;
+}
+
+// A tile box [x0, x1) x [y0, y1) in two words (x0 | y0 << 16, x1 | y1 << 16);
+// {0, 0}: empty.  The carried bins' per-splat boxes (train.hip).
+__device__ __forceinline__ uint2 pack_box(unsigned x0, unsigned y0, unsigned x1, unsigned y1) {
+    return (x1 > x0 && y1 > y0) ? make_uint2(x0 | (y0 << 16), x1 | (y1 << 16)) : make_uint2(0u, 0u);
+}
+__device__ __forceinline__ bool box_has(uint2 b, unsigned tx, unsigned ty) {
+    return tx >= (b.x & 0xffffu) && tx < (b.y & 0xffffu) && ty >= (b.x >> 16) && ty < (b.y >> 16);
 }
 
 // Activations (GaussianSplats_Represent.py:57-70) + projection of splat i and
@@ -179,7 +193,8 @@ __device__ __forceinline__ int slab_insert_window(const SplatOut &S, unsigned x0
                                                   unsigned *__restrict__ counts,
                                                   float4 *__restrict__ slab, unsigned *s_cnt,
                                                   int (*s_box)[kProjThreads / 64],
-                                                  long long *st = nullptr) {
+                                                  long long *st = nullptr,
+                                                  int *__restrict__ ids = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     // diagnostic (st != NULL): s_memrealtime per wave after each phase
     auto mark = [&](int k) {
@@ -222,7 +237,7 @@ __device__ __forceinline__ int slab_insert_window(const SplatOut &S, unsigned x0
     int hits = 0;
     if (vis && !(agg && small))
         hits = slab_insert_pairs<8>(S.P.xy.x, S.P.xy.y, S.P.rad, tbx, tby, S.r0, S.r1, S.r2,
-                                    counts, slab, 0);
+                                    counts, slab, 0, ids);
     if (agg) {
         const int cells = ww * wh;
         for (int c = tid; c < cells; c += kProjThreads) s_cnt[c] = 0u;
@@ -249,8 +264,11 @@ __device__ __forceinline__ int slab_insert_window(const SplatOut &S, unsigned x0
             for (unsigned y = y0; y < y1; ++y)
                 for (unsigned x = x0; x < x1; ++x) {
                     const unsigned sl = atomicAdd(&s_cnt[((int)y - by0) * ww + ((int)x - bx0)], 1u);
-                    if (sl < (unsigned)kTilePix) {
-                        float4 *d = slab_rec(slab, ntiles, (int)(y * (unsigned)tbx + x), (int)sl);
+                    const int tl = (int)(y * (unsigned)tbx + x);
+                    if (sl < (unsigned)kTilePix && ids) {
+                        ids[(size_t)tl * kTilePix + sl] = __float_as_int(S.r2.y);
+                    } else if (sl < (unsigned)kTilePix) {
+                        float4 *d = slab_rec(slab, ntiles, tl, (int)sl);
                         d[0] = S.r0;
                         d[1] = S.r1;
                         d[2] = S.r2;

@@ -28,6 +28,7 @@
 #include "adan.h"
 #include "binning.h"
 #include "frame.h"
+#include "frame_dev.h"
 #include "det.h"
 #include "tile_ids.h"
 
@@ -66,6 +67,21 @@ struct TrainTileArgs {
     float4 *det_part;
     long long det_cap;
     int prio;  // raise the wave priority over the order phase (s_setprio; knob 16 = 1 off)
+    // GSVC_TRAIN_CARRY (band kernel): the tile's candidates are the splat ids
+    // cids[tile][0, counts[tile]) -- a superset of its entries carried from
+    // step to step (train_splat_kernel) -- and an entry is a candidate whose
+    // current tile box cbox[id] holds the tile; records come from rec by id.
+    // m_clear: the next frame's M slot (zeroed here; the splat kernel fills it)
+    const int *cids;
+    const uint2 *cbox;
+    int *m_clear;
+    // loss != NULL (band kernel): one extra workgroup (the last, blockIdx ==
+    // ntiles) waits for every tile's error sums (``done`` counts them) and
+    // publishes the losses (publish_loss) while the tiles' backward still runs
+    float *loss;
+    unsigned loss_seq;
+    double inv_count;
+    unsigned *done;
 };
 
 __device__ __forceinline__ float clamp_unit(float x) {
@@ -595,6 +611,80 @@ __device__ __forceinline__ void wave_seg_sums(float (&g)[8], int key) {
 }
 #undef GSVC_FMAC_DPP8
 
+// The loss workgroup's loads per round: 16 tile pairs per thread in flight, so
+// a 1080p frame (4080 pairs) is one round trip.
+constexpr int kLossBatch = 16;
+
+// The frame's losses from the tiles' error sums, in double and in ONE fixed
+// order whatever the workgroup size (kThreads = 128 or 256 emulate the same 256
+// virtual threads: virtual thread v sums pairs v, v + 256, ... in batches, the
+// 64-lane xor trees reduce virtual waves, the four are added pairwise), then
+// stored into ``loss`` -- with GSVC_TRAIN_LOSS_SEQ the pair count (det) and the
+// sequence word after them, released to the host.  Every thread calls it.
+// (kBatch: loads in flight per round; the order of the additions does not
+// depend on it)
+template <int kThreads, int kBatch = kLossBatch>
+__device__ __forceinline__ void publish_loss(const float2 *err, int ntiles, double inv_count,
+                                             float *loss, unsigned loss_seq, const int *det_off,
+                                             int n, double (*s_l)[4]) {
+    constexpr int kV = 256 / kThreads;  // virtual threads per thread
+    const int tid = threadIdx.x;
+    double s2[kV], s1[kV];
+    const int npair = ntiles >> 1;
+    const float4 *e4 = reinterpret_cast<const float4 *>(err);
+#pragma unroll
+    for (int q = 0; q < kV; ++q) {
+        s2[q] = 0.0;
+        s1[q] = 0.0;
+        for (int t0 = tid + q * kThreads; t0 < npair; t0 += kBatch * 256) {
+            float4 e[kBatch];
+#pragma unroll
+            for (int k = 0; k < kBatch; ++k) {
+                const int t = t0 + 256 * k;
+                e[k] = t < npair ? e4[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int k = 0; k < kBatch; ++k) {
+                s2[q] += (double)e[k].x;
+                s1[q] += (double)e[k].y;
+                s2[q] += (double)e[k].z;
+                s1[q] += (double)e[k].w;
+            }
+        }
+    }
+    if ((ntiles & 1) && tid == 0) {
+        const float2 e = err[ntiles - 1];
+        s2[0] += (double)e.x;
+        s1[0] += (double)e.y;
+    }
+#pragma unroll
+    for (int q = 0; q < kV; ++q) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            s2[q] += __shfl_xor(s2[q], off, 64);
+            s1[q] += __shfl_xor(s1[q], off, 64);
+        }
+        if ((tid & 63) == 0) {
+            s_l[0][(tid + q * kThreads) >> 6] = s2[q];
+            s_l[1][(tid + q * kThreads) >> 6] = s1[q];
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        loss[0] = (float)(((s_l[0][0] + s_l[0][1]) + (s_l[0][2] + s_l[0][3])) * inv_count);
+        loss[1] = (float)(((s_l[1][0] + s_l[1][1]) + (s_l[1][2] + s_l[1][3])) * inv_count);
+        // deterministic mode: this frame's (splat, tile) pair count, so
+        // the caller can size det_capacity (word 3, before the release)
+        if (loss_seq && det_off) reinterpret_cast<unsigned *>(loss)[3] = (unsigned)det_off[n];
+        // coherent host memory: the host stops waiting here, while the
+        // rest of the step still runs (later work on the stream is ordered
+        // after it anyway)
+        if (loss_seq)
+            __hip_atomic_store(reinterpret_cast<unsigned *>(loss) + 2, loss_seq, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // v_out rows padded to 17 words: the backward's lanes read pixels of
 // different rows of one column, which with 16-word rows share a bank every 4
 // rows (measured: LDS bank conflicts ~ the VALU time at trained density).
@@ -610,14 +700,50 @@ struct BandLds {
     signed char own[kBThreads];    // backward: per wave, the entry of the round's first items
     signed char perm[kBThreads];   // backward: per wave, the chunk's entries by item length
     int misc[4];   // the waves' error sums
+    int nsel;      // carried bins: the tile's entries among its candidates
 };
 
 // kDet: GSVC_TRAIN_DETERMINISTIC's slot stores in place of the atomics (its
 // own instantiation: the slot arithmetic in the flush would cost the atomic
 // kernel two spilled VGPRs)
-template <bool kStamp, bool kDet = false>
+// kCarry: GSVC_TRAIN_CARRY's carried bins (A.cids) in place of the slab
+template <bool kStamp, bool kDet = false, bool kCarry = false>
 __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTileArgs A) {
     __shared__ BandLds S;
+    if (A.loss && (int)blockIdx.x == A.ntiles) {
+        // the loss workgroup: dispatched after every tile (in-order dispatch),
+        // so each tile it waits for is resident or done; a bounded wait (a
+        // tile that never reports -- impossible short of a fault -- gives NaN
+        // losses rather than a hang)
+        __shared__ double s_l[2][4];
+        __shared__ int s_ok;
+        if (threadIdx.x == 0) {
+            int ok = 0;
+            for (int it = 0; it < (1 << 22); ++it) {
+                // (relaxed polls: an acquire per poll would invalidate the L2)
+                if (__hip_atomic_load(A.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                    (unsigned)A.ntiles) {
+                    ok = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+            s_ok = ok;
+        }
+        __syncthreads();
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        if (s_ok) {
+            publish_loss<kBThreads, 4>(A.err, A.ntiles, A.inv_count, A.loss, A.loss_seq, A.det_off,
+                                       A.num_points, s_l);
+        } else if (threadIdx.x == 0) {
+            A.loss[0] = A.loss[1] = __builtin_nanf("");
+            if (A.loss_seq)
+                __hip_atomic_store(reinterpret_cast<unsigned *>(A.loss) + 2, A.loss_seq,
+                                   __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        if (threadIdx.x == 0) *A.done = 0u;  // the next step's count (after the kernel boundary)
+        return;
+    }
     // Wave issue priority: the arbiter favours older waves, so without it a
     // workgroup dispatched late onto a busy CU waits behind its elders' blending
     // before it can even issue its loads and ranking (stamps: the order phase
@@ -643,10 +769,20 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     // slab records (lanes past kBSpec re-read slot 0: the same lines), the
     // pair's targets (lanes outside the image read pixel 0; only the loss
     // reads them, masked)
+    constexpr bool carry = kCarry;
     const int m_frame = *A.m_dev;
     const unsigned cnt_raw = A.counts[tile];
-    const float4 *h0 = slab_rec(A.slab, A.ntiles, tile, tid < A.spec ? tid : 0);
-    float4 r0 = h0[0], r1 = h0[1], r2 = h0[2];
+    float4 r0, r1, r2;
+    int cid = 0;  // carried bins: the lane's candidate id
+    const int *tcids = carry ? A.cids + (size_t)tile * kTilePix : nullptr;
+    if (carry) {
+        cid = tcids[tid < A.spec ? tid : 0];
+    } else {
+        const float4 *h0 = slab_rec(A.slab, A.ntiles, tile, tid < A.spec ? tid : 0);
+        r0 = h0[0];
+        r1 = h0[1];
+        r2 = h0[2];
+    }
     float gt[3][2];
     {
         const size_t b0 = nin > 0 ? pix0 : 0, b1 = nin > 1 ? pix0 + 1 : b0;
@@ -659,6 +795,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     const bool empty = m_frame < 1;  // rasterize_sum.py:121-127: background, no gradient
     // (a mask, not a branch: the count's load must not sink behind M's)
     const int n_all = (int)__builtin_amdgcn_readfirstlane(cnt_raw) & -(int)!empty;
+    if (carry && tile == 0 && tid == 0) *A.m_clear = 0;  // the next frame's M (the splat kernel's)
     if (tid == 0) {
         A.counts_clear[tile] = 0u;  // the next frame's counts
         // the grouped forward's padding entry: sigma = +inf at every pixel, so
@@ -675,7 +812,31 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     int n = n_all;
 
     // 1. the order
-    if (!dense) {
+    if (!dense && carry) {
+        // <= 64 candidates: wave 0 gathers their records and boxes by id, keeps
+        // the tile's entries and ranks them by id (the others rank last)
+        if (w == 0) {
+            if (lane >= A.spec && lane < n) cid = tcids[lane];
+            bool mem = false;
+            if (lane < n) {
+                const uint2 b = A.cbox[cid];
+                r0 = A.rec[3 * (size_t)cid];
+                r1 = A.rec[3 * (size_t)cid + 1];
+                r2 = A.rec[3 * (size_t)cid + 2];
+                mem = box_has(b, (unsigned)tx, (unsigned)ty);
+            }
+            const int id = mem ? cid : 0x7fffffff;
+            const int rank = rank_below(id, n);
+            if (mem) {
+                S.geo[rank] = r0;
+                S.col[rank] = make_float4(r1.x, r1.z, r1.w, r2.x);
+                S.gid[rank] = id;
+                S.ro[rank] = ellipse_rect(r0.x, r0.y, 2.0f * r0.z, r0.w, 2.0f * r1.x, 1.0f, tx0, ty0);
+            }
+            const int nm = __popcll(__ballot(mem));  // (the whole wave's ballot)
+            if (lane == 0) S.nsel = nm;
+        }
+    } else if (!dense) {
         if (tid >= A.spec && tid < n) {
             const float4 *h = slab_rec(A.slab, A.ntiles, tile, tid);
             r0 = h[0];
@@ -691,15 +852,31 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             S.ro[rank] = ellipse_rect(r0.x, r0.y, 2.0f * r0.z, r0.w, 2.0f * r1.x, 1.0f, tx0, ty0);
         }
     } else if (brute) {
-        if (w == 0)
+        if (w == 0) {
             n = wave_brute_ids(A.xys, A.radii, 0, A.num_points, A.tbx,
                                (A.img_h + kTile - 1) / kTile, tile, s_key);
-        n = min(n_all, kTilePix);  // both waves: wave_brute_ids finds >= 256 of them
+            if (lane == 0) S.nsel = n;
+        }
+        // both waves: wave_brute_ids finds >= 256 of them (carried bins: the
+        // candidates overflowed, the entries may be fewer -- wave 0's count)
+        n = min(n_all, kTilePix);
     } else {
         // the slab's ids, sorted by wave 0 with an LDS bitmap over the id range
         // (tile_ids.h; O(n + id range / 16384 windows), not O(n^2) compares)
-        for (int j = tid; j < n; j += kBThreads)
-            s_ids[j] = __float_as_int(slab_rec(A.slab, A.ntiles, tile, j)[2].y);
+        if (carry) {
+            // carried bins: the candidates whose box holds the tile, compacted
+            if (tid == 0) S.nsel = 0;
+            __syncthreads();
+            for (int j = tid; j < n; j += kBThreads) {
+                const int c = tcids[j];
+                if (box_has(A.cbox[c], (unsigned)tx, (unsigned)ty)) s_ids[atomicAdd(&S.nsel, 1)] = c;
+            }
+            __syncthreads();
+            n = S.nsel;
+        } else {
+            for (int j = tid; j < n; j += kBThreads)
+                s_ids[j] = __float_as_int(slab_rec(A.slab, A.ntiles, tile, j)[2].y);
+        }
         __syncthreads();
         if (w == 0) {
             SegIds ids;
@@ -710,6 +887,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
         }
     }
     __syncthreads();
+    if (carry && (!dense || brute)) n = S.nsel;
     if (A.prio) __builtin_amdgcn_s_setprio(0);
     if (kStamp && tid == 0) st[1] = tstamp();
 
@@ -902,9 +1080,21 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             S.misc[2 * w + 1] = __float_as_int(ae);
         }
         __syncthreads();
-        if (tid == 0)
-            A.err[tile] = make_float2(__int_as_float(S.misc[0]) + __int_as_float(S.misc[2]),
-                                      __int_as_float(S.misc[1]) + __int_as_float(S.misc[3]));
+        if (tid == 0) {
+            const float2 e = make_float2(__int_as_float(S.misc[0]) + __int_as_float(S.misc[2]),
+                                         __int_as_float(S.misc[1]) + __int_as_float(S.misc[3]));
+            if (A.loss) {
+                // reported to the loss workgroup: the sums written through to
+                // memory (sc0 sc1) and acknowledged, then the count -- an
+                // agent-scope release fence here would write back the whole
+                // L2 of the XCD for every tile (measured: 72 -> 174 us a step)
+                asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+                             ::"v"(A.err + tile), "v"(e) : "memory");
+                __hip_atomic_fetch_add(A.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                A.err[tile] = e;
+            }
+        }
     }
     if (kStamp && tid == 0) st[3] = tstamp();
 
@@ -1119,15 +1309,73 @@ struct TrainSplatArgs {
     const int *det_off;
     const float4 *det_part;
     long long det_cap;
+    // GSVC_TRAIN_CARRY: after its update the splat projects itself for the next
+    // frame (rec, xys, radii, its tile box cbox; its gradient record zeroed)
+    // and, when the box leaves the hull of the boxes it was binned under
+    // (chull), appends its id to the tiles the grown hull adds (cids, ccount);
+    // its box area goes into the next frame's M (m_next)
+    int carry, tbx, tby;
+    float2 *xys;
+    uint2 *cbox, *chull;
+    unsigned *ccount;
+    int *cids;
+    int *m_next;
 };
 
-// The loss workgroup's loads per round: 16 tile pairs per thread in flight, so
-// a 1080p frame (4080 pairs) is one round trip.
-constexpr int kLossBatch = 16;
+// GSVC_TRAIN_CARRY: splat i's projection for the next frame from its updated
+// parameters p = {xyz 2, cholesky 3, features 3, rgb_w} -- load_project's op
+// sequence (frame_dev.h), so the record bits equal a projection kernel's --
+// and the upkeep of its carried bins.  Returns its box area (its share of M).
+__device__ __forceinline__ int carry_splat(const TrainSplatArgs &A, int i, const float (&p)[9]) {
+    const float mx = tanhf(p[0]), my = tanhf(p[1]);
+    float l11 = p[2], l21 = p[3], l22 = p[4];
+    if (A.chol_bound) {
+        l11 = l11 + A.chol_bound[0];
+        l21 = l21 + A.chol_bound[1];
+        l22 = l22 + A.chol_bound[2];
+    }
+    float r = p[5], g = p[6], b = p[7];
+    if (A.rgbw) {
+        r = r * p[8];
+        g = g * p[8];
+        b = b * p[8];
+    }
+    const SplatOut S = splat_out(i, mx, my, l11, l21, l22, r, g, b, 1.0f, A.hw, A.hh, A.tbx, A.tby);
+    A.rec[3 * i] = S.r0;
+    A.rec[3 * i + 1] = S.r1;
+    A.rec[3 * i + 2] = S.r2;
+    A.xys[i] = S.P.xy;
+    A.radii[i] = S.P.rad;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) A.grad[4 * i + q] = z;
+    unsigned x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+    if (S.P.rad > 0) tile_bbox(S.P.xy.x, S.P.xy.y, (float)S.P.rad, A.tbx, A.tby, x0, y0, x1, y1);
+    const uint2 nb = pack_box(x0, y0, x1, y1);
+    A.cbox[i] = nb;
+    if (nb.x == nb.y) return 0;  // empty
+    const uint2 h = A.chull[i];
+    const bool hv = h.x != h.y;
+    const unsigned hx0 = h.x & 0xffffu, hy0 = h.x >> 16, hx1 = h.y & 0xffffu, hy1 = h.y >> 16;
+    if (!hv || x0 < hx0 || y0 < hy0 || x1 > hx1 || y1 > hy1) {
+        // the grown hull; its new tiles get the id (the hull's own tiles have it)
+        const unsigned ux0 = hv ? min(x0, hx0) : x0, uy0 = hv ? min(y0, hy0) : y0;
+        const unsigned ux1 = hv ? max(x1, hx1) : x1, uy1 = hv ? max(y1, hy1) : y1;
+        for (unsigned y = uy0; y < uy1; ++y)
+            for (unsigned x = ux0; x < ux1; ++x) {
+                if (hv && x >= hx0 && x < hx1 && y >= hy0 && y < hy1) continue;
+                const unsigned t = y * (unsigned)A.tbx + x;
+                const unsigned sl = atomicAdd(A.ccount + t, 1u);
+                if (sl < (unsigned)kTilePix) A.cids[(size_t)t * kTilePix + sl] = i;
+            }
+        A.chull[i] = pack_box(ux0, uy0, ux1, uy1);
+    }
+    return (int)((x1 - x0) * (y1 - y0));
+}
 
 // One splat's step: the projection VJP, activation VJPs and the Adan update of
 // its elements (update == 0: the gradients into grads_out).
-__device__ __forceinline__ void splat_step(const TrainSplatArgs &A, int i) {
+__device__ __forceinline__ int splat_step(const TrainSplatArgs &A, int i) {
     // Every operand is loaded up front, before any arithmetic: one round trip
     // per lane instead of three (gradient + radius -> record -> Adan state).
     // rec is written for every splat by the projection, so its load needs no
@@ -1210,17 +1458,20 @@ __device__ __forceinline__ void splat_step(const TrainSplatArgs &A, int i) {
         o[6] = df1;
         o[7] = df2;
         o[8] = A.rgbw_train ? dw : 0.0f;
-        return;
+        return 0;
     }
     // Adan on the 8 (9 with rgb_W) elements of this splat
     const float g[9] = {dx0, dx1, vl0, vl1, vl2, df0, df1, df2, dw};
     const float pin[9] = {x0, x1, c0, c1, c2, f0, f1, f2, w};
+    float pnew[9];
 #pragma unroll
     for (int e = 0; e < 9; ++e) {
         const int q = e < 2 ? 0 : (e < 5 ? 1 : (e < 8 ? 2 : 3));
+        pnew[e] = pin[e];
         if (q == 3 && !A.rgbw_train) continue;
         if (A.first[q]) npg[e] = -(g[e] * A.S.clip);
         const float pv = adan_update(A.S, pin[e], g[e], m[e], v[e], df[e], npg[e]);
+        pnew[e] = pv;
         const size_t j = q == 0 ? 2 * (size_t)i + e : (q == 1 ? 3 * (size_t)i + (e - 2)
                                                   : (q == 2 ? 3 * (size_t)i + (e - 5) : (size_t)i));
         float *param = q == 0 ? A.xyz : (q == 1 ? A.chol : (q == 2 ? A.feat : A.rgbw));
@@ -1230,70 +1481,36 @@ __device__ __forceinline__ void splat_step(const TrainSplatArgs &A, int i) {
         A.state[q][2][j] = df[e];
         A.state[q][3][j] = npg[e];
     }
+    return A.carry ? carry_splat(A, i, pnew) : 0;
 }
 
 __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
     if (blockIdx.x == 0) {
-        // the first workgroup (no splats): the loss, the tiles' error sums in a
-        // fixed order, in double; dispatched first so it runs beside the splats
+        // the first workgroup (no splats): the loss, unless the tile kernel's
+        // loss workgroup published it; dispatched first so it runs beside the
+        // splats
         __shared__ double s_l[2][4];
-        double s2 = 0.0, s1 = 0.0;
-        const int npair = A.ntiles >> 1;
-        const float4 *e4 = reinterpret_cast<const float4 *>(A.err);
-        for (int t0 = threadIdx.x; t0 < npair; t0 += kLossBatch * 256) {
-            float4 e[kLossBatch];
-#pragma unroll
-            for (int k = 0; k < kLossBatch; ++k) {
-                const int t = t0 + 256 * k;
-                e[k] = t < npair ? e4[t] : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int k = 0; k < kLossBatch; ++k) {
-                s2 += (double)e[k].x;
-                s1 += (double)e[k].y;
-                s2 += (double)e[k].z;
-                s1 += (double)e[k].w;
-            }
-        }
-        if ((A.ntiles & 1) && threadIdx.x == 0) {
-            const float2 e = A.err[A.ntiles - 1];
-            s2 += (double)e.x;
-            s1 += (double)e.y;
-        }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            s2 += __shfl_xor(s2, off, 64);
-            s1 += __shfl_xor(s1, off, 64);
-        }
-        if ((threadIdx.x & 63) == 0) {
-            s_l[0][threadIdx.x >> 6] = s2;
-            s_l[1][threadIdx.x >> 6] = s1;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            A.loss[0] = (float)(((s_l[0][0] + s_l[0][1]) + (s_l[0][2] + s_l[0][3])) * A.inv_count);
-            A.loss[1] = (float)(((s_l[1][0] + s_l[1][1]) + (s_l[1][2] + s_l[1][3])) * A.inv_count);
-            // deterministic mode: this frame's (splat, tile) pair count, so
-            // the caller can size det_capacity (word 3, before the release)
-            if (A.loss_seq && A.det_off)
-                reinterpret_cast<unsigned *>(A.loss)[3] = (unsigned)A.det_off[A.n];
-            // coherent host memory: the host stops waiting here, while the
-            // splat workgroups still run (later work on the stream is ordered
-            // after them anyway)
-            if (A.loss_seq)
-                __hip_atomic_store(reinterpret_cast<unsigned *>(A.loss) + 2, A.loss_seq,
-                                   __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        if (A.loss) publish_loss<256>(A.err, A.ntiles, A.inv_count, A.loss, A.loss_seq, A.det_off, A.n, s_l);
         return;
     }
     const int t = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
-    if (t < A.n) splat_step(A, t);
+    const int hits = t < A.n ? splat_step(A, t) : 0;
+    if (A.carry) {
+        __shared__ int s_hits[4];
+        add_hits(hits, s_hits, A.m_next);  // the next frame's M
+    }
 }
 
 struct TrainWs {
     FrameWs f;  // with the splat order buffers (GSVC_TRAIN_ORDER)
     float4 *grad;
     float2 *err;
+    // GSVC_TRAIN_CARRY: per tile its candidate ids and their count, per splat
+    // its current tile box and the hull of the boxes it is binned under
+    int *cids;
+    unsigned *ccount;
+    uint2 *cbox, *chull;
+    unsigned *done;  // the tile kernel's count of tiles whose error sums are stored
     size_t bytes;
 };
 
@@ -1309,6 +1526,11 @@ static TrainWs train_ws(char *base, int n, int ntiles) {
     };
     w.grad = (float4 *)take(sizeof(float4) * 4 * nn);
     w.err = (float2 *)take(sizeof(float2) * nt);
+    w.cids = (int *)take(sizeof(int) * kTilePix * nt);
+    w.ccount = (unsigned *)take(sizeof(unsigned) * nt);
+    w.cbox = (uint2 *)take(sizeof(uint2) * nn);
+    w.chull = (uint2 *)take(sizeof(uint2) * nn);
+    w.done = (unsigned *)take(sizeof(unsigned));
     w.bytes = off;
     return w;
 }
@@ -1384,6 +1606,19 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
                                        "projection flags; PROJECT_NEXT needs PROJECTED");
     if (next && !update)
         return set_error(GSVC_ERR_ARG, "train_step_sum: PROJECT_NEXT needs the Adan update");
+    // GSVC_TRAIN_CARRY: the carried bins (a projection builds them; a step
+    // consumes them and its splat kernel carries them to frame_index + 1)
+    const bool carry = (adan_flags & GSVC_TRAIN_CARRY) != 0 && num_points > 0;
+    if (carry && next)
+        return set_error(GSVC_ERR_ARG, "train_step_sum: CARRY excludes PROJECT_NEXT");
+    // (with grads_out the step reads carried bins but carries nothing: the
+    // parameters do not change)
+    if (carry) {
+        ord.carry_ids = w.cids;
+        ord.carry_counts = w.ccount;
+        ord.carry_box = w.cbox;
+        ord.carry_hull = w.chull;
+    }
     const bool det = (adan_flags & GSVC_TRAIN_DETERMINISTIC) != 0;
     int *det_off = nullptr;
     float4 *det_part = nullptr;
@@ -1404,10 +1639,20 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     };
     int rc = GSVC_OK;
     if (!projected) {
+        // (the loss workgroup's count starts at zero; each step leaves it zero)
+        if (hipMemsetAsync(w.done, 0, sizeof(unsigned), s) != hipSuccess)
+            return set_error(GSVC_ERR_HIP, "train_step_sum: memset failed");
+        if (carry) {
+            // a new set of carried bins: counts and this frame's M from zero (a
+            // previous step's splat kernel may have carried into them)
+            if (hipMemsetAsync(w.ccount, 0, sizeof(unsigned) * (size_t)ntiles, s) != hipSuccess ||
+                hipMemsetAsync(f.m_acc, 0, sizeof(int), s) != hipSuccess)
+                return set_error(GSVC_ERR_HIP, "train_step_sum: memset failed");
+        }
         // a refreshing projection's sort runs after the step (off the loss's path)
         rc = frame_project_launch(num_points, xyz, 1, cholesky, cholesky_bound, features, rgb_w,
                                   nullptr, img_height, img_width, w.f, f, w.grad, s, 1, nullptr, 0,
-                                  (use_order || refresh) ? &ord : nullptr);
+                                  (use_order || refresh || carry) ? &ord : nullptr);
         if (rc) return rc;
         if (only) return refresh ? splat_order_sort(w.f, num_points, tbx, tby, s) : GSVC_OK;
     }
@@ -1423,6 +1668,10 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
         if (rc) return rc;
     }
     const double count = 3.0 * (double)img_height * (double)img_width;  // numel of [3, H, W]
+    // GSVC_TRAIN_LOSS_SEQ: ``loss`` is coherent host memory of 3 words; word 2
+    // receives the call's sequence number (frame_index + 1, never 0)
+    const unsigned loss_seq =
+        (adan_flags & GSVC_TRAIN_LOSS_SEQ) ? ((unsigned)frame_index + 1u) | 0x80000000u : 0u;
     TrainTileArgs T{};
     T.tbx = tbx;
     T.img_w = (int)img_width;
@@ -1453,23 +1702,47 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     T.det_off = det_off;
     T.det_part = det_part;
     T.det_cap = det_capacity;
-    if (g_knobs[5] == 2 && g_debug_ptr) {  // diagnostic: per-tile stamps
+    if (carry) {
+        T.counts = w.ccount;
+        T.cids = w.cids;
+        T.cbox = w.cbox;
+        T.m_clear = f.m_clear;
+    }
+    if (g_knobs[5] == 2 && g_debug_ptr && !carry) {  // diagnostic: per-tile stamps
         T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
         auto kfn = train_tile_kernel<true>;
         hipLaunchKernelGGL(kfn, dim3(ntiles), dim3(kT), 0, s, T);
     } else if (g_knobs[5] == 3 && g_debug_ptr) {  // diagnostic: per-tile stamps, band kernel
         T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
-        hipLaunchKernelGGL(train_tile_band_kernel<true>, dim3(ntiles), dim3(kBThreads), 0, s, T);
+        if (carry)
+            hipLaunchKernelGGL((train_tile_band_kernel<true, false, true>), dim3(ntiles), dim3(kBThreads),
+                               0, s, T);
+        else
+            hipLaunchKernelGGL(train_tile_band_kernel<true>, dim3(ntiles), dim3(kBThreads), 0, s, T);
     } else {
         // knob 8 = 1: the 256-thread workgroup-per-tile kernel (A/B; atomics only)
+        const bool old_kernel = g_knobs[8] == 1 && !det && !carry;
+        if (!old_kernel && g_knobs[19] != 1) {
+            // the band kernel's loss workgroup publishes the losses (A/B knob
+            // 19 = 1: the splat kernel's first workgroup does, after the tiles)
+            T.loss = loss;
+            T.loss_seq = loss_seq;
+            T.inv_count = 1.0 / count;
+            T.done = w.done;
+        }
+        const dim3 grid(ntiles + (T.loss ? 1 : 0));
         hipEvent_t tev[2];
         const int tslot = timing_begin(s, tev, kTimingTrainTile);
-        if (g_knobs[8] == 1 && !det)
+        if (old_kernel)
             launch_timed(train_tile_kernel<false>, dim3(ntiles), dim3(kT), 0, s, tev, T);
+        else if (det && carry)
+            launch_timed(train_tile_band_kernel<false, true, true>, grid, dim3(kBThreads), 0, s, tev, T);
         else if (det)
-            launch_timed(train_tile_band_kernel<false, true>, dim3(ntiles), dim3(kBThreads), 0, s, tev, T);
+            launch_timed(train_tile_band_kernel<false, true>, grid, dim3(kBThreads), 0, s, tev, T);
+        else if (carry)
+            launch_timed(train_tile_band_kernel<false, false, true>, grid, dim3(kBThreads), 0, s, tev, T);
         else
-            launch_timed(train_tile_band_kernel<false>, dim3(ntiles), dim3(kBThreads), 0, s, tev, T);
+            launch_timed(train_tile_band_kernel<false>, grid, dim3(kBThreads), 0, s, tev, T);
         timing_end(s, tslot, kTimingTrainTile);
     }
     rc = check_launch("train_step_sum: tiles");
@@ -1502,10 +1775,19 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     P.det_part = det_part;
     P.det_cap = det_capacity;
     P.err = w.err;
-    P.loss = loss;
-    // GSVC_TRAIN_LOSS_SEQ: ``loss`` is coherent host memory of 3 words; word 2
-    // receives the call's sequence number (frame_index + 1, never 0)
-    P.loss_seq = (adan_flags & GSVC_TRAIN_LOSS_SEQ) ? ((unsigned)frame_index + 1u) | 0x80000000u : 0u;
+    P.loss = T.loss ? nullptr : loss;  // (published by the tile kernel's loss workgroup)
+    if (carry && update) {
+        P.carry = 1;
+        P.tbx = tbx;
+        P.tby = tby;
+        P.xys = (float2 *)w.f.xys;
+        P.cbox = w.cbox;
+        P.chull = w.chull;
+        P.ccount = w.ccount;
+        P.cids = w.cids;
+        P.m_next = f.m_clear;  // frame_index + 1's M slot (the tile kernel zeroed it)
+    }
+    P.loss_seq = loss_seq;
     // one extra (first) workgroup sums the loss, beside the splat workgroups
     const int blocks = (num_points > 0 ? ceil_div(num_points, 256) : 0) + 1;
     hipEvent_t tev[2];

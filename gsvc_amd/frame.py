@@ -338,9 +338,12 @@ class GaussianVideoFrame(nn.Module):
         self.scheduler.optimizer._opt_called = True
         self.__dict__["fused_steps"] += 1  # a plain counter: skip Module.__setattr__
         self.scheduler.step()
+        # the loss as a host scalar tensor (callers take .item() / float() of it),
+        # made while the kernels run: after the wait only its value is stored
+        loss = torch.empty(())
+        loss_np = loss.numpy()
         mse, l1 = bs.result()  # the reference's PSNR .item(): one stream wait
-        # the loss as a host scalar tensor (callers take .item() / float() of it)
-        loss = torch.tensor(l1 if self.loss_type == "L1" else mse)
+        loss_np[...] = l1 if self.loss_type == "L1" else mse
         psnr = 10 * math.log10(1.0 / mse)
         return loss, psnr
 

@@ -31,7 +31,17 @@ TRAIN_PROJECTED = 0x1000  # GSVC_TRAIN_PROJECTED
 TRAIN_PROJECT_NEXT = 0x2000  # GSVC_TRAIN_PROJECT_NEXT
 TRAIN_DETERMINISTIC = 0x4000  # GSVC_TRAIN_DETERMINISTIC
 DET_CAPACITY_PER_SPLAT = 8  # first det_capacity guess: M / N is ~2.5 at init, ~5 trained
-PROJECT_AHEAD = True  # a bound step enqueues the next step's projection after itself
+PROJECT_AHEAD = True  # a bound step leaves the next step's frame projected behind itself
+TRAIN_CARRY = 0x8000  # GSVC_TRAIN_CARRY
+# Carried bins (GSVC_TRAIN_CARRY): a bound step's splat kernel projects the next
+# frame itself and keeps the tile bins from step to step (at trained density
+# ~160 of 50k splats change tile box per step, tools/bin_drift.py), so no
+# projection kernel runs between steps; a projection rebuilds them every
+# CARRY_REBUILD_EVERY steps (the bins only grow) and whenever PROJECT_AHEAD's
+# checks fail.  False: the projection of the next frame is enqueued instead
+# (GSVC_TRAIN_PROJECT_NEXT).
+CARRY_BINS = True
+CARRY_REBUILD_EVERY = 64
 
 # A step's projection of the NEXT frame is used only if nothing could have
 # changed the parameters since: no other fused launch on the same parameters
@@ -71,6 +81,7 @@ class _TrainWorkspace:
         #                        (weakref to the step, frame, launch count, epoch, versions)
         self.det_buf = None    # GSVC_TRAIN_DETERMINISTIC workspace
         self.det_cap = 0
+        self.carry_age = 0     # steps since the carried bins were rebuilt
 
     def det_workspace(self, dev: torch.device, n: int, pairs: int = 0):
         """The deterministic mode's slot buffer for n splats, with room for at
@@ -208,6 +219,7 @@ class BoundStep:
         self.det = False        # this step runs GSVC_TRAIN_DETERMINISTIC
         self.det_pairs = 0      # the (splat, tile) pairs its last det step reported
         self.det_overflows = 0  # det steps whose capacity was short (those fell back to atomics)
+        self.ahead_steps = 0    # steps that used the projection the previous step enqueued
         self.params = tuple(t for t in (xyz, cholesky, features, rgb_w) if t is not None)
 
     def __del__(self):
@@ -273,11 +285,17 @@ class BoundStep:
                 # the workspace -- start from zeroed counters
                 ws.dirty = True
                 ws = _workspace(self.dev, self.n, self.H, self.W)
-            if not ahead:
-                self._call(ws, lib, gt, int(adan_flags) | TRAIN_PROJECT_ONLY | ws.order_flags())
-            flags |= TRAIN_PROJECTED | TRAIN_PROJECT_NEXT
+            carry = TRAIN_CARRY if CARRY_BINS else 0
+            if not ahead or (carry and ws.carry_age >= CARRY_REBUILD_EVERY):
+                self._call(ws, lib, gt, int(adan_flags) | TRAIN_PROJECT_ONLY | carry | ws.order_flags())
+                ws.carry_age = 0
+            if ahead:
+                self.ahead_steps += 1
+            ws.carry_age += 1
+            flags |= TRAIN_PROJECTED | (carry or TRAIN_PROJECT_NEXT)
         self.seq = ((ws.frame + 1) & 0xFFFFFFFF) | 0x80000000
-        self._call(ws, lib, gt, flags | ws.order_flags())
+        # the order flags go with a projection (PROJECT_NEXT's or the call's own)
+        self._call(ws, lib, gt, flags | (0 if flags & TRAIN_CARRY else ws.order_flags()))
         launches = _note_launch(a.xyz)
         if PROJECT_AHEAD:
             ws.pending = (weakref.ref(self), ws.frame + 1, launches, _param_epoch[0], versions)

@@ -366,6 +366,20 @@ int gsvc_render_frame_sum_ex(int num_points, const float *xyz, int xyz_tanh,
  * word 3 receives the frame's M (before the sequence word), so the caller can
  * grow det_capacity. */
 #define GSVC_TRAIN_DETERMINISTIC 0x4000
+/* GSVC_TRAIN_CARRY (speed only; the same results): carried bins.  The tile
+ * bins are kept from step to step instead of re-projected: with
+ * GSVC_TRAIN_PROJECT_ONLY (or a call without GSVC_TRAIN_PROJECTED) the
+ * projection builds them -- per tile the ids of the splats whose tile box
+ * holds it -- and a step with GSVC_TRAIN_PROJECTED | GSVC_TRAIN_CARRY reads
+ * them, keeping of each tile's candidates those whose current box holds the
+ * tile, while its splat kernel, right after a splat's Adan update, projects the
+ * splat for frame_index + 1 and appends its id to the tiles its box newly
+ * reaches (the bins only grow: stale candidates are skipped).  Each step thus
+ * leaves the next frame projected and binned, with no projection kernel.  The
+ * caller rebuilds them now and then (a PROJECT_ONLY call) and whenever the
+ * parameters changed outside the steps, as for GSVC_TRAIN_PROJECT_NEXT, which
+ * it excludes. */
+#define GSVC_TRAIN_CARRY 0x8000
 size_t gsvc_train_step_det_workspace_bytes(int num_points, long long det_capacity);
 size_t gsvc_train_step_workspace_bytes(int num_points, unsigned img_height,
                                        unsigned img_width);

@@ -1,0 +1,144 @@
+"""Carried bins (GSVC_TRAIN_CARRY, train.hip): the training step keeps its tile
+bins from step to step -- the splat kernel projects each splat for the next
+frame right after its Adan update and appends its id to the tiles its box
+newly reaches -- instead of running a projection kernel between steps.
+
+The bins hold a superset of each tile's entries and the tile kernel keeps
+the candidates whose current box holds the tile, so results cannot change: under
+torch.use_deterministic_algorithms (bitwise reproducible gradients) carried and
+re-projected trajectories must be BITWISE equal -- parameters, Adan state and
+every loss -- through rebuilds (every CARRY_REBUILD_EVERY steps), fast-moving
+splats (large learning rate: many appends per step), tiles whose candidates
+overflow 256 (the bbox rebuild), and splats leaving / entering the image.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def deterministic():
+    prev = torch.are_deterministic_algorithms_enabled()
+    prev_warn = torch.is_deterministic_algorithms_warn_only_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    yield
+    torch.use_deterministic_algorithms(prev, warn_only=prev_warn)
+
+
+def _run(cuda, carry, H, W, n, steps, lr=1e-3, seed=3, gt_seed=4, edit=None, rebuild=None):
+    from gsvc_amd import train as T
+    from gsvc_amd.frame import make_frame_model, synthetic_gt
+    old = (T.CARRY_BINS, T.CARRY_REBUILD_EVERY)
+    T.CARRY_BINS = carry
+    if rebuild is not None:
+        T.CARRY_REBUILD_EVERY = rebuild
+    try:
+        m = make_frame_model(H, W, n, cuda, seed=seed, lr=lr)
+        if edit is not None:
+            edit(m)
+        gt = synthetic_gt(H, W, gt_seed, cuda)
+        losses = [float(m.train_iter(gt, it)[0]) for it in range(1, steps + 1)]
+        torch.cuda.synchronize()
+        assert m.fused_steps == steps
+        return m, losses
+    finally:
+        T.CARRY_BINS, T.CARRY_REBUILD_EVERY = old
+
+
+def _same(a, b):
+    la, lb = a[1], b[1]
+    assert la == lb
+    ma, mb = a[0], b[0]
+    for k, v in ma.state_dict().items():
+        assert torch.equal(v, mb.state_dict()[k]), k
+    for p, q in zip(ma.optimizer.param_groups[0]["params"], mb.optimizer.param_groups[0]["params"]):
+        for key in ("exp_avg", "exp_avg_sq", "exp_avg_diff", "neg_pre_grad"):
+            assert torch.equal(ma.optimizer.state[p][key], mb.optimizer.state[q][key]), key
+
+
+def test_carried_equals_reprojected_through_rebuilds(cuda, deterministic):
+    """70 steps at 256x256 / 2000 splats: past the rebuild at step 64."""
+    _same(_run(cuda, True, 256, 256, 2000, 70), _run(cuda, False, 256, 256, 2000, 70))
+
+
+def test_carried_fast_motion_and_overflow(cuda, deterministic):
+    """lr 0.05: splats jump tiles every step (many appends, hulls growing
+    across the image); a quarter of 6000 splats piled on one spot overflows
+    that tile's 256 candidates (the bbox rebuild path); no rebuild for 40 steps."""
+    def pile(m):
+        with torch.no_grad():
+            sel = torch.arange(0, m._xyz.shape[0], 4, device=m._xyz.device)
+            m._xyz[sel] = torch.atanh(torch.full((len(sel), 2), -0.25, device=m._xyz.device)
+                                      + 0.05 * torch.rand(len(sel), 2, device=m._xyz.device))
+            m._cholesky[sel] = torch.tensor([2.5, 0.3, 1.5], device=m._xyz.device)
+    a = _run(cuda, True, 128, 192, 6000, 40, lr=0.05, edit=pile, rebuild=1000)
+    b = _run(cuda, False, 128, 192, 6000, 40, lr=0.05, edit=pile)
+    _same(a, b)
+
+
+def test_carried_bins_trained_density(cuda, deterministic):
+    """The bench's frame at 1080p / 50k from its trained state (the
+    train_state fixture): 20 carried steps bitwise equal to re-projected ones."""
+    from conftest import load_golden
+    from gsvc_amd.frame import synthetic_gt
+    z = load_golden("train_state_1080p_n50k")
+
+    def load(m):
+        with torch.no_grad():
+            for k in ("_xyz", "_cholesky", "_features_dc"):
+                getattr(m, k).copy_(torch.from_numpy(z["state_" + k]))
+
+    H, W = 1080, 1920
+    gt_seed = int(z["gt_seed"])
+    a = _run(cuda, True, H, W, int(z["n"]), 20, seed=0, gt_seed=gt_seed, edit=load)
+    b = _run(cuda, False, H, W, int(z["n"]), 20, seed=0, gt_seed=gt_seed, edit=load)
+    _same(a, b)
+    assert a[0]._bound_step.ahead_steps == 19
+
+
+def test_carried_atomic_path_close(cuda):
+    """Without the deterministic mode (the default float-atomic backward):
+    carried and re-projected trajectories agree to the atomics' run-to-run
+    spread."""
+    a = _run(cuda, True, 256, 256, 2000, 30)
+    b = _run(cuda, False, 256, 256, 2000, 30)
+    for x, y in zip(a[1], b[1]):
+        assert abs(x - y) <= 2e-5 * abs(y)
+    assert torch.allclose(a[0]._xyz, b[0]._xyz, rtol=1e-3, atol=1e-4)
+
+
+def test_loss_workgroup_matches_splat_kernel_loss(cuda, deterministic):
+    """The tile kernel's loss workgroup (publishing while the backward runs)
+    and the splat kernel's first workgroup (A/B knob 19 = 1) add the tiles'
+    error sums in the same order: identical loss bits."""
+    from gsvc_amd import _lib
+    lib = _lib.load()
+    try:
+        lib.gsvc_debug_set(19, 1)
+        b = _run(cuda, True, 256, 384, 3000, 12)
+    finally:
+        lib.gsvc_debug_set(19, 0)
+    a = _run(cuda, True, 256, 384, 3000, 12)
+    _same(a, b)
+
+
+def test_carried_bins_through_prune_and_densify(cuda, deterministic, tmp_path):
+    """BASELINE config 5's loop (gsvc_amd.video: removal on the K-frame,
+    densify + prune on the P-frames, splat counts changing between steps):
+    carried and re-projected bins give bitwise the same frames."""
+    from gsvc_amd import train as T
+    from gsvc_amd import video as V
+    argv = ["--synthetic", "3", "--height", "1080", "--width", "1920", "--num_points", "100000",
+            "--iterations", "1100", "--k_frames", "1", "--is_rm", "--is_ad",
+            "--densification_interval", "100", "--removal_rate", "0.1"]
+    out = []
+    for carry in (True, False):
+        old = T.CARRY_BINS
+        T.CARRY_BINS = carry
+        try:
+            out.append(V.main(argv + ["--root", str(tmp_path / str(carry))]))
+        finally:
+            T.CARRY_BINS = old
+    a, b = ([(r["num_gaussians"], r["psnr"]) for r in x["frames"]] for x in out)
+    assert a == b

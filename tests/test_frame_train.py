@@ -116,6 +116,42 @@ def _ahead_run(cuda, ahead, edits):
         Tr.PROJECT_AHEAD = old
 
 
+def test_projection_ahead_per_parameter_set(cuda):
+    """Two models training interleaved on two streams keep their projections
+    ahead (launches are counted per parameter set), and
+    each trajectory is bitwise the one it has alone (deterministic backward)."""
+    from gsvc_amd.frame import make_frame_model, synthetic_gt
+    prev = torch.are_deterministic_algorithms_enabled()
+    prev_warn = torch.is_deterministic_algorithms_warn_only_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        specs = [(2000, 3), (3000, 7)]
+        gts = [synthetic_gt(256, 256, 4, cuda), synthetic_gt(256, 256, 5, cuda)]
+        streams = [torch.cuda.Stream(cuda), torch.cuda.Stream(cuda)]
+
+        def run(which):
+            ms = {k: make_frame_model(256, 256, specs[k][0], cuda, seed=specs[k][1]) for k in which}
+            torch.cuda.synchronize()
+            out = {k: [] for k in which}
+            for it in range(1, 13):
+                for k in which:
+                    with torch.cuda.stream(streams[k]):
+                        out[k].append(float(ms[k].train_iter(gts[k], it)[0]))
+            torch.cuda.synchronize()
+            return ms, out
+
+        both, lb = run([0, 1])
+        for k in (0, 1):
+            solo, ls = run([k])
+            assert lb[k] == ls[k]
+            assert torch.equal(both[k]._xyz, solo[k]._xyz)
+            assert torch.equal(both[k]._features_dc, solo[k]._features_dc)
+            # every step after the first used the projection its predecessor enqueued
+            assert both[k].fused_steps == 12 and both[k]._bound_step.ahead_steps == 11
+    finally:
+        torch.use_deterministic_algorithms(prev, warn_only=prev_warn)
+
+
 def test_projection_ahead_matches_and_honours_edits(cuda):
     """The fused step's projection of the next frame, enqueued ahead, gives the
     same trajectory as projecting at the start of each step, and is discarded
