@@ -75,13 +75,6 @@ struct TrainTileArgs {
     const int *cids;
     const uint2 *cbox;
     int *m_clear;
-    // loss != NULL (band kernel): one extra workgroup (the last, blockIdx ==
-    // ntiles) waits for every tile's error sums (``done`` counts them) and
-    // publishes the losses (publish_loss) while the tiles' backward still runs
-    float *loss;
-    unsigned loss_seq;
-    double inv_count;
-    unsigned *done;
 };
 
 __device__ __forceinline__ float clamp_unit(float x) {
@@ -618,7 +611,11 @@ constexpr int kLossBatch = 16;
 // The frame's losses from the tiles' error sums, in double and in ONE fixed
 // order whatever the workgroup size (kThreads = 128 or 256 emulate the same 256
 // virtual threads: virtual thread v sums pairs v, v + 256, ... in batches, the
-// 64-lane xor trees reduce virtual waves, the four are added pairwise), then
+// 64-lane xor trees reduce virtual waves, the four are added pairwise; a
+// 128-thread loss workgroup in the tile kernel, publishing while the last
+// tiles' backward ran, was measured and removed: tile kernel 117 / 57 vs 52.8
+// us with a per-tile counter / written-through sentinel polls,
+// profiles/r03/loss_wg/), then
 // stored into ``loss`` -- with GSVC_TRAIN_LOSS_SEQ the pair count (det) and the
 // sequence word after them, released to the host.  Every thread calls it.
 // (kBatch: loads in flight per round; the order of the additions does not
@@ -710,40 +707,6 @@ struct BandLds {
 template <bool kStamp, bool kDet = false, bool kCarry = false>
 __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTileArgs A) {
     __shared__ BandLds S;
-    if (A.loss && (int)blockIdx.x == A.ntiles) {
-        // the loss workgroup: dispatched after every tile (in-order dispatch),
-        // so each tile it waits for is resident or done; a bounded wait (a
-        // tile that never reports -- impossible short of a fault -- gives NaN
-        // losses rather than a hang)
-        __shared__ double s_l[2][4];
-        __shared__ int s_ok;
-        if (threadIdx.x == 0) {
-            int ok = 0;
-            for (int it = 0; it < (1 << 22); ++it) {
-                // (relaxed polls: an acquire per poll would invalidate the L2)
-                if (__hip_atomic_load(A.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-                    (unsigned)A.ntiles) {
-                    ok = 1;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(4);
-            }
-            s_ok = ok;
-        }
-        __syncthreads();
-        __atomic_thread_fence(__ATOMIC_ACQUIRE);
-        if (s_ok) {
-            publish_loss<kBThreads, 4>(A.err, A.ntiles, A.inv_count, A.loss, A.loss_seq, A.det_off,
-                                       A.num_points, s_l);
-        } else if (threadIdx.x == 0) {
-            A.loss[0] = A.loss[1] = __builtin_nanf("");
-            if (A.loss_seq)
-                __hip_atomic_store(reinterpret_cast<unsigned *>(A.loss) + 2, A.loss_seq,
-                                   __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        if (threadIdx.x == 0) *A.done = 0u;  // the next step's count (after the kernel boundary)
-        return;
-    }
     // Wave issue priority: the arbiter favours older waves, so without it a
     // workgroup dispatched late onto a busy CU waits behind its elders' blending
     // before it can even issue its loads and ranking (stamps: the order phase
@@ -1083,17 +1046,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
         if (tid == 0) {
             const float2 e = make_float2(__int_as_float(S.misc[0]) + __int_as_float(S.misc[2]),
                                          __int_as_float(S.misc[1]) + __int_as_float(S.misc[3]));
-            if (A.loss) {
-                // reported to the loss workgroup: the sums written through to
-                // memory (sc0 sc1) and acknowledged, then the count -- an
-                // agent-scope release fence here would write back the whole
-                // L2 of the XCD for every tile (measured: 72 -> 174 us a step)
-                asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
-                             ::"v"(A.err + tile), "v"(e) : "memory");
-                __hip_atomic_fetch_add(A.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                A.err[tile] = e;
-            }
+            A.err[tile] = e;
         }
     }
     if (kStamp && tid == 0) st[3] = tstamp();
@@ -1486,11 +1439,10 @@ __device__ __forceinline__ int splat_step(const TrainSplatArgs &A, int i) {
 
 __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
     if (blockIdx.x == 0) {
-        // the first workgroup (no splats): the loss, unless the tile kernel's
-        // loss workgroup published it; dispatched first so it runs beside the
-        // splats
+        // the first workgroup (no splats): the loss; dispatched first so it
+        // runs beside the splats
         __shared__ double s_l[2][4];
-        if (A.loss) publish_loss<256>(A.err, A.ntiles, A.inv_count, A.loss, A.loss_seq, A.det_off, A.n, s_l);
+        publish_loss<256>(A.err, A.ntiles, A.inv_count, A.loss, A.loss_seq, A.det_off, A.n, s_l);
         return;
     }
     const int t = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
@@ -1510,7 +1462,6 @@ struct TrainWs {
     int *cids;
     unsigned *ccount;
     uint2 *cbox, *chull;
-    unsigned *done;  // the tile kernel's count of tiles whose error sums are stored
     size_t bytes;
 };
 
@@ -1530,7 +1481,6 @@ static TrainWs train_ws(char *base, int n, int ntiles) {
     w.ccount = (unsigned *)take(sizeof(unsigned) * nt);
     w.cbox = (uint2 *)take(sizeof(uint2) * nn);
     w.chull = (uint2 *)take(sizeof(uint2) * nn);
-    w.done = (unsigned *)take(sizeof(unsigned));
     w.bytes = off;
     return w;
 }
@@ -1639,9 +1589,6 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     };
     int rc = GSVC_OK;
     if (!projected) {
-        // (the loss workgroup's count starts at zero; each step leaves it zero)
-        if (hipMemsetAsync(w.done, 0, sizeof(unsigned), s) != hipSuccess)
-            return set_error(GSVC_ERR_HIP, "train_step_sum: memset failed");
         if (carry) {
             // a new set of carried bins: counts and this frame's M from zero (a
             // previous step's splat kernel may have carried into them)
@@ -1722,15 +1669,7 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     } else {
         // knob 8 = 1: the 256-thread workgroup-per-tile kernel (A/B; atomics only)
         const bool old_kernel = g_knobs[8] == 1 && !det && !carry;
-        if (!old_kernel && g_knobs[19] != 1) {
-            // the band kernel's loss workgroup publishes the losses (A/B knob
-            // 19 = 1: the splat kernel's first workgroup does, after the tiles)
-            T.loss = loss;
-            T.loss_seq = loss_seq;
-            T.inv_count = 1.0 / count;
-            T.done = w.done;
-        }
-        const dim3 grid(ntiles + (T.loss ? 1 : 0));
+        const dim3 grid(ntiles);
         hipEvent_t tev[2];
         const int tslot = timing_begin(s, tev, kTimingTrainTile);
         if (old_kernel)
@@ -1775,7 +1714,7 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     P.det_part = det_part;
     P.det_cap = det_capacity;
     P.err = w.err;
-    P.loss = T.loss ? nullptr : loss;  // (published by the tile kernel's loss workgroup)
+    P.loss = loss;
     if (carry && update) {
         P.carry = 1;
         P.tbx = tbx;

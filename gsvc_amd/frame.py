@@ -318,8 +318,8 @@ class GaussianVideoFrame(nn.Module):
                 st["neg_pre_grad"] = torch.empty_like(p)  # the kernel starts it at -grad
                 flags |= 1 << (1 + q)
             state += [st["exp_avg"], st["exp_avg_sq"], st["exp_avg_diff"], st["neg_pre_grad"]]
-        gt = gt_image.detach()
-        if gt.dtype != torch.float32 or not gt.is_contiguous():
+        gt = gt_image.detach() if gt_image.requires_grad else gt_image
+        if gt.dtype is not torch.float32 or not gt.is_contiguous():
             gt = gt.float().contiguous()
         # the step bound to these tensors: pointers built once, rebuilt when any
         # parameter, state tensor or constant object changes

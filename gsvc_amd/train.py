@@ -119,6 +119,7 @@ def order_flags(ws) -> int:
 
 
 _workspaces = {}
+_data_ptr = torch.Tensor.data_ptr
 _raw_stream = torch._C._cuda_getCurrentRawStream  # current stream handle, no Stream object
 
 
@@ -196,7 +197,8 @@ class BoundStep:
             self.state[k] = _f32_ptr(t, "adan_state", numels[k // 4]) or None
         # the storage pointers ``matches`` re-checks (parameters, constants, state)
         self.live = [k for k, t in enumerate(self.tensors) if t is not None]
-        self.ptrs = [self.tensors[k].data_ptr() for k in self.live]
+        self.live_tensors = [self.tensors[k] for k in self.live]
+        self.ptrs = list(map(_data_ptr, self.live_tensors))
         self.hp = (ctypes.c_double * 10)()
         a = self.args = _StepArgs()
         a.num_points = n
@@ -235,7 +237,8 @@ class BoundStep:
         # ``state[k].data = ...`` or ``set_`` swap it under the same object)
         if tuple(map(id, tensors)) != self.ids:
             return False
-        return [tensors[k].data_ptr() for k in self.live] == self.ptrs
+        # (the same objects as self.tensors: their storages now)
+        return list(map(_data_ptr, self.live_tensors)) == self.ptrs
 
     def launch(self, gt: Tensor, adan_hparams, adan_flags: int) -> None:
         """Enqueue one fused step on the current stream.  The step's last

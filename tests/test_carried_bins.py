@@ -108,21 +108,6 @@ def test_carried_atomic_path_close(cuda):
     assert torch.allclose(a[0]._xyz, b[0]._xyz, rtol=1e-3, atol=1e-4)
 
 
-def test_loss_workgroup_matches_splat_kernel_loss(cuda, deterministic):
-    """The tile kernel's loss workgroup (publishing while the backward runs)
-    and the splat kernel's first workgroup (A/B knob 19 = 1) add the tiles'
-    error sums in the same order: identical loss bits."""
-    from gsvc_amd import _lib
-    lib = _lib.load()
-    try:
-        lib.gsvc_debug_set(19, 1)
-        b = _run(cuda, True, 256, 384, 3000, 12)
-    finally:
-        lib.gsvc_debug_set(19, 0)
-    a = _run(cuda, True, 256, 384, 3000, 12)
-    _same(a, b)
-
-
 def test_carried_bins_through_prune_and_densify(cuda, deterministic, tmp_path):
     """BASELINE config 5's loop (gsvc_amd.video: removal on the K-frame,
     densify + prune on the P-frames, splat counts changing between steps):
