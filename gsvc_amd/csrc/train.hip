@@ -1279,7 +1279,8 @@ struct TrainSplatArgs {
 // parameters p = {xyz 2, cholesky 3, features 3, rgb_w} -- load_project's op
 // sequence (frame_dev.h), so the record bits equal a projection kernel's --
 // and the upkeep of its carried bins.  Returns its box area (its share of M).
-__device__ __forceinline__ int carry_splat(const TrainSplatArgs &A, int i, const float (&p)[9]) {
+__device__ __forceinline__ int carry_splat(const TrainSplatArgs &A, int i, const float (&p)[9],
+                                           uint2 h) {
     const float mx = tanhf(p[0]), my = tanhf(p[1]);
     float l11 = p[2], l21 = p[3], l22 = p[4];
     if (A.chol_bound) {
@@ -1307,7 +1308,6 @@ __device__ __forceinline__ int carry_splat(const TrainSplatArgs &A, int i, const
     const uint2 nb = pack_box(x0, y0, x1, y1);
     A.cbox[i] = nb;
     if (nb.x == nb.y) return 0;  // empty
-    const uint2 h = A.chull[i];
     const bool hv = h.x != h.y;
     const unsigned hx0 = h.x & 0xffffu, hy0 = h.x >> 16, hx1 = h.y & 0xffffu, hy1 = h.y >> 16;
     if (!hv || x0 < hx0 || y0 < hy0 || x1 > hx1 || y1 > hy1) {
@@ -1354,6 +1354,8 @@ __device__ __forceinline__ int splat_step(const TrainSplatArgs &A, int i) {
     const float x0 = A.xyz[2 * i], x1 = A.xyz[2 * i + 1];
     const float f0 = A.feat[3 * i], f1 = A.feat[3 * i + 1], f2 = A.feat[3 * i + 2];
     const float w = A.rgbw ? A.rgbw[i] : 1.0f;
+    // the carry's hull, with the other operands (not a round trip after the update)
+    const uint2 hull = A.carry ? A.chull[i] : make_uint2(0u, 0u);
     const bool upd = A.update != 0;
     float m[9], v[9], df[9], npg[9];
 #pragma unroll
@@ -1434,7 +1436,7 @@ __device__ __forceinline__ int splat_step(const TrainSplatArgs &A, int i) {
         A.state[q][2][j] = df[e];
         A.state[q][3][j] = npg[e];
     }
-    return A.carry ? carry_splat(A, i, pnew) : 0;
+    return A.carry ? carry_splat(A, i, pnew, hull) : 0;
 }
 
 __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
@@ -1570,6 +1572,16 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
         ord.carry_hull = w.chull;
     }
     const bool det = (adan_flags & GSVC_TRAIN_DETERMINISTIC) != 0;
+    // GSVC_TRAIN_TILES_NEXT: after the splat kernel (which carried the bins to
+    // frame_index + 1), enqueue frame_index + 1's tile kernel with this call's
+    // target -- it reads only the carried bins, the records and gt, none of
+    // the next call's hyper-parameters; GSVC_TRAIN_TILED: this frame's tile
+    // kernel is that one (the call launches the splat kernel only)
+    const bool tiled = (adan_flags & GSVC_TRAIN_TILED) != 0;
+    const bool tiles_next = (adan_flags & GSVC_TRAIN_TILES_NEXT) != 0;
+    if ((tiled || tiles_next) && (!carry || !projected || !update || det || render_out))
+        return set_error(GSVC_ERR_ARG, "train_step_sum: TILED / TILES_NEXT need CARRY | PROJECTED, "
+                                       "the Adan update, no render_out and no DETERMINISTIC");
     int *det_off = nullptr;
     float4 *det_part = nullptr;
     if (det) {
@@ -1628,9 +1640,6 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     T.loss_l1 = loss_kind;
     T.norm = loss_kind ? 1.0f / (float)count : (float)(2.0 / count);
     T.slab = w.f.slab;
-    T.counts = f.counts;
-    T.counts_clear = f.counts_next;
-    T.m_dev = f.m_acc;
     T.xys = w.f.xys;
     T.radii = w.f.radii;
     T.rec = w.f.rec;
@@ -1650,42 +1659,50 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     T.det_part = det_part;
     T.det_cap = det_capacity;
     if (carry) {
-        T.counts = w.ccount;
         T.cids = w.cids;
         T.cbox = w.cbox;
-        T.m_clear = f.m_clear;
     }
-    if (g_knobs[5] == 2 && g_debug_ptr && !carry) {  // diagnostic: per-tile stamps
-        T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
-        auto kfn = train_tile_kernel<true>;
-        hipLaunchKernelGGL(kfn, dim3(ntiles), dim3(kT), 0, s, T);
-    } else if (g_knobs[5] == 3 && g_debug_ptr) {  // diagnostic: per-tile stamps, band kernel
-        T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
-        if (carry)
-            hipLaunchKernelGGL((train_tile_band_kernel<true, false, true>), dim3(ntiles), dim3(kBThreads),
-                               0, s, T);
-        else
-            hipLaunchKernelGGL(train_tile_band_kernel<true>, dim3(ntiles), dim3(kBThreads), 0, s, T);
-    } else {
-        // knob 8 = 1: the 256-thread workgroup-per-tile kernel (A/B; atomics only)
-        const bool old_kernel = g_knobs[8] == 1 && !det && !carry;
-        const dim3 grid(ntiles);
-        hipEvent_t tev[2];
-        const int tslot = timing_begin(s, tev, kTimingTrainTile);
-        if (old_kernel)
-            launch_timed(train_tile_kernel<false>, dim3(ntiles), dim3(kT), 0, s, tev, T);
-        else if (det && carry)
-            launch_timed(train_tile_band_kernel<false, true, true>, grid, dim3(kBThreads), 0, s, tev, T);
-        else if (det)
-            launch_timed(train_tile_band_kernel<false, true>, grid, dim3(kBThreads), 0, s, tev, T);
-        else if (carry)
-            launch_timed(train_tile_band_kernel<false, false, true>, grid, dim3(kBThreads), 0, s, tev, T);
-        else
-            launch_timed(train_tile_band_kernel<false>, grid, dim3(kBThreads), 0, s, tev, T);
-        timing_end(s, tslot, kTimingTrainTile);
+    // the tile kernel of the frame whose slots are fs
+    auto launch_tiles = [&](const FrameSlots &fs) {
+        T.counts = carry ? w.ccount : fs.counts;
+        T.counts_clear = fs.counts_next;
+        T.m_dev = fs.m_acc;
+        T.m_clear = carry ? fs.m_clear : nullptr;
+        if (g_knobs[5] == 2 && g_debug_ptr && !carry) {  // diagnostic: per-tile stamps
+            T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
+            auto kfn = train_tile_kernel<true>;
+            hipLaunchKernelGGL(kfn, dim3(ntiles), dim3(kT), 0, s, T);
+        } else if (g_knobs[5] == 3 && g_debug_ptr) {  // diagnostic: per-tile stamps, band kernel
+            T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
+            if (carry)
+                hipLaunchKernelGGL((train_tile_band_kernel<true, false, true>), dim3(ntiles),
+                                   dim3(kBThreads), 0, s, T);
+            else
+                hipLaunchKernelGGL(train_tile_band_kernel<true>, dim3(ntiles), dim3(kBThreads), 0, s, T);
+        } else {
+            // knob 8 = 1: the 256-thread workgroup-per-tile kernel (A/B; atomics only)
+            const bool old_kernel = g_knobs[8] == 1 && !det && !carry;
+            const dim3 grid(ntiles);
+            hipEvent_t tev[2];
+            const int tslot = timing_begin(s, tev, kTimingTrainTile);
+            if (old_kernel)
+                launch_timed(train_tile_kernel<false>, dim3(ntiles), dim3(kT), 0, s, tev, T);
+            else if (det && carry)
+                launch_timed(train_tile_band_kernel<false, true, true>, grid, dim3(kBThreads), 0, s, tev, T);
+            else if (det)
+                launch_timed(train_tile_band_kernel<false, true>, grid, dim3(kBThreads), 0, s, tev, T);
+            else if (carry)
+                launch_timed(train_tile_band_kernel<false, false, true>, grid, dim3(kBThreads), 0, s, tev, T);
+            else
+                launch_timed(train_tile_band_kernel<false>, grid, dim3(kBThreads), 0, s, tev, T);
+            timing_end(s, tslot, kTimingTrainTile);
+        }
+        return check_launch("train_step_sum: tiles");
+    };
+    if (!tiled) {
+        rc = launch_tiles(f);
+        if (rc) return rc;
     }
-    rc = check_launch("train_step_sum: tiles");
-    if (rc) return rc;
 
     TrainSplatArgs P{};
     P.n = num_points;
@@ -1735,6 +1752,7 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     timing_end(s, tslot, kTimingTrainSplat);
     rc = check_launch("train_step_sum: splats");
     if (rc) return rc;
+    if (tiles_next) return launch_tiles(frame_slots(w.f, ntiles, frame_index + 1));
     if (next) return project(frame_slots(w.f, ntiles, frame_index + 1));
     if (!projected && refresh) return splat_order_sort(w.f, num_points, tbx, tby, s);
     return GSVC_OK;

@@ -42,6 +42,20 @@ TRAIN_CARRY = 0x8000  # GSVC_TRAIN_CARRY
 # (GSVC_TRAIN_PROJECT_NEXT).
 CARRY_BINS = True
 CARRY_REBUILD_EVERY = 64
+# Tile kernel ahead (GSVC_TRAIN_TILES_NEXT / GSVC_TRAIN_TILED, with the carried
+# bins): a bound step also enqueues the NEXT iteration's tile kernel (forward,
+# loss, backward: it depends on the parameters this step leaves and on gt, not
+# on the next call's hyper-parameters) against this call's target, so the GPU
+# goes on while the host returns the loss and makes the next call; that call
+# then launches only the splat kernel (Adan with its own hyper-parameters).
+# Used only when the next call passes the same target (same storage, no
+# in-place change) and nothing touched the parameters (PROJECT_AHEAD's checks);
+# otherwise the pending work is discarded by a rebuild.  Enqueued only when
+# this call's target is the previous call's (a caller that alternates targets
+# would discard every time).
+TILES_AHEAD = True
+TRAIN_TILES_NEXT = 0x10000  # GSVC_TRAIN_TILES_NEXT
+TRAIN_TILED = 0x20000  # GSVC_TRAIN_TILED
 
 # A step's projection of the NEXT frame is used only if nothing could have
 # changed the parameters since: no other fused launch on the same parameters
@@ -78,7 +92,10 @@ class _TrainWorkspace:
         self.order_for = None  # (n, H, W) the workspace's splat order was sorted for
         self.order_age = 0     # steps since it was sorted
         self.pending = None    # the projection a bound step enqueued ahead (BoundStep.launch):
-        #                        (weakref to the step, frame, launch count, epoch, versions)
+        #                        (weakref to the step, frame, launch count, epoch, versions,
+        #                        tiles: None or (gt, gt version, background version) of the
+        #                        tile kernel enqueued ahead -- gt held so its storage stays
+        #                        alive and unreused while that kernel may read it)
         self.det_buf = None    # GSVC_TRAIN_DETERMINISTIC workspace
         self.det_cap = 0
         self.carry_age = 0     # steps since the carried bins were rebuilt
@@ -222,7 +239,10 @@ class BoundStep:
         self.det_pairs = 0      # the (splat, tile) pairs its last det step reported
         self.det_overflows = 0  # det steps whose capacity was short (those fell back to atomics)
         self.ahead_steps = 0    # steps that used the projection the previous step enqueued
+        self.tiled_steps = 0    # steps whose tile kernel the previous step enqueued
+        self.last_gt = None     # (data_ptr, version) of the previous launch's target
         self.params = tuple(t for t in (xyz, cholesky, features, rgb_w) if t is not None)
+        self.background = background
 
     def __del__(self):
         if getattr(self, "host", None) is not None:
@@ -277,12 +297,21 @@ class BoundStep:
             adan_flags = int(adan_flags) | TRAIN_DETERMINISTIC
         else:
             a.det_workspace, a.det_workspace_bytes, a.det_capacity = None, 0, 0
+        tiles = None
         if PROJECT_AHEAD:
             versions = tuple(t._version for t in self.params)
             pend = ws.pending
             ahead = (pend is not None and pend[0]() is self and pend[1] == ws.frame
                      and pend[2] == _param_launches.get(a.xyz, 0) and pend[3] == _param_epoch[0]
                      and pend[4] == versions)
+            tiled = False
+            if ahead and pend[5] is not None:
+                # this frame's tile kernel ran against the previous call's target
+                # and background: usable only if they are this call's, unchanged
+                pgt, pver, pbg = pend[5]
+                tiled = (not self.det and pgt.data_ptr() == gt.data_ptr() and gt._version == pver
+                         and pgt._version == pver and self.background._version == pbg)
+                ahead = tiled  # else its gradient sums are in the records: rebuild
             if pend is not None and not ahead:
                 # an enqueued projection that cannot be used: its counts are in
                 # the workspace -- start from zeroed counters
@@ -290,18 +319,29 @@ class BoundStep:
                 ws = _workspace(self.dev, self.n, self.H, self.W)
             carry = TRAIN_CARRY if CARRY_BINS else 0
             if not ahead or (carry and ws.carry_age >= CARRY_REBUILD_EVERY):
+                # (a step that enqueued its successor's tiles never leaves a rebuild due)
                 self._call(ws, lib, gt, int(adan_flags) | TRAIN_PROJECT_ONLY | carry | ws.order_flags())
                 ws.carry_age = 0
+                tiled = False
             if ahead:
                 self.ahead_steps += 1
             ws.carry_age += 1
             flags |= TRAIN_PROJECTED | (carry or TRAIN_PROJECT_NEXT)
+            if tiled:
+                flags |= TRAIN_TILED
+                self.tiled_steps += 1
+            gkey = (gt.data_ptr(), gt._version)
+            if (TILES_AHEAD and carry and not self.det and gkey == self.last_gt
+                    and ws.carry_age < CARRY_REBUILD_EVERY):
+                flags |= TRAIN_TILES_NEXT
+                tiles = (gt, gt._version, self.background._version)
+            self.last_gt = gkey
         self.seq = ((ws.frame + 1) & 0xFFFFFFFF) | 0x80000000
         # the order flags go with a projection (PROJECT_NEXT's or the call's own)
         self._call(ws, lib, gt, flags | (0 if flags & TRAIN_CARRY else ws.order_flags()))
         launches = _note_launch(a.xyz)
         if PROJECT_AHEAD:
-            ws.pending = (weakref.ref(self), ws.frame + 1, launches, _param_epoch[0], versions)
+            ws.pending = (weakref.ref(self), ws.frame + 1, launches, _param_epoch[0], versions, tiles)
         ws.frame += 1
 
     def _call(self, ws, lib, gt, flags):

@@ -380,6 +380,22 @@ int gsvc_render_frame_sum_ex(int num_points, const float *xyz, int xyz_tanh,
  * parameters changed outside the steps, as for GSVC_TRAIN_PROJECT_NEXT, which
  * it excludes. */
 #define GSVC_TRAIN_CARRY 0x8000
+/* Tile kernel ahead (speed only; the same results; with CARRY | PROJECTED and
+ * the Adan update, not with DETERMINISTIC or render_out).
+ * GSVC_TRAIN_TILES_NEXT: after the step, enqueue frame_index + 1's tile kernel
+ * (forward, loss and backward into the workspace's gradient records and tile
+ * errors) against this call's ``gt`` -- it reads the bins and records this
+ * step's splat kernel carried, and none of the next call's hyper-parameters --
+ * so the device starts the next iteration while the host is still returning
+ * this one's loss.  GSVC_TRAIN_TILED: this frame's tile kernel is the one the
+ * previous call enqueued; the call launches the splat kernel (the loss, the
+ * Adan update with this call's hyper-parameters, the carry).  The caller
+ * guarantees that neither the parameters nor gt (nor background) changed
+ * between the two calls; otherwise it discards the pending kernel's work by
+ * rebuilding (re-zeroing the workspace and a PROJECT_ONLY call, which also
+ * zeroes the gradient records). */
+#define GSVC_TRAIN_TILES_NEXT 0x10000
+#define GSVC_TRAIN_TILED 0x20000
 size_t gsvc_train_step_det_workspace_bytes(int num_points, long long det_capacity);
 size_t gsvc_train_step_workspace_bytes(int num_points, unsigned img_height,
                                        unsigned img_width);

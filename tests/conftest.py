@@ -17,6 +17,15 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+def pytest_collection_modifyitems(config, items):
+    # a test that takes the ``cuda`` fixture needs the GPU whether or not it
+    # carries the marker: mark it, so ``-m gpu`` selects it (and ``-m "not gpu"``
+    # does not collect a test that could only skip)
+    for item in items:
+        if "cuda" in getattr(item, "fixturenames", ()) and item.get_closest_marker("gpu") is None:
+            item.add_marker(pytest.mark.gpu)
+
+
 def load_golden(name):
     z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     return {k: z[k] for k in z.files}

@@ -152,6 +152,65 @@ def test_projection_ahead_per_parameter_set(cuda):
         torch.use_deterministic_algorithms(prev, warn_only=prev_warn)
 
 
+def _tiles_run(cuda, tiles, gts, schedule):
+    """20 fused iterations with TILES_AHEAD = tiles; schedule[it] picks the
+    target (an index into gts, or a callable making one); returns the losses,
+    the mse each iteration should report (the render of the parameters it
+    starts from against its target, computed before the call) and the model."""
+    from gsvc_amd import train as Tr
+    from gsvc_amd.frame import make_frame_model
+    old = Tr.TILES_AHEAD
+    Tr.TILES_AHEAD = tiles
+    try:
+        model = make_frame_model(256, 256, 2000, cuda, seed=3)
+        losses, want = [], []
+        for it in range(1, 21):
+            g = schedule.get(it, 0)
+            gt = g() if callable(g) else gts[g]
+            with torch.no_grad():
+                img = model.forward()["render"]  # same bits as the fused forward
+                want.append(float(torch.mean((img - gt) ** 2)))
+            loss, _ = model.train_iter(gt, it)
+            losses.append(float(loss))
+        assert model.fused_steps == 20
+        return np.array(losses), np.array(want), model
+    finally:
+        Tr.TILES_AHEAD = old
+
+
+def test_tiles_ahead_matches_and_honours_target_changes(cuda):
+    """The next iteration's tile kernel, enqueued ahead against the current
+    target, gives the trajectory of launching it in its own call, and its work
+    is discarded when the next call's target differs: another tensor, the same
+    tensor edited in place, a fresh copy each call.  Each iteration's loss is
+    the mse of the render it starts from against ITS target."""
+    from gsvc_amd.frame import synthetic_gt
+    gts = [synthetic_gt(256, 256, 4, cuda), synthetic_gt(256, 256, 9, cuda)]
+    edit = gts[0].clone()
+
+    def edited():
+        edit.mul_(0.97)  # in place: same storage, new _version
+        return edit
+
+    schedule = {6: 1, 7: 1, 8: 0, 11: edited, 12: edited, 13: edited,
+                15: lambda: gts[0].clone(), 16: lambda: gts[0].clone()}
+    la, wa, ma = _tiles_run(cuda, True, gts, schedule)
+    lb, wb, mb = _tiles_run(cuda, False, gts, schedule)
+    # each loss is its own target's (a stale tile kernel would report the old one)
+    np.testing.assert_allclose(la, wa, rtol=2e-5, atol=1e-8)
+    np.testing.assert_allclose(lb, wb, rtol=2e-5, atol=1e-8)
+    # float atomics in the backward: equal up to their summation order
+    np.testing.assert_allclose(la, lb, rtol=2e-5, atol=1e-8)
+    np.testing.assert_allclose(ma._xyz.detach().cpu().numpy(), mb._xyz.detach().cpu().numpy(),
+                               rtol=1e-3, atol=1e-4)
+    bs = ma._bound_step
+    assert mb._bound_step.tiled_steps == 0
+    # tiled: an iteration whose target is its predecessor's, which in turn
+    # repeated the target before it (3-5, 10, 19-20); the edited and fresh-copy
+    # targets never match
+    assert bs.tiled_steps == 6, bs.tiled_steps
+
+
 def test_projection_ahead_matches_and_honours_edits(cuda):
     """The fused step's projection of the next frame, enqueued ahead, gives the
     same trajectory as projecting at the start of each step, and is discarded
