@@ -186,16 +186,19 @@ def test_tiles_ahead_matches_and_honours_target_changes(cuda):
     the mse of the render it starts from against ITS target."""
     from gsvc_amd.frame import synthetic_gt
     gts = [synthetic_gt(256, 256, 4, cuda), synthetic_gt(256, 256, 9, cuda)]
-    edit = gts[0].clone()
 
-    def edited():
-        edit.mul_(0.97)  # in place: same storage, new _version
-        return edit
+    def schedule():  # a fresh edited target per run
+        edit = gts[0].clone()
 
-    schedule = {6: 1, 7: 1, 8: 0, 11: edited, 12: edited, 13: edited,
+        def edited():
+            edit.mul_(0.97)  # in place: same storage, new _version
+            return edit
+
+        return {6: 1, 7: 1, 8: 0, 11: edited, 12: edited, 13: edited,
                 15: lambda: gts[0].clone(), 16: lambda: gts[0].clone()}
-    la, wa, ma = _tiles_run(cuda, True, gts, schedule)
-    lb, wb, mb = _tiles_run(cuda, False, gts, schedule)
+
+    la, wa, ma = _tiles_run(cuda, True, gts, schedule())
+    lb, wb, mb = _tiles_run(cuda, False, gts, schedule())
     # each loss is its own target's (a stale tile kernel would report the old one)
     np.testing.assert_allclose(la, wa, rtol=2e-5, atol=1e-8)
     np.testing.assert_allclose(lb, wb, rtol=2e-5, atol=1e-8)
