@@ -1273,6 +1273,7 @@ struct TrainSplatArgs {
     unsigned *ccount;
     int *cids;
     int *m_next;
+    long long *stamps;  // diagnostic: int64[waves][8]
 };
 
 // GSVC_TRAIN_CARRY: splat i's projection for the next frame from its updated
@@ -1300,9 +1301,12 @@ __device__ __forceinline__ int carry_splat(const TrainSplatArgs &A, int i, const
     A.rec[3 * i + 2] = S.r2;
     A.xys[i] = S.P.xy;
     A.radii[i] = S.P.rad;
+    // the record's first 32 bytes (v_xy, v_conic, v_colors: what the tile
+    // kernel adds and this kernel reads; v_opacity and the padding stay as a
+    // projection zeroed them -- nothing in the fused step writes them)
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) A.grad[4 * i + q] = z;
+    A.grad[4 * i] = z;
+    A.grad[4 * i + 1] = z;
     unsigned x0 = 0, y0 = 0, x1 = 0, y1 = 0;
     if (S.P.rad > 0) tile_bbox(S.P.xy.x, S.P.xy.y, (float)S.P.rad, A.tbx, A.tby, x0, y0, x1, y1);
     const uint2 nb = pack_box(x0, y0, x1, y1);
@@ -1326,9 +1330,54 @@ __device__ __forceinline__ int carry_splat(const TrainSplatArgs &A, int i, const
     return (int)((x1 - x0) * (y1 - y0));
 }
 
+// Row i of a [N, C] float tensor (C = 1, 2, 3) as one vector access.
+struct Row3 {
+    float x, y, z;
+};
+template <int C>
+__device__ __forceinline__ void ld_row(const float *base, int i, float *out) {
+    const float *p = base + (size_t)C * (size_t)i;
+    if constexpr (C == 2) {
+        const float2 t = *reinterpret_cast<const float2 *>(p);
+        out[0] = t.x;
+        out[1] = t.y;
+    } else if constexpr (C == 3) {
+        const Row3 t = *reinterpret_cast<const Row3 *>(p);
+        out[0] = t.x;
+        out[1] = t.y;
+        out[2] = t.z;
+    } else {
+        out[0] = p[0];
+    }
+}
+template <int C>
+__device__ __forceinline__ void st_row(float *base, int i, const float *in) {
+    float *p = base + (size_t)C * (size_t)i;
+    if constexpr (C == 2) {
+        *reinterpret_cast<float2 *>(p) = make_float2(in[0], in[1]);
+    } else if constexpr (C == 3) {
+        *reinterpret_cast<Row3 *>(p) = Row3{in[0], in[1], in[2]};
+    } else {
+        p[0] = in[0];
+    }
+}
+
+// Diagnostic (gsvc_debug_set(5, 4) with gsvc_debug_set_ptr): s_memrealtime
+// stamps per wave by lane 0 -- start, operands landed, Adan stores issued,
+// carry done, M added, stores acknowledged -- as int64[8] at st.
+__device__ __forceinline__ void splat_stamp(long long *st, int k) {
+    if (st) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const long long t = tstamp();
+        if ((threadIdx.x & 63) == 0) st[k] = t;
+    }
+}
+
 // One splat's step: the projection VJP, activation VJPs and the Adan update of
-// its elements (update == 0: the gradients into grads_out).
-__device__ __forceinline__ int splat_step(const TrainSplatArgs &A, int i) {
+// its elements (update == 0: the gradients into grads_out).  st: stamps
+// (kStamp instances only).
+template <bool kStamp>
+__device__ __forceinline__ int splat_step(const TrainSplatArgs &A, int i, long long *st) {
     // Every operand is loaded up front, before any arithmetic: one round trip
     // per lane instead of three (gradient + radius -> record -> Adan state).
     // rec is written for every splat by the projection, so its load needs no
@@ -1356,19 +1405,32 @@ __device__ __forceinline__ int splat_step(const TrainSplatArgs &A, int i) {
     const float w = A.rgbw ? A.rgbw[i] : 1.0f;
     // the carry's hull, with the other operands (not a round trip after the update)
     const uint2 hull = A.carry ? A.chull[i] : make_uint2(0u, 0u);
+    if (kStamp) splat_stamp(st, 1);
     const bool upd = A.update != 0;
+    // Adan state rows, one vector access per (tensor, splat): xyz e 0-1, cholesky
+    // 2-4, features 5-7, rgb_W 8 (a row of 2 or 3 floats is one dwordx2 / x3)
     float m[9], v[9], df[9], npg[9];
 #pragma unroll
-    for (int e = 0; e < 9; ++e) {
-        const int q = e < 2 ? 0 : (e < 5 ? 1 : (e < 8 ? 2 : 3));
-        m[e] = v[e] = df[e] = npg[e] = 0.0f;
-        if (!upd || (q == 3 && !A.rgbw_train)) continue;
-        const size_t j = q == 0 ? 2 * (size_t)i + e : (q == 1 ? 3 * (size_t)i + (e - 2)
-                                                  : (q == 2 ? 3 * (size_t)i + (e - 5) : (size_t)i));
-        m[e] = A.state[q][0][j];
-        v[e] = A.state[q][1][j];
-        df[e] = A.state[q][2][j];
-        npg[e] = A.state[q][3][j];
+    for (int e = 0; e < 9; ++e) m[e] = v[e] = df[e] = npg[e] = 0.0f;
+    if (upd) {
+        ld_row<2>(A.state[0][0], i, m);
+        ld_row<2>(A.state[0][1], i, v);
+        ld_row<2>(A.state[0][2], i, df);
+        ld_row<2>(A.state[0][3], i, npg);
+        ld_row<3>(A.state[1][0], i, m + 2);
+        ld_row<3>(A.state[1][1], i, v + 2);
+        ld_row<3>(A.state[1][2], i, df + 2);
+        ld_row<3>(A.state[1][3], i, npg + 2);
+        ld_row<3>(A.state[2][0], i, m + 5);
+        ld_row<3>(A.state[2][1], i, v + 5);
+        ld_row<3>(A.state[2][2], i, df + 5);
+        ld_row<3>(A.state[2][3], i, npg + 5);
+        if (A.rgbw_train) {
+            ld_row<1>(A.state[3][0], i, m + 8);
+            ld_row<1>(A.state[3][1], i, v + 8);
+            ld_row<1>(A.state[3][2], i, df + 8);
+            ld_row<1>(A.state[3][3], i, npg + 8);
+        }
     }
     // 2D projection VJP, backward2d.cu:8-51 (the op's project2d_bwd_kernel sequence)
     float vl0 = 0.f, vl1 = 0.f, vl2 = 0.f, vmx = 0.f, vmy = 0.f;
@@ -1425,33 +1487,59 @@ __device__ __forceinline__ int splat_step(const TrainSplatArgs &A, int i) {
         pnew[e] = pin[e];
         if (q == 3 && !A.rgbw_train) continue;
         if (A.first[q]) npg[e] = -(g[e] * A.S.clip);
-        const float pv = adan_update(A.S, pin[e], g[e], m[e], v[e], df[e], npg[e]);
-        pnew[e] = pv;
-        const size_t j = q == 0 ? 2 * (size_t)i + e : (q == 1 ? 3 * (size_t)i + (e - 2)
-                                                  : (q == 2 ? 3 * (size_t)i + (e - 5) : (size_t)i));
-        float *param = q == 0 ? A.xyz : (q == 1 ? A.chol : (q == 2 ? A.feat : A.rgbw));
-        param[j] = pv;
-        A.state[q][0][j] = m[e];
-        A.state[q][1][j] = v[e];
-        A.state[q][2][j] = df[e];
-        A.state[q][3][j] = npg[e];
+        pnew[e] = adan_update(A.S, pin[e], g[e], m[e], v[e], df[e], npg[e]);
     }
-    return A.carry ? carry_splat(A, i, pnew, hull) : 0;
+    // the rows back, one vector store per (tensor, splat)
+    st_row<2>(A.xyz, i, pnew);
+    st_row<2>(A.state[0][0], i, m);
+    st_row<2>(A.state[0][1], i, v);
+    st_row<2>(A.state[0][2], i, df);
+    st_row<2>(A.state[0][3], i, npg);
+    st_row<3>(A.chol, i, pnew + 2);
+    st_row<3>(A.state[1][0], i, m + 2);
+    st_row<3>(A.state[1][1], i, v + 2);
+    st_row<3>(A.state[1][2], i, df + 2);
+    st_row<3>(A.state[1][3], i, npg + 2);
+    st_row<3>(A.feat, i, pnew + 5);
+    st_row<3>(A.state[2][0], i, m + 5);
+    st_row<3>(A.state[2][1], i, v + 5);
+    st_row<3>(A.state[2][2], i, df + 5);
+    st_row<3>(A.state[2][3], i, npg + 5);
+    if (A.rgbw_train) {
+        st_row<1>(A.rgbw, i, pnew + 8);
+        st_row<1>(A.state[3][0], i, m + 8);
+        st_row<1>(A.state[3][1], i, v + 8);
+        st_row<1>(A.state[3][2], i, df + 8);
+        st_row<1>(A.state[3][3], i, npg + 8);
+    }
+    if (kStamp) splat_stamp(st, 2);
+    const int hits = A.carry ? carry_splat(A, i, pnew, hull) : 0;
+    if (kStamp) splat_stamp(st, 3);
+    return hits;
 }
 
+template <bool kStamp>
 __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
+    long long *st = kStamp ? A.stamps + 8 * (size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6))
+                           : nullptr;
+    if (kStamp && (threadIdx.x & 63) == 0) st[0] = tstamp();
     if (blockIdx.x == 0) {
         // the first workgroup (no splats): the loss; dispatched first so it
         // runs beside the splats
         __shared__ double s_l[2][4];
         publish_loss<256>(A.err, A.ntiles, A.inv_count, A.loss, A.loss_seq, A.det_off, A.n, s_l);
+        if (kStamp) splat_stamp(st, 5);
         return;
     }
     const int t = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
-    const int hits = t < A.n ? splat_step(A, t) : 0;
+    const int hits = t < A.n ? splat_step<kStamp>(A, t, st) : 0;
     if (A.carry) {
         __shared__ int s_hits[4];
         add_hits(hits, s_hits, A.m_next);  // the next frame's M
+    }
+    if (kStamp) {
+        if ((threadIdx.x & 63) == 0) st[4] = tstamp();
+        splat_stamp(st, 5);
     }
 }
 
@@ -1748,7 +1836,12 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     const int blocks = (num_points > 0 ? ceil_div(num_points, 256) : 0) + 1;
     hipEvent_t tev[2];
     const int tslot = timing_begin(s, tev, kTimingTrainSplat);
-    launch_timed(train_splat_kernel, dim3(blocks), dim3(256), 0, s, tev, P);
+    if (g_knobs[5] == 4 && g_debug_ptr) {  // diagnostic: per-wave stamps of the splat kernel
+        P.stamps = reinterpret_cast<long long *>(g_debug_ptr);
+        hipLaunchKernelGGL(train_splat_kernel<true>, dim3(blocks), dim3(256), 0, s, P);
+    } else {
+        launch_timed(train_splat_kernel<false>, dim3(blocks), dim3(256), 0, s, tev, P);
+    }
     timing_end(s, tslot, kTimingTrainSplat);
     rc = check_launch("train_step_sum: splats");
     if (rc) return rc;

@@ -37,6 +37,8 @@ def main():
                     help="with --stamps: save the raw per-tile stamps (us, tile order) as npz")
     ap.add_argument("--proj-stamps", action="store_true",
                     help="also stamp the projection kernel's waves (start, projected, inserted, end)")
+    ap.add_argument("--splat-stamps", action="store_true",
+                    help="also stamp the splat kernel's waves (start, operands, Adan, carry, M, end)")
     ap.add_argument("--order-every", type=int, default=None,
                     help="steps between splat-order sorts (gsvc_amd.train.ORDER_REFRESH_EVERY; 0: none)")
     ap.add_argument("--frozen", type=int, default=0,
@@ -151,6 +153,30 @@ def main():
                               slab_stores=q((t[:, 7] - t[:, 6])[t[:, 6] > 0]),
                               windowed_waves=int((t[:, 6] > 0).sum()),
                               end=q(t[:, 3] - t0))), flush=True)
+    if a.splat_stamps:
+        import ctypes
+        import numpy as np
+        from gsvc_amd import _lib as L
+        lib = L.load()
+        st = torch.zeros(((a.splats + 255) // 256 * 4 + 8, 8), dtype=torch.int64, device=dev)
+        lib.gsvc_debug_set_ptr(ctypes.c_void_p(st.data_ptr()))
+        lib.gsvc_debug_set(5, 4)
+        model.train_iter(gt, a.warmup + a.iters + 400)
+        torch.cuda.synchronize()
+        lib.gsvc_debug_set(5, 0)
+        lib.gsvc_debug_set_ptr(None)
+        t = st.cpu().numpy().astype(np.float64) * 0.01
+        loss_wg = t[:4]
+        t = t[4:]
+        t = t[t[:, 5] > 0]
+        t0 = min(t[:, 0].min(), loss_wg[loss_wg[:, 0] > 0][:, 0].min())
+        q = lambda x: [round(float(np.percentile(x, p)), 2) for p in (0, 10, 50, 90, 100)]  # noqa
+        print(json.dumps(dict(splat_stamps="percentiles 0/10/50/90/100 (us)", waves=int(len(t)),
+                              start=q(t[:, 0] - t0), operands=q(t[:, 1] - t[:, 0]),
+                              adan=q(t[:, 2] - t[:, 1]), carry=q(t[:, 3] - t[:, 2]),
+                              m_add=q(t[:, 4] - t[:, 3]), drain=q(t[:, 5] - t[:, 4]),
+                              end=q(t[:, 5] - t0),
+                              loss_wg_end=round(float(loss_wg[:, 5].max() - t0), 2))), flush=True)
     if a.stamps:
         import ctypes
         import numpy as np
