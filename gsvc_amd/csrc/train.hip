@@ -746,13 +746,20 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
         r1 = h0[1];
         r2 = h0[2];
     }
-    float gt[3][2];
+    // the pair's targets go straight into LDS (global_load_lds: no VGPRs held
+    // over the order and forward phases -- held in registers they spilled, and
+    // the spill's vmcnt(0) cost the carried-bins kernel a round trip), into the
+    // v_out planes' space, [wave][c][q][lane], which the loss phase overwrites
+    // only after every wave has read its targets back
+    float *sgt = &S.v[0][0] + w * (6 * 64);
     {
+        typedef __attribute__((address_space(1))) void gvoid;
+        typedef __attribute__((address_space(3))) void lvoid;
         const size_t b0 = nin > 0 ? pix0 : 0, b1 = nin > 1 ? pix0 + 1 : b0;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            gt[c][0] = A.gt[c * hw + b0];
-            gt[c][1] = A.gt[c * hw + b1];
+            __builtin_amdgcn_global_load_lds((gvoid *)(A.gt + c * hw + b0), (lvoid *)(sgt + (2 * c) * 64), 4, 0, 0);
+            __builtin_amdgcn_global_load_lds((gvoid *)(A.gt + c * hw + b1), (lvoid *)(sgt + (2 * c + 1) * 64), 4, 0, 0);
         }
     }
     const bool empty = m_frame < 1;  // rasterize_sum.py:121-127: background, no gradient
@@ -1001,6 +1008,13 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     // clamp backward (passes where 0 <= out <= 1), error sums; v_out planes
     {
         const float o[3][2] = {{ar.x, ar.y}, {ag.x, ag.y}, {ab.x, ab.y}};
+        float gt[3][2];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the targets' global_load_lds
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            gt[c][0] = sgt[(2 * c) * 64 + lane];
+            gt[c][1] = sgt[(2 * c + 1) * 64 + lane];
+        }
         float se = 0.f, ae = 0.f;
         float v[3][2];
 #pragma unroll
@@ -1028,6 +1042,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                 for (int q = 0; q < nin; ++q) A.out[c * hw + pix0 + q] = clamp_unit(o[c][q]);
         }
         const int p = prow * kVRow + pcol;
+        __syncthreads();  // every wave has its targets: the planes take v_out
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             S.v[c][p] = v[c][0];
