@@ -30,6 +30,8 @@ _SIGS = {
     "gsvc_last_error": [],
     "gsvc_debug_set": [_I, _I],
     "gsvc_debug_set_ptr": [_P],
+    "gsvc_alpha_cut_bits": [],
+    "gsvc_alpha_cut_scan": [_P, _P],
     "gsvc_stream_sync": [_P],
     "gsvc_host_alloc": [_SZ],
     "gsvc_host_free": [_P],
@@ -93,6 +95,7 @@ _SIGS = {
 }
 _RESTYPE = {
     "gsvc_debug_set_ptr": None,
+    "gsvc_alpha_cut_bits": _U,
     "gsvc_host_alloc": _P,
     "gsvc_last_error": ctypes.c_char_p,
     "gsvc_cumsum_workspace_bytes": _SZ,

@@ -18,6 +18,12 @@ constexpr int kTile = 16;          // BLOCK_X = BLOCK_Y (reference config.h:1-2)
 constexpr int kTilePix = 256;      // BLOCK_SIZE (config.h:3): entries blended per tile
 constexpr float kNegLog2e = -1.4426950408889634f;
 constexpr float kAlphaMin = 1.0f / 255.0f;
+// At unit opacity the reference's alpha cut (forward.cu:598-606:
+// !(sigma < 0) && !(min(1, exp(-sigma)) < 1/255)) keeps exactly the sigma
+// whose float bits lie in [0, kSigmaCutBits], and exp(-sigma) <= 1 there
+// (alpha_cut.hip proves both on the device over every float; a NaN sigma is
+// the exception -- see there).
+constexpr unsigned kSigmaCutBits = 0x40b15208u;  // sigma 5.5412636 (gfx950 v_exp_f32, tests/test_alpha_cut.py)
 
 // Host-side error plumbing -------------------------------------------------
 int set_error(int code, const char *fmt, ...);

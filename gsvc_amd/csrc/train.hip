@@ -25,6 +25,8 @@
 //       doubled L cross term), activation VJPs and the Adan update of every
 //       parameter element; an extra first workgroup sums the tiles' errors in
 //       a fixed order into the loss.
+#include <type_traits>
+
 #include "adan.h"
 #include "binning.h"
 #include "frame.h"
@@ -514,6 +516,33 @@ __device__ __forceinline__ void blend2_unit_fin(float gx, float ha, float bdy, f
     ab = __builtin_elementwise_fma((v2f)cb, av, ab);
 }
 
+// blend2_unit_fin with the alpha cut as a sigma threshold (common.h
+// kSigmaCutBits: the same pairs pass, and alpha = exp(-sigma) <= 1 for them,
+// so the min(1, .) goes too) -- for entries whose colour AND geometry are
+// finite (sigma then is never NaN, the one value the threshold decides
+// differently).  The same bits as blend2_unit_fin.
+__device__ __forceinline__ void blend2_cut(float gx, float ha, float bdy, float cq, float cr,
+                                           float cg, float cb, v2f px, v2f &ar, v2f &ag, v2f &ab) {
+    const v2f dx = gx - px;
+    const v2f q = __builtin_elementwise_fma((v2f)ha, dx, (v2f)bdy);
+    const v2f sg = __builtin_elementwise_fma(q, dx, (v2f)cq);
+    const v2f x = sg * kNegLog2e;
+    const v2f e = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+    const bool v0 = __float_as_uint(sg.x) <= kSigmaCutBits;
+    const bool v1 = __float_as_uint(sg.y) <= kSigmaCutBits;
+    const v2f av = {v0 ? e.x : 0.0f, v1 ? e.y : 0.0f};
+    ar = __builtin_elementwise_fma((v2f)cr, av, ar);
+    ag = __builtin_elementwise_fma((v2f)cg, av, ag);
+    ab = __builtin_elementwise_fma((v2f)cb, av, ab);
+}
+
+// An entry's geometry (x, y, a/2, b; c/2) is finite: its sigma is then never
+// NaN, and the sigma-threshold alpha cut (kSigmaCutBits) applies.
+__device__ __forceinline__ bool geo_finite(const float4 &G, float hc) {
+    return __builtin_isfinite(G.x) && __builtin_isfinite(G.y) && __builtin_isfinite(G.z) &&
+           __builtin_isfinite(G.w) && __builtin_isfinite(hc);
+}
+
 // Inclusive scans over one wave's 64 lanes with DPP (no LDS traffic):
 // row_shr 1, 2, 4, 8 inside each 16-lane row, then row_bcast 15 / 31 carry a
 // row's last lane into the rows above; ``id`` is the operation's identity.
@@ -904,7 +933,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             // The pairs skipped contribute nothing (the band culling's own
             // argument), so every pixel sees the same sequence of blends.
             unsigned gm = 0u;
-            bool fin = false;
+            bool fin = false, cutok = false;
             if (lane < cnt) {
                 const unsigned rc = S.ro[lane];
                 if (rc != kNoRect) {
@@ -917,6 +946,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                 }
                 const float4 C = S.col[lane];
                 fin = __builtin_isfinite(C.y) && __builtin_isfinite(C.z) && __builtin_isfinite(C.w);
+                cutok = fin && geo_finite(S.geo[lane], C.x);
             }
             if (A.diag & 4) gm = 0u;  // diagnostic: no forward blending (wrong results)
             // row `lane` of the lists: the sentinel, then the entries
@@ -933,9 +963,21 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             }
             const unsigned long long any = __ballot(gm != 0u);
             const unsigned long long fm = __ballot(fin);
+            const unsigned long long cm = __ballot(cutok);
             __builtin_amdgcn_wave_barrier();
             const unsigned char *ml = wlist + grp;
-            if ((any & ~fm) == 0) {
+            if ((any & ~cm) == 0) {
+                // finite colours and geometry (the rule): the threshold cut
+                for (int it = 0; it < maxlen; ++it) {
+                    const int k = ml[8 * it];
+                    const float4 G = S.geo[k];
+                    const float4 C = S.col[k];
+                    const float dy = G.y - py;
+                    const float cq = (C.x * dy) * dy;
+                    const float bdy = G.w * dy;
+                    blend2_cut(G.x, G.z, bdy, cq, C.y, C.z, C.w, px, ar, ag, ab);
+                }
+            } else if ((any & ~fm) == 0) {
                 for (int it = 0; it < maxlen; ++it) {
                     const int k = ml[8 * it];
                     const float4 G = S.geo[k];
@@ -1123,6 +1165,9 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             wperm[rank] = (signed char)lane;
         }
         __builtin_amdgcn_wave_barrier();
+        // the chunk's geometry finite: the backward's alpha cut by threshold
+        const bool bcut =
+            __ballot(lane < gn && !geo_finite(S.geo[lane], S.col[lane].x)) == 0ull;
         const int ent = wperm[lane];  // the entry in sorted slot `lane`
         const int sitems = __shfl(items, ent, 64);
         const int incl = wave_scan_dpp<false>(sitems, 0);
@@ -1175,22 +1220,37 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                     const float *vp = &S.v[0][0] + row * kVRow + cs;
                     const float *const ve = &S.v[0][0] + row * kVRow + ce;
                     float dx = ex - (tx0 + (float)cs);
-                    for (; vp <= ve; ++vp, dx -= 1.0f) {
-                        const float Px = vp[0], Py = vp[kTile * kVRow], Pz = vp[2 * kTile * kVRow];
-                        const float sgm = fmaf(fmaf(eha, dx, bdy), dx, cq);
-                        const float vis = exp_neg(sgm);
-                        const float al = fminf(1.0f, vis);  // opacity 1
-                        if (sgm < 0.0f || al < kAlphaMin) continue;
-                        const float v_alpha = fmaf(C.w, Pz, fmaf(C.z, Py, C.y * Px));
-                        const float v_sigma = (-vis) * v_alpha;  // (-opacity * vis) * v_alpha
-                        g[5] = fmaf(al, Px, g[5]);
-                        g[6] = fmaf(al, Py, g[6]);
-                        g[7] = fmaf(al, Pz, g[7]);
-                        s0 += v_sigma;
-                        const float vdx = v_sigma * dx;
-                        s1 += vdx;
-                        s2 = fmaf(vdx, dx, s2);
-                    }
+                    // kCut: the chunk's geometry is finite, so the alpha cut is
+                    // the sigma threshold and alpha = vis (kSigmaCutBits); else
+                    // the reference's test as written
+                    auto walk = [&](auto kcut) {
+                        for (; vp <= ve; ++vp, dx -= 1.0f) {
+                            const float Px = vp[0], Py = vp[kTile * kVRow], Pz = vp[2 * kTile * kVRow];
+                            const float sgm = fmaf(fmaf(eha, dx, bdy), dx, cq);
+                            const float vis = exp_neg(sgm);
+                            float al;
+                            if constexpr (decltype(kcut)::value) {
+                                if (__float_as_uint(sgm) > kSigmaCutBits) continue;
+                                al = vis;
+                            } else {
+                                al = fminf(1.0f, vis);  // opacity 1
+                                if (sgm < 0.0f || al < kAlphaMin) continue;
+                            }
+                            const float v_alpha = fmaf(C.w, Pz, fmaf(C.z, Py, C.y * Px));
+                            const float v_sigma = (-vis) * v_alpha;  // (-opacity * vis) * v_alpha
+                            g[5] = fmaf(al, Px, g[5]);
+                            g[6] = fmaf(al, Py, g[6]);
+                            g[7] = fmaf(al, Pz, g[7]);
+                            s0 += v_sigma;
+                            const float vdx = v_sigma * dx;
+                            s1 += vdx;
+                            s2 = fmaf(vdx, dx, s2);
+                        }
+                    };
+                    if (bcut)
+                        walk(std::true_type{});
+                    else
+                        walk(std::false_type{});
                     const float hdy = 0.5f * dy;
                     g[0] = fmaf(2.0f * eha, s1, bdy * s0);
                     g[1] = fmaf(eb, s1, ((2.0f * C.x) * dy) * s0);

@@ -97,6 +97,13 @@ int gsvc_timing_collect_channel(int channel, float *ms, int max_out, int *count)
  * mode 6; returns the previous value.  Not part of the reference interface;
  * results are identical for every value (modes 4/5 are ablations). */
 int gsvc_debug_set(int key, int value);
+/* The unit-opacity alpha cut as a sigma threshold (alpha_cut.hip): the
+ * kernels' constant, and a device scan over all 2^31 non-negative float
+ * patterns of the reference predicate (forward.cu:598-606 at opacity 1) into
+ * out[4] (device memory) = {largest kept, smallest dropped, kept with
+ * exp(-sigma) > 1, kept NaN patterns}.  Test hooks; not part of the reference. */
+unsigned gsvc_alpha_cut_bits(void);
+int gsvc_alpha_cut_scan(unsigned *out, void *stream);
 
 /* hipStreamSynchronize(stream): the fused training step writes its losses
  * into caller memory that may be pinned host memory; the caller waits with
