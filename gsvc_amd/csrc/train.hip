@@ -1742,9 +1742,15 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     // kernel is that one (the call launches the splat kernel only)
     const bool tiled = (adan_flags & GSVC_TRAIN_TILED) != 0;
     const bool tiles_next = (adan_flags & GSVC_TRAIN_TILES_NEXT) != 0;
+    // GSVC_TRAIN_REBUILD_NEXT (with TILES_NEXT): before that tile kernel, rebuild
+    // frame_index + 1's bins from scratch (the PROJECT_ONLY | CARRY projection;
+    // the order flags apply to it), so the periodic rebuild costs no host gap
+    const bool rebuild_next = (adan_flags & GSVC_TRAIN_REBUILD_NEXT) != 0;
     if ((tiled || tiles_next) && (!carry || !projected || !update || det || render_out))
         return set_error(GSVC_ERR_ARG, "train_step_sum: TILED / TILES_NEXT need CARRY | PROJECTED, "
                                        "the Adan update, no render_out and no DETERMINISTIC");
+    if (rebuild_next && !tiles_next)
+        return set_error(GSVC_ERR_ARG, "train_step_sum: REBUILD_NEXT needs TILES_NEXT");
     int *det_off = nullptr;
     float4 *det_part = nullptr;
     if (det) {
@@ -1920,7 +1926,26 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     timing_end(s, tslot, kTimingTrainSplat);
     rc = check_launch("train_step_sum: splats");
     if (rc) return rc;
-    if (tiles_next) return launch_tiles(frame_slots(w.f, ntiles, frame_index + 1));
+    if (tiles_next) {
+        const FrameSlots fn = frame_slots(w.f, ntiles, frame_index + 1);
+        if (rebuild_next) {
+            // the splat kernel's carry is superseded: counts and M from zero,
+            // then the projection bins frame_index + 1 afresh (and re-zeroes the
+            // gradient records)
+            if (hipMemsetAsync(w.ccount, 0, sizeof(unsigned) * (size_t)ntiles, s) != hipSuccess ||
+                hipMemsetAsync(fn.m_acc, 0, sizeof(int), s) != hipSuccess)
+                return set_error(GSVC_ERR_HIP, "train_step_sum: memset failed");
+            rc = frame_project_launch(num_points, xyz, 1, cholesky, cholesky_bound, features, rgb_w,
+                                      nullptr, img_height, img_width, w.f, fn, w.grad, s, 1, nullptr, 0,
+                                      &ord);
+            if (rc) return rc;
+            if (refresh) {
+                rc = splat_order_sort(w.f, num_points, tbx, tby, s);
+                if (rc) return rc;
+            }
+        }
+        return launch_tiles(fn);
+    }
     if (next) return project(frame_slots(w.f, ntiles, frame_index + 1));
     if (!projected && refresh) return splat_order_sort(w.f, num_points, tbx, tby, s);
     return GSVC_OK;

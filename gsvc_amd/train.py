@@ -56,6 +56,7 @@ CARRY_REBUILD_EVERY = 64
 TILES_AHEAD = True
 TRAIN_TILES_NEXT = 0x10000  # GSVC_TRAIN_TILES_NEXT
 TRAIN_TILED = 0x20000  # GSVC_TRAIN_TILED
+TRAIN_REBUILD_NEXT = 0x40000  # GSVC_TRAIN_REBUILD_NEXT
 
 # A step's projection of the NEXT frame is used only if nothing could have
 # changed the parameters since: no other fused launch on the same parameters
@@ -298,6 +299,7 @@ class BoundStep:
         else:
             a.det_workspace, a.det_workspace_bytes, a.det_capacity = None, 0, 0
         tiles = None
+        order = 0  # the order flags of a REBUILD_NEXT projection
         if PROJECT_AHEAD:
             versions = tuple(t._version for t in self.params)
             pend = ws.pending
@@ -331,14 +333,20 @@ class BoundStep:
                 flags |= TRAIN_TILED
                 self.tiled_steps += 1
             gkey = (gt.data_ptr(), gt._version)
-            if (TILES_AHEAD and carry and not self.det and gkey == self.last_gt
-                    and ws.carry_age < CARRY_REBUILD_EVERY):
+            if TILES_AHEAD and carry and not self.det and gkey == self.last_gt:
                 flags |= TRAIN_TILES_NEXT
                 tiles = (gt, gt._version, self.background._version)
+                if ws.carry_age >= CARRY_REBUILD_EVERY:
+                    # the next frame's bins are rebuilt behind this step, not at
+                    # the start of the next call
+                    flags |= TRAIN_REBUILD_NEXT
+                    order = ws.order_flags()
+                    ws.carry_age = 0
             self.last_gt = gkey
         self.seq = ((ws.frame + 1) & 0xFFFFFFFF) | 0x80000000
-        # the order flags go with a projection (PROJECT_NEXT's or the call's own)
-        self._call(ws, lib, gt, flags | (0 if flags & TRAIN_CARRY else ws.order_flags()))
+        # the order flags go with a projection (PROJECT_NEXT's, REBUILD_NEXT's or
+        # the call's own)
+        self._call(ws, lib, gt, flags | (order if flags & TRAIN_CARRY else ws.order_flags()))
         launches = _note_launch(a.xyz)
         if PROJECT_AHEAD:
             ws.pending = (weakref.ref(self), ws.frame + 1, launches, _param_epoch[0], versions, tiles)

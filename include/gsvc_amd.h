@@ -403,6 +403,11 @@ int gsvc_render_frame_sum_ex(int num_points, const float *xyz, int xyz_tanh,
  * zeroes the gradient records). */
 #define GSVC_TRAIN_TILES_NEXT 0x10000
 #define GSVC_TRAIN_TILED 0x20000
+/* GSVC_TRAIN_REBUILD_NEXT (with TILES_NEXT): rebuild frame_index + 1's carried
+ * bins from scratch (the PROJECT_ONLY | CARRY projection of the updated
+ * parameters; the order flags apply to it) before enqueueing its tile kernel --
+ * the periodic rebuild without a host round trip. */
+#define GSVC_TRAIN_REBUILD_NEXT 0x40000
 size_t gsvc_train_step_det_workspace_bytes(int num_points, long long det_capacity);
 size_t gsvc_train_step_workspace_bytes(int num_points, unsigned img_height,
                                        unsigned img_width);

@@ -152,15 +152,17 @@ def test_projection_ahead_per_parameter_set(cuda):
         torch.use_deterministic_algorithms(prev, warn_only=prev_warn)
 
 
-def _tiles_run(cuda, tiles, gts, schedule):
+def _tiles_run(cuda, tiles, gts, schedule, rebuild_every=None):
     """20 fused iterations with TILES_AHEAD = tiles; schedule[it] picks the
     target (an index into gts, or a callable making one); returns the losses,
     the mse each iteration should report (the render of the parameters it
     starts from against its target, computed before the call) and the model."""
     from gsvc_amd import train as Tr
     from gsvc_amd.frame import make_frame_model
-    old = Tr.TILES_AHEAD
+    old = Tr.TILES_AHEAD, Tr.CARRY_REBUILD_EVERY
     Tr.TILES_AHEAD = tiles
+    if rebuild_every is not None:
+        Tr.CARRY_REBUILD_EVERY = rebuild_every
     try:
         model = make_frame_model(256, 256, 2000, cuda, seed=3)
         losses, want = [], []
@@ -175,7 +177,7 @@ def _tiles_run(cuda, tiles, gts, schedule):
         assert model.fused_steps == 20
         return np.array(losses), np.array(want), model
     finally:
-        Tr.TILES_AHEAD = old
+        Tr.TILES_AHEAD, Tr.CARRY_REBUILD_EVERY = old
 
 
 def test_tiles_ahead_matches_and_honours_target_changes(cuda):
@@ -212,6 +214,22 @@ def test_tiles_ahead_matches_and_honours_target_changes(cuda):
     # repeated the target before it (3-5, 10, 19-20); the edited and fresh-copy
     # targets never match
     assert bs.tiled_steps == 6, bs.tiled_steps
+
+
+def test_tiles_ahead_with_rebuilds_ahead(cuda):
+    """Bins rebuilt every 3 steps: the rebuild is enqueued behind the step
+    before it (GSVC_TRAIN_REBUILD_NEXT) together with the next tile kernel, and
+    the trajectory is the one of rebuilding at the start of the call."""
+    from gsvc_amd.frame import synthetic_gt
+    gts = [synthetic_gt(256, 256, 4, cuda)]
+    la, wa, ma = _tiles_run(cuda, True, gts, {}, rebuild_every=3)
+    lb, wb, mb = _tiles_run(cuda, False, gts, {}, rebuild_every=3)
+    np.testing.assert_allclose(la, wa, rtol=2e-5, atol=1e-8)
+    np.testing.assert_allclose(la, lb, rtol=2e-5, atol=1e-8)
+    np.testing.assert_allclose(ma._xyz.detach().cpu().numpy(), mb._xyz.detach().cpu().numpy(),
+                               rtol=1e-3, atol=1e-4)
+    # every step after the second takes the tile kernel its predecessor enqueued
+    assert ma._bound_step.tiled_steps == 18, ma._bound_step.tiled_steps
 
 
 def test_projection_ahead_matches_and_honours_edits(cuda):
