@@ -1056,8 +1056,9 @@ extern "C" int gsvc_rasterize_sum_backward_det(
     if (ntiles == 0 || num_points == 0) return GSVC_OK;
     int *off = (int *)det_workspace;
     float *part = (float *)((char *)det_workspace + 256 * ((sizeof(int) * ((size_t)num_points + 1) + 255) / 256));
-    hipLaunchKernelGGL(det_offsets_kernel, dim3(1), dim3(kDetScanThreads), 0, s, num_points,
-                       (const float2 *)xys, radii, tbx, tby, off);
+    // (the block totals live in part until its memset below)
+    det_offsets_launch(num_points, (const float2 *)xys, radii, tbx, tby, off, (int *)part,
+                       9 * (size_t)det_capacity, s);
     if (det_capacity > 0 &&
         hipMemsetAsync(part, 0, sizeof(float) * 9 * (size_t)det_capacity, s) != hipSuccess)
         return set_error(GSVC_ERR_HIP, "rasterize_sum_backward_det: memset failed");

@@ -1746,9 +1746,9 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     // frame_index + 1's bins from scratch (the PROJECT_ONLY | CARRY projection;
     // the order flags apply to it), so the periodic rebuild costs no host gap
     const bool rebuild_next = (adan_flags & GSVC_TRAIN_REBUILD_NEXT) != 0;
-    if ((tiled || tiles_next) && (!carry || !projected || !update || det || render_out))
+    if ((tiled || tiles_next) && (!carry || !projected || !update || render_out))
         return set_error(GSVC_ERR_ARG, "train_step_sum: TILED / TILES_NEXT need CARRY | PROJECTED, "
-                                       "the Adan update, no render_out and no DETERMINISTIC");
+                                       "the Adan update and no render_out");
     if (rebuild_next && !tiles_next)
         return set_error(GSVC_ERR_ARG, "train_step_sum: REBUILD_NEXT needs TILES_NEXT");
     int *det_off = nullptr;
@@ -1785,14 +1785,18 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
         if (only) return refresh ? splat_order_sort(w.f, num_points, tbx, tby, s) : GSVC_OK;
     }
 
-    if (det) {
-        // this frame's (splat, tile) slot offsets, from the projection's xys / radii
-        hipLaunchKernelGGL(det_offsets_kernel, dim3(1), dim3(kDetScanThreads), 0, s, num_points,
-                           (const float2 *)w.f.xys, w.f.radii, tbx, tby, det_off);
+    // a frame's (splat, tile) slot offsets, from its projection's xys / radii,
+    // and its zeroed slots (the block totals live in det_part until the memset)
+    auto det_prepare = [&]() {
+        det_offsets_launch(num_points, (const float2 *)w.f.xys, w.f.radii, tbx, tby, det_off,
+                           (int *)det_part, det_capacity > 0 ? 8 * (size_t)det_capacity : 0, s);
         if (det_capacity > 0 &&
             hipMemsetAsync(det_part, 0, sizeof(float4) * 2 * (size_t)det_capacity, s) != hipSuccess)
             return set_error(GSVC_ERR_HIP, "train_step_sum: memset failed");
-        rc = check_launch("train_step_sum: det offsets");
+        return check_launch("train_step_sum: det offsets");
+    };
+    if (det && !tiled) {  // (TILED: the previous call prepared them with its tile kernel)
+        rc = det_prepare();
         if (rc) return rc;
     }
     const double count = 3.0 * (double)img_height * (double)img_width;  // numel of [3, H, W]
@@ -1943,6 +1947,10 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
                 rc = splat_order_sort(w.f, num_points, tbx, tby, s);
                 if (rc) return rc;
             }
+        }
+        if (det) {  // frame_index + 1's slots (the splat kernel has read this frame's)
+            rc = det_prepare();
+            if (rc) return rc;
         }
         return launch_tiles(fn);
     }

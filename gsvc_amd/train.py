@@ -94,9 +94,10 @@ class _TrainWorkspace:
         self.order_age = 0     # steps since it was sorted
         self.pending = None    # the projection a bound step enqueued ahead (BoundStep.launch):
         #                        (weakref to the step, frame, launch count, epoch, versions,
-        #                        tiles: None or (gt, gt version, background version) of the
-        #                        tile kernel enqueued ahead -- gt held so its storage stays
-        #                        alive and unreused while that kernel may read it)
+        #                        tiles: None or (gt, gt version, background version, det
+        #                        mode + workspace + capacity) of the tile kernel enqueued
+        #                        ahead -- gt held so its storage stays alive and unreused
+        #                        while that kernel may read it)
         self.det_buf = None    # GSVC_TRAIN_DETERMINISTIC workspace
         self.det_cap = 0
         self.carry_age = 0     # steps since the carried bins were rebuilt
@@ -310,9 +311,10 @@ class BoundStep:
             if ahead and pend[5] is not None:
                 # this frame's tile kernel ran against the previous call's target
                 # and background: usable only if they are this call's, unchanged
-                pgt, pver, pbg = pend[5]
-                tiled = (not self.det and pgt.data_ptr() == gt.data_ptr() and gt._version == pver
-                         and pgt._version == pver and self.background._version == pbg)
+                pgt, pver, pbg, pdet = pend[5]
+                tiled = (pgt.data_ptr() == gt.data_ptr() and gt._version == pver
+                         and pgt._version == pver and self.background._version == pbg
+                         and pdet == (self.det, a.det_workspace, a.det_capacity))
                 ahead = tiled  # else its gradient sums are in the records: rebuild
             if pend is not None and not ahead:
                 # an enqueued projection that cannot be used: its counts are in
@@ -333,9 +335,11 @@ class BoundStep:
                 flags |= TRAIN_TILED
                 self.tiled_steps += 1
             gkey = (gt.data_ptr(), gt._version)
-            if TILES_AHEAD and carry and not self.det and gkey == self.last_gt:
+            if TILES_AHEAD and carry and gkey == self.last_gt:
                 flags |= TRAIN_TILES_NEXT
-                tiles = (gt, gt._version, self.background._version)
+                # (deterministic mode: the next call must keep this det workspace)
+                tiles = (gt, gt._version, self.background._version,
+                         (self.det, a.det_workspace, a.det_capacity))
                 if ws.carry_age >= CARRY_REBUILD_EVERY:
                     # the next frame's bins are rebuilt behind this step, not at
                     # the start of the next call

@@ -388,7 +388,8 @@ int gsvc_render_frame_sum_ex(int num_points, const float *xyz, int xyz_tanh,
  * it excludes. */
 #define GSVC_TRAIN_CARRY 0x8000
 /* Tile kernel ahead (speed only; the same results; with CARRY | PROJECTED and
- * the Adan update, not with DETERMINISTIC or render_out).
+ * the Adan update, not with render_out; with DETERMINISTIC the next call must
+ * pass the same det_workspace and det_capacity).
  * GSVC_TRAIN_TILES_NEXT: after the step, enqueue frame_index + 1's tile kernel
  * (forward, loss and backward into the workspace's gradient records and tile
  * errors) against this call's ``gt`` -- it reads the bins and records this

@@ -155,8 +155,7 @@ def test_host_seq_wait_without_gpu_work():
 def test_train_step_ahead_flag_errors_without_launch():
     """The tile-kernel-ahead flags (GSVC_TRAIN_TILES_NEXT / TILED / REBUILD_NEXT)
     are checked before any HIP call: they need the carried bins of a projected
-    frame and the Adan update, and exclude the deterministic mode; REBUILD_NEXT
-    needs TILES_NEXT."""
+    frame and the Adan update; REBUILD_NEXT needs TILES_NEXT."""
     from gsvc_amd import _lib
     from gsvc_amd import train as T
     lib = _lib.load()
@@ -170,20 +169,16 @@ def test_train_step_ahead_flag_errors_without_launch():
     a.adan_state, a.adan_hparams = ctypes.addressof(state), ctypes.addressof(hp)
     a.workspace, a.workspace_bytes = dummy, 1 << 40
     base = T.TRAIN_PROJECTED | T.TRAIN_CARRY
-    det_bytes = lib.gsvc_train_step_det_workspace_bytes(10, 100)
     cases = [
-        (T.TRAIN_PROJECTED | T.TRAIN_TILED, None, b"TILED"),  # no carried bins
-        (T.TRAIN_CARRY | T.TRAIN_TILES_NEXT, None, b"TILED"),  # not projected
-        (base | T.TRAIN_TILES_NEXT | T.TRAIN_DETERMINISTIC, (dummy, det_bytes, 100), b"DETERMINISTIC"),
-        (base | T.TRAIN_REBUILD_NEXT, None, b"REBUILD_NEXT"),
+        (T.TRAIN_PROJECTED | T.TRAIN_TILED, b"TILED"),  # no carried bins
+        (T.TRAIN_CARRY | T.TRAIN_TILES_NEXT, b"TILED"),  # not projected
+        (base | T.TRAIN_REBUILD_NEXT, b"REBUILD_NEXT"),
     ]
-    for flags, det, msg in cases:
+    for flags, msg in cases:
         a.adan_flags = flags
-        a.det_workspace, a.det_workspace_bytes, a.det_capacity = det or (None, 0, 0)
         assert lib.gsvc_train_step_sum_args(ctypes.byref(a)) == 1, hex(flags)
         assert msg in lib.gsvc_last_error(), (hex(flags), lib.gsvc_last_error())
     # the gradient-only test hook has no update to run the next tile kernel behind
     a.adan_flags, a.grads_out = base | T.TRAIN_TILES_NEXT, dummy
-    a.det_workspace, a.det_workspace_bytes, a.det_capacity = None, 0, 0
     assert lib.gsvc_train_step_sum_args(ctypes.byref(a)) == 1
     assert b"Adan update" in lib.gsvc_last_error()

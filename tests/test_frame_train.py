@@ -232,6 +232,27 @@ def test_tiles_ahead_with_rebuilds_ahead(cuda):
     assert ma._bound_step.tiled_steps == 18, ma._bound_step.tiled_steps
 
 
+def test_tiles_ahead_deterministic_is_bitwise(cuda):
+    """Under torch.use_deterministic_algorithms(True) the tile kernel ahead
+    (with its slot offsets prepared behind the step) changes nothing: the
+    trajectory with and without it is bitwise identical, rebuilds included."""
+    from gsvc_amd.frame import synthetic_gt
+    prev = torch.are_deterministic_algorithms_enabled()
+    prev_warn = torch.is_deterministic_algorithms_warn_only_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        gts = [synthetic_gt(256, 256, 4, cuda), synthetic_gt(256, 256, 9, cuda)]
+        sched = {9: 1, 10: 1}
+        la, _, ma = _tiles_run(cuda, True, gts, sched, rebuild_every=5)
+        lb, _, mb = _tiles_run(cuda, False, gts, sched, rebuild_every=5)
+        assert la.tolist() == lb.tolist()
+        assert torch.equal(ma._xyz, mb._xyz) and torch.equal(ma._cholesky, mb._cholesky)
+        assert torch.equal(ma._features_dc, mb._features_dc)
+        assert ma._bound_step.tiled_steps >= 12, ma._bound_step.tiled_steps
+    finally:
+        torch.use_deterministic_algorithms(prev, warn_only=prev_warn)
+
+
 def test_projection_ahead_matches_and_honours_edits(cuda):
     """The fused step's projection of the next frame, enqueued ahead, gives the
     same trajectory as projecting at the start of each step, and is discarded
