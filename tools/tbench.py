@@ -39,6 +39,8 @@ def main():
                     help="also stamp the projection kernel's waves (start, projected, inserted, end)")
     ap.add_argument("--splat-stamps", action="store_true",
                     help="also stamp the splat kernel's waves (start, operands, Adan, carry, M, end)")
+    ap.add_argument("--rebuild-every", type=int, default=None,
+                    help="steps between carried-bin rebuilds (gsvc_amd.train.CARRY_REBUILD_EVERY)")
     ap.add_argument("--order-every", type=int, default=None,
                     help="steps between splat-order sorts (gsvc_amd.train.ORDER_REFRESH_EVERY; 0: none)")
     ap.add_argument("--frozen", type=int, default=0,
@@ -55,6 +57,8 @@ def main():
     from gsvc_amd import train as _train
     if a.order_every is not None:
         _train.ORDER_REFRESH_EVERY = a.order_every
+    if a.rebuild_every is not None:
+        _train.CARRY_REBUILD_EVERY = a.rebuild_every
     _lib.load().gsvc_debug_set(8, 1 if a.tile_kernel == "wg256" else 0)
     for kv in a.knob:
         k, v = kv.split("=")
