@@ -139,6 +139,18 @@ def order_flags(ws) -> int:
 
 _workspaces = {}
 _data_ptr = torch.Tensor.data_ptr
+
+
+def _dropped_step(ws):
+    """Weakref callback: the bound step whose work is pending in ``ws`` is gone
+    (its model was freed) -- release what the pending entry holds (the target)
+    and start the workspace's next user from zeroed counters."""
+    def cb(ref):
+        pend = ws.pending
+        if pend is not None and pend[0] is ref:
+            ws.pending = None
+            ws.dirty = True
+    return cb
 _raw_stream = torch._C._cuda_getCurrentRawStream  # current stream handle, no Stream object
 
 
@@ -353,7 +365,8 @@ class BoundStep:
         self._call(ws, lib, gt, flags | (order if flags & TRAIN_CARRY else ws.order_flags()))
         launches = _note_launch(a.xyz)
         if PROJECT_AHEAD:
-            ws.pending = (weakref.ref(self), ws.frame + 1, launches, _param_epoch[0], versions, tiles)
+            ws.pending = (weakref.ref(self, _dropped_step(ws)), ws.frame + 1, launches,
+                          _param_epoch[0], versions, tiles)
         ws.frame += 1
 
     def _call(self, ws, lib, gt, flags):

@@ -283,3 +283,28 @@ def test_projection_ahead_matches_and_honours_edits(cuda):
     # the edits matter: without them the trajectory differs clearly
     lc, _ = _ahead_run(cuda, True, {})
     assert np.abs(lc[6:] - la[6:]).max() > 1e-4
+
+
+def test_pending_work_released_with_its_model(cuda):
+    """A model whose last step left work pending (the next projection / tile
+    kernel, holding its target) releases it when the model is freed: the
+    workspace forgets the pending entry and re-zeroes its counters for the next
+    user, whose steps then match a fresh run."""
+    import gc
+    from gsvc_amd import train as Tr
+    from gsvc_amd.frame import make_frame_model, synthetic_gt
+    gt = synthetic_gt(64, 64, 2, cuda)
+    model = make_frame_model(64, 64, 200, cuda, seed=1)
+    for it in range(1, 6):
+        model.train_iter(gt, it)
+    key = (cuda.index, torch._C._cuda_getCurrentRawStream(cuda.index))
+    ws = Tr._workspaces[key]
+    assert ws.pending is not None and ws.pending[5] is not None  # tiles ahead, target held
+    del model
+    gc.collect()
+    assert ws.pending is None and ws.dirty
+    # the next model on the same workspace trains as on a fresh one
+    la = [float(make_frame_model(64, 64, 200, cuda, seed=1).train_iter(gt, 1)[0])]
+    m2 = make_frame_model(64, 64, 200, cuda, seed=1)
+    lb = [float(m2.train_iter(gt, it)[0]) for it in (1, 2, 3)]
+    assert abs(la[0] - lb[0]) <= 1e-6 * abs(lb[0])
