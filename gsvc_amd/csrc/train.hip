@@ -653,7 +653,9 @@ template <int kThreads, int kBatch = kLossBatch>
 __device__ __forceinline__ void publish_loss(const float2 *err, int ntiles, double inv_count,
                                              float *loss, unsigned loss_seq, const int *det_off,
                                              int n, double (*s_l)[4]) {
-    constexpr int kV = 256 / kThreads;  // virtual threads per thread
+    // virtual threads per thread (a workgroup wider than 256: its first 256
+    // threads are the virtual ones, the others add nothing)
+    constexpr int kV = kThreads >= 256 ? 1 : 256 / kThreads;
     const int tid = threadIdx.x;
     double s2[kV], s1[kV];
     const int npair = ntiles >> 1;
@@ -662,7 +664,8 @@ __device__ __forceinline__ void publish_loss(const float2 *err, int ntiles, doub
     for (int q = 0; q < kV; ++q) {
         s2[q] = 0.0;
         s1[q] = 0.0;
-        for (int t0 = tid + q * kThreads; t0 < npair; t0 += kBatch * 256) {
+        for (int t0 = tid + q * kThreads; t0 < npair && (kThreads <= 256 || tid < 256);
+             t0 += kBatch * 256) {
             float4 e[kBatch];
 #pragma unroll
             for (int k = 0; k < kBatch; ++k) {
@@ -690,7 +693,7 @@ __device__ __forceinline__ void publish_loss(const float2 *err, int ntiles, doub
             s2[q] += __shfl_xor(s2[q], off, 64);
             s1[q] += __shfl_xor(s1[q], off, 64);
         }
-        if ((tid & 63) == 0) {
+        if ((tid & 63) == 0 && tid + q * kThreads < 256) {
             s_l[0][(tid + q * kThreads) >> 6] = s2[q];
             s_l[1][(tid + q * kThreads) >> 6] = s1[q];
         }
@@ -1593,8 +1596,8 @@ __device__ __forceinline__ int splat_step(const TrainSplatArgs &A, int i, long l
     return hits;
 }
 
-template <bool kStamp>
-__global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
+template <bool kStamp, int kBlock = 256>
+__global__ __launch_bounds__(kBlock) void train_splat_kernel(TrainSplatArgs A) {
     long long *st = kStamp ? A.stamps + 8 * (size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6))
                            : nullptr;
     if (kStamp && (threadIdx.x & 63) == 0) st[0] = tstamp();
@@ -1602,13 +1605,20 @@ __global__ __launch_bounds__(256) void train_splat_kernel(TrainSplatArgs A) {
         // the first workgroup (no splats): the loss; dispatched first so it
         // runs beside the splats
         __shared__ double s_l[2][4];
-        publish_loss<256>(A.err, A.ntiles, A.inv_count, A.loss, A.loss_seq, A.det_off, A.n, s_l);
+        publish_loss<kBlock>(A.err, A.ntiles, A.inv_count, A.loss, A.loss_seq, A.det_off, A.n, s_l);
         if (kStamp) splat_stamp(st, 5);
         return;
     }
     const int t = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
     const int hits = t < A.n ? splat_step<kStamp>(A, t, st) : 0;
-    if (A.carry) {
+    if (A.carry == 2) {
+        // the next frame's M is read only as M >= 1 (the tile kernel's background
+        // branch, rasterize_sum.py:121-127): one plain store of 1 per wave that
+        // has tiles, instead of a per-workgroup device-scope atomic add -- those
+        // all go to one address and serialise at the memory side (~5 us of the
+        // kernel at 196 workgroups, ~20 us at 782)
+        if (__ballot(hits > 0) != 0ull && (threadIdx.x & 63) == 0) *A.m_next = 1;
+    } else if (A.carry) {
         __shared__ int s_hits[4];
         add_hits(hits, s_hits, A.m_next);  // the next frame's M
     }
@@ -1906,7 +1916,8 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     P.err = w.err;
     P.loss = loss;
     if (carry && update) {
-        P.carry = 1;
+        // 2: M as a flag (A/B knob 22 = 1: the exact count by atomics)
+        P.carry = g_knobs[22] == 1 ? 1 : 2;
         P.tbx = tbx;
         P.tby = tby;
         P.xys = (float2 *)w.f.xys;
@@ -1918,12 +1929,20 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     }
     P.loss_seq = loss_seq;
     // one extra (first) workgroup sums the loss, beside the splat workgroups
-    const int blocks = (num_points > 0 ? ceil_div(num_points, 256) : 0) + 1;
+    // A/B knob 21 = 64 or 128: smaller splat workgroups (more of them, over more CUs)
+    const int sb = g_knobs[21] == 64 || g_knobs[21] == 128 || g_knobs[21] == 512 ? g_knobs[21] : 256;
+    const int blocks = (num_points > 0 ? ceil_div(num_points, sb) : 0) + 1;
     hipEvent_t tev[2];
     const int tslot = timing_begin(s, tev, kTimingTrainSplat);
     if (g_knobs[5] == 4 && g_debug_ptr) {  // diagnostic: per-wave stamps of the splat kernel
         P.stamps = reinterpret_cast<long long *>(g_debug_ptr);
-        hipLaunchKernelGGL(train_splat_kernel<true>, dim3(blocks), dim3(256), 0, s, P);
+        hipLaunchKernelGGL(train_splat_kernel<true>, dim3(ceil_div(num_points, 256) + 1), dim3(256), 0, s, P);
+    } else if (sb == 64) {
+        launch_timed(train_splat_kernel<false, 64>, dim3(blocks), dim3(64), 0, s, tev, P);
+    } else if (sb == 128) {
+        launch_timed(train_splat_kernel<false, 128>, dim3(blocks), dim3(128), 0, s, tev, P);
+    } else if (sb == 512) {
+        launch_timed(train_splat_kernel<false, 512>, dim3(blocks), dim3(512), 0, s, tev, P);
     } else {
         launch_timed(train_splat_kernel<false>, dim3(blocks), dim3(256), 0, s, tev, P);
     }
