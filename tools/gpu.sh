@@ -17,7 +17,8 @@
 #                                      on frozen trained-density steps
 #   fbench_ab TAG [fbench args]        composite A/B by fbench + kernel trace
 #   shared_ranks TAG                   N = 1, 2, 4 bench ranks sharing one GPU (gloo)
-#   alpha_ab TAG                       alpha backward DPP vs shuffle sums (knob 9),
+#   alpha_ab TAG [KNOB ['V1 V2']]      alpha path A/B (default knob 9: backward DPP vs shuffle sums;
+#                                      knob 18 = 100000: forward without lane-group lists),
 #                                      interleaved twice
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -115,9 +116,10 @@ shared_ranks)
     GSVC_BENCH_SHARED_GPU=1 run n$n 400 python bench.py --gpus $n --backend gloo --no-cpu
   done ;;
 alpha_ab)
+  KN=${1:-9}; VALS=${2:-"0 1"}
   for rep in 1 2; do
-    for k in 0 1; do
-      run "k${k}_$rep" 200 rocprofv3 --kernel-trace --stats -d "$OUT/k${k}_$rep" -o a --output-format csv -- python3 tools/alphabench.py --splats 50000 --calls 100 --knob 9=$k
+    for k in $VALS; do
+      run "k${k}_$rep" 200 rocprofv3 --kernel-trace --stats -d "$OUT/k${k}_$rep" -o a --output-format csv -- python3 tools/alphabench.py --splats 50000 --calls 100 --knob $KN=$k
     done
   done ;;
 *)
