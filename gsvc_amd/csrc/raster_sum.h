@@ -18,6 +18,7 @@ struct SumFwdArgs {
     int store_policy;  // CHW plane stores: kStore* (gsvc_debug_set(7) selects)
     int spec_slots;    // frame path: slab records loaded with the count (<= kHeadSlots)
     int group_min;     // sparse chunks of <= this many entries skip the lane-group lists
+    int cut;           // sparse render chunks may take the sigma-threshold blend (knob 19 = 1: never)
     const int *m_dev;  // device num_intersects (NULL: > 0); 0 -> background
     const float *bg;
     const int *ids;

@@ -38,6 +38,8 @@
 // request per entry instead of the reference's 9 per warp).
 #include <hip/hip_ext.h>
 
+#include <type_traits>
+
 #include "cull.h"
 #include "det.h"
 #include "frame.h"
@@ -120,6 +122,33 @@ __device__ __forceinline__ void blend_pair(float gx, float ha, float b, float bd
         l1 = v1 ? k : l1;
     }
     (void)b;
+}
+
+// blend_pair for an entry of unit opacity, finite colour and bounded geometry
+// (cull.h geo_bounded): the alpha cut as a sigma threshold (common.h
+// kSigmaCutBits -- the same pairs pass, sigma is never NaN there, and
+// alpha = exp(-sigma) <= 1 needs no min), and a failing pair adds colour * 0
+// instead of selecting (+-0: an accumulator starts at +0 and is never -0).
+// The same bits as blend_pair without the last-index tracking.
+__device__ __forceinline__ void blend_pair_cut(float gx, float ha, float bdy, float cq, float cr,
+                                               float cg, float cb, v2f px, v2f &ar, v2f &ag,
+                                               v2f &ab) {
+    const v2f dx = gx - px;
+    const v2f q = __builtin_elementwise_fma((v2f)ha, dx, (v2f)bdy);
+    const v2f sg = __builtin_elementwise_fma(q, dx, (v2f)cq);
+    const v2f x = sg * kNegLog2e;
+    const v2f e = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+    const v2f av = {__float_as_uint(sg.x) <= kSigmaCutBits ? e.x : 0.0f,
+                    __float_as_uint(sg.y) <= kSigmaCutBits ? e.y : 0.0f};
+    ar = __builtin_elementwise_fma((v2f)cr, av, ar);
+    ag = __builtin_elementwise_fma((v2f)cg, av, ag);
+    ab = __builtin_elementwise_fma((v2f)cb, av, ab);
+}
+
+// A staged entry takes blend_pair_cut: unit opacity, finite colour, bounded geometry.
+__device__ __forceinline__ bool entry_cut_ok(const float4 &geo, const float4 &col, float blu) {
+    return col.y == 1.0f && __builtin_isfinite(col.z) && __builtin_isfinite(col.w) &&
+           __builtin_isfinite(blu) && geo_bounded(geo.x, geo.y, geo.z, geo.w, col.x);
 }
 
 // Can splat (x, y, conic a b c, opacity o) reach alpha >= 1/255 on any pixel
@@ -266,6 +295,9 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
     v2f ar23 = ar01, ag23 = ag01, ab23 = ab01;
     const v2f px01 = {px0, px1}, px23 = {px2, px3};
     int l0 = 0, l1 = 0, l2 = 0, l3 = 0;
+    // the chunk's entries all take blend_pair_cut (render paths only: the
+    // cut variant tracks no last index)
+    bool cut = false;
     if (seg_rec) {
         // <= 64 slab records in fill order: staged at their rank by id, before
         // the chunk loop (the speculative records die here)
@@ -280,6 +312,7 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         }
         const int id = lane < cnt ? __float_as_int(bx.y) : 0x7fffffff;
         const int rank = rank_below(id, cnt);
+        if (!kIdx) cut = A.cut && __ballot(lane < cnt && !entry_cut_ok(geo, col, bx.x)) == 0ull;
         if (lane < cnt) {
             s_geo[rank] = geo;
             s_col[rank] = col;
@@ -291,35 +324,52 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
     }
     for (int base = 0; base < n; base += kChunk) {
         const int cnt = min(kChunk, n - base);
-        if (!seg_rec && lane < cnt) {  // (seg_rec: staged above, n <= 64: one chunk)
-            float4 geo, col;
-            float blu;
-            const int j = base + lane;
-            load_splat(A, ids_in_lds ? s_ids[j] : A.ids[range.x + j], geo, col, blu);
-            s_geo[lane] = geo;
-            s_col[lane] = col;
-            s_blu[lane] = blu;
-            if (cnt > kGroupMin)
-                s_gm[lane] = (unsigned short)ellipse_blocks<16>(
-                    geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, tile_origin(tx), tile_origin(ty));
+        if (!seg_rec) {  // (seg_rec: staged above, n <= 64: one chunk)
+            bool ok = true;
+            if (lane < cnt) {
+                float4 geo, col;
+                float blu;
+                const int j = base + lane;
+                load_splat(A, ids_in_lds ? s_ids[j] : A.ids[range.x + j], geo, col, blu);
+                s_geo[lane] = geo;
+                s_col[lane] = col;
+                s_blu[lane] = blu;
+                if (cnt > kGroupMin)
+                    s_gm[lane] = (unsigned short)ellipse_blocks<16>(
+                        geo.x, geo.y, 2.0f * geo.z, geo.w, 2.0f * col.x, col.y, tile_origin(tx), tile_origin(ty));
+                if (!kIdx) ok = entry_cut_ok(geo, col, blu);
+            }
+            if (!kIdx) cut = A.cut && __ballot(!ok) == 0ull;
         }
         wave_lds_sync();
         const int k0 = range.x + base;
+        // entry t of the chunk into the lane's 4 pixels
+        auto blend = [&](int t, auto cutc) {
+            const float4 G = s_geo[t];
+            const float4 C = s_col[t];
+            const float bl = s_blu[t];
+            const float dy = G.y - py;
+            const float cq = (C.x * dy) * dy;
+            const float bdy = G.w * dy;
+            if constexpr (decltype(cutc)::value) {
+                blend_pair_cut(G.x, G.z, bdy, cq, C.z, C.w, bl, px01, ar01, ag01, ab01);
+                blend_pair_cut(G.x, G.z, bdy, cq, C.z, C.w, bl, px23, ar23, ag23, ab23);
+            } else {
+                const int k = k0 + t;
+                blend_pair<kIdx>(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, px01, k, ar01, ag01, ab01, l0, l1);
+                blend_pair<kIdx>(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, px23, k, ar23, ag23, ab23, l2, l3);
+            }
+        };
         if (cnt <= kGroupMin) {
             if (kMode == kModeSparsePrio) __builtin_amdgcn_s_setprio(0);
             // a few entries: every lane walks them all (the lists would cost
             // more than the pairs they skip)
             if (kMode == kModeSparseStamp && base == 0 && lane == 0) A.stamps[4 * (size_t)tile + 1] = stamp();
             for (int t = 0; t < cnt; ++t) {
-                const float4 G = s_geo[t];
-                const float4 C = s_col[t];
-                const float bl = s_blu[t];
-                const float dy = G.y - py;
-                const float cq = (C.x * dy) * dy;
-                const float bdy = G.w * dy;
-                const int k = k0 + t;
-                blend_pair<kIdx>(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, px01, k, ar01, ag01, ab01, l0, l1);
-                blend_pair<kIdx>(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, px23, k, ar23, ag23, ab23, l2, l3);
+                if (!kIdx && cut)
+                    blend(t, std::true_type{});
+                else
+                    blend(t, std::false_type{});
             }
             wave_lds_sync();
             continue;
@@ -343,16 +393,10 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         // the lane's 4x4 block of the tile
         const unsigned char *ml = s_list + (((lane >> 4) << 2) | (lane & 3));
         for (int it = 0; it < maxlen; ++it) {
-            const int t = ml[16 * it];
-            const float4 G = s_geo[t];
-            const float4 C = s_col[t];
-            const float bl = s_blu[t];
-            const float dy = G.y - py;
-            const float cq = (C.x * dy) * dy;
-            const float bdy = G.w * dy;
-            const int k = k0 + t;
-            blend_pair<kIdx>(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, px01, k, ar01, ag01, ab01, l0, l1);
-            blend_pair<kIdx>(G.x, G.z, G.w, bdy, cq, C.y, C.z, C.w, bl, px23, k, ar23, ag23, ab23, l2, l3);
+            if (!kIdx && cut)
+                blend(ml[16 * it], std::true_type{});
+            else
+                blend(ml[16 * it], std::false_type{});
         }
         wave_lds_sync();
     }
@@ -865,6 +909,7 @@ void sum_fwd_args_init(SumFwdArgs &A) {
     // A/B knob 10: speculative slab records per tile (default all kHeadSlots)
     A.spec_slots = g_knobs[10] > 0 && g_knobs[10] < kHeadSlots ? g_knobs[10] : kHeadSlots;
     A.group_min = g_knobs[15] > 0 ? g_knobs[15] - 1 : kGroupMinDefault;
+    A.cut = g_knobs[19] != 1;
     A.layout = kLayoutHWC;
     A.frames = 1;
 }

@@ -29,6 +29,7 @@
 
 #include "adan.h"
 #include "binning.h"
+#include "cull.h"
 #include "frame.h"
 #include "frame_dev.h"
 #include "det.h"
@@ -518,9 +519,9 @@ __device__ __forceinline__ void blend2_unit_fin(float gx, float ha, float bdy, f
 
 // blend2_unit_fin with the alpha cut as a sigma threshold (common.h
 // kSigmaCutBits: the same pairs pass, and alpha = exp(-sigma) <= 1 for them,
-// so the min(1, .) goes too) -- for entries whose colour AND geometry are
-// finite (sigma then is never NaN, the one value the threshold decides
-// differently).  The same bits as blend2_unit_fin.
+// so the min(1, .) goes too) -- for entries whose colour is finite and whose
+// geometry is bounded (geo_cut_ok: sigma is then never NaN, the one value the
+// threshold decides differently).  The same bits as blend2_unit_fin.
 __device__ __forceinline__ void blend2_cut(float gx, float ha, float bdy, float cq, float cr,
                                            float cg, float cb, v2f px, v2f &ar, v2f &ag, v2f &ab) {
     const v2f dx = gx - px;
@@ -536,11 +537,10 @@ __device__ __forceinline__ void blend2_cut(float gx, float ha, float bdy, float 
     ab = __builtin_elementwise_fma((v2f)cb, av, ab);
 }
 
-// An entry's geometry (x, y, a/2, b; c/2) is finite: its sigma is then never
-// NaN, and the sigma-threshold alpha cut (kSigmaCutBits) applies.
-__device__ __forceinline__ bool geo_finite(const float4 &G, float hc) {
-    return __builtin_isfinite(G.x) && __builtin_isfinite(G.y) && __builtin_isfinite(G.z) &&
-           __builtin_isfinite(G.w) && __builtin_isfinite(hc);
+// An entry's geometry (x, y, a/2, b; c/2) is bounded (cull.h geo_bounded):
+// its sigma is then never NaN, and the sigma-threshold alpha cut applies.
+__device__ __forceinline__ bool geo_cut_ok(const float4 &G, float hc) {
+    return geo_bounded(G.x, G.y, G.z, G.w, hc);
 }
 
 // Inclusive scans over one wave's 64 lanes with DPP (no LDS traffic):
@@ -949,7 +949,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                 }
                 const float4 C = S.col[lane];
                 fin = __builtin_isfinite(C.y) && __builtin_isfinite(C.z) && __builtin_isfinite(C.w);
-                cutok = fin && geo_finite(S.geo[lane], C.x);
+                cutok = fin && geo_cut_ok(S.geo[lane], C.x);
             }
             if (A.diag & 4) gm = 0u;  // diagnostic: no forward blending (wrong results)
             // row `lane` of the lists: the sentinel, then the entries
@@ -1170,7 +1170,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
         __builtin_amdgcn_wave_barrier();
         // the chunk's geometry finite: the backward's alpha cut by threshold
         const bool bcut =
-            __ballot(lane < gn && !geo_finite(S.geo[lane], S.col[lane].x)) == 0ull;
+            __ballot(lane < gn && !geo_cut_ok(S.geo[lane], S.col[lane].x)) == 0ull;
         const int ent = wperm[lane];  // the entry in sorted slot `lane`
         const int sitems = __shfl(items, ent, 64);
         const int incl = wave_scan_dpp<false>(sitems, 0);

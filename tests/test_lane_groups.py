@@ -95,3 +95,45 @@ def test_train_forward_lists_bit_identical(cuda, chol):
     assert torch.equal(res[0][0], res[1][0])
     torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(res[0][2], res[1][2], rtol=0, atol=0)
+
+
+def _bits(t):
+    return t.contiguous().view(torch.int32)
+
+
+@pytest.mark.parametrize("case", ["unit", "unit_dense", "mixed", "edge"])
+def test_composite_sigma_cut_bit_identical(cuda, oracle, case):
+    """The sparse render's sigma-threshold blend (chunks whose entries all have
+    unit opacity, finite colour and bounded geometry; knob 19 = 1 turns it off)
+    gives the same bits as the test as written -- including chunks that hold a
+    NaN or infinite colour, an overflowing conic or a non-unit opacity, which
+    must keep the written test (bitwise compare: NaN pixels included)."""
+    from gsvc_amd import _lib
+    from gsvc_amd.render import render_sum_frame
+    lib = _lib.load()
+    n = 30000 if case == "unit_dense" else 8000
+    means, L, colors, opac = oracle.synthetic_frame(
+        n, seed=7, rgb_w=2.0, chol_scale=3.0 if case == "unit_dense" else 1.0)
+    opac = np.ones_like(opac)
+    if case == "mixed":
+        opac[::7] = 0.5
+    if case == "edge":
+        colors = colors.copy()
+        L = L.copy()
+        colors[3] = np.nan
+        colors[11, 1] = np.inf
+        L[17] = [1e-19, 0.0, 1e-19]   # conic past the cut's bounds (or culled)
+        L[23] = [40.0, 39.9, 1e-3]    # a needle: large, nearly singular conic
+    bg = torch.ones(3, device="cuda")
+    outs = []
+    for knob in (0, 1):
+        olds = _knobs(lib, [(0, 1), (19, knob)])
+        try:
+            outs.append(render_sum_frame(T(means), T(L), T(colors), T(opac), H, W, _tb(H, W), bg))
+        finally:
+            _restore(lib, olds)
+    assert torch.equal(_bits(outs[0]), _bits(outs[1])), case
+    if case == "unit_dense":
+        ref = oracle.render_sum(means, L, colors, opac, H, W)["out"]
+        ref = np.clip(ref, 0, 1).reshape(H, W, 3).transpose(2, 0, 1)[None]
+        np.testing.assert_allclose(outs[0].cpu().numpy(), ref, rtol=0, atol=1e-5)
