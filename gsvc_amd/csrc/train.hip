@@ -655,7 +655,7 @@ __device__ __forceinline__ void publish_loss(const float2 *err, int ntiles, doub
                                              int n, double (*s_l)[4]) {
     // virtual threads per thread (a workgroup wider than 256: its first 256
     // threads are the virtual ones, the others add nothing)
-    constexpr int kV = kThreads >= 256 ? 1 : 256 / kThreads;
+    constexpr int kV = (256 + kThreads - 1) / kThreads;
     const int tid = threadIdx.x;
     double s2[kV], s1[kV];
     const int npair = ntiles >> 1;
@@ -664,7 +664,7 @@ __device__ __forceinline__ void publish_loss(const float2 *err, int ntiles, doub
     for (int q = 0; q < kV; ++q) {
         s2[q] = 0.0;
         s1[q] = 0.0;
-        for (int t0 = tid + q * kThreads; t0 < npair && (kThreads <= 256 || tid < 256);
+        for (int t0 = tid + q * kThreads; t0 < npair && tid + q * kThreads < 256;
              t0 += kBatch * 256) {
             float4 e[kBatch];
 #pragma unroll
@@ -1929,8 +1929,10 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     }
     P.loss_seq = loss_seq;
     // one extra (first) workgroup sums the loss, beside the splat workgroups
-    // A/B knob 21 = 64 or 128: smaller splat workgroups (more of them, over more CUs)
-    const int sb = g_knobs[21] == 64 || g_knobs[21] == 128 || g_knobs[21] == 512 ? g_knobs[21] : 256;
+    // A/B knob 21 = 64, 128, 192 or 512: other splat workgroup sizes
+    const int sb = g_knobs[21] == 64 || g_knobs[21] == 128 || g_knobs[21] == 192 || g_knobs[21] == 512
+                       ? g_knobs[21]
+                       : 256;
     const int blocks = (num_points > 0 ? ceil_div(num_points, sb) : 0) + 1;
     hipEvent_t tev[2];
     const int tslot = timing_begin(s, tev, kTimingTrainSplat);
@@ -1941,6 +1943,8 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
         launch_timed(train_splat_kernel<false, 64>, dim3(blocks), dim3(64), 0, s, tev, P);
     } else if (sb == 128) {
         launch_timed(train_splat_kernel<false, 128>, dim3(blocks), dim3(128), 0, s, tev, P);
+    } else if (sb == 192) {
+        launch_timed(train_splat_kernel<false, 192>, dim3(blocks), dim3(192), 0, s, tev, P);
     } else if (sb == 512) {
         launch_timed(train_splat_kernel<false, 512>, dim3(blocks), dim3(512), 0, s, tev, P);
     } else {
