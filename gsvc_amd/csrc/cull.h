@@ -24,8 +24,19 @@ __device__ __forceinline__ unsigned ellipse_blocks(float x, float y, float a, fl
     const float lg = __logf(255.0f * o);
     if (lg < -0.01f) return 0u;  // o < e^-0.01 / 255: alpha < 1/255 everywhere
     const float S2 = 2.0f * (lg * 1.001f + 0.01f);
-    const float ex = sqrtf(S2 * c / det) * 1.001f + 0.01f;
-    const float ey = sqrtf(S2 * a / det) * 1.001f + 0.01f;
+    // whole tiles: hardware rcp / sqrt (~1 ulp; f32 denormals are kept, so a
+    // det near the float maximum still gets its reciprocal) -- the margins
+    // dwarf their error; bands keep the IEEE forms (the banded composite's
+    // register budget: the shorter sequence spilled there)
+    float ex, ey;
+    if constexpr (kRows == 16) {
+        const float inv_det = __builtin_amdgcn_rcpf(det);
+        ex = __builtin_amdgcn_sqrtf(S2 * c * inv_det) * 1.001f + 0.01f;
+        ey = __builtin_amdgcn_sqrtf(S2 * a * inv_det) * 1.001f + 0.01f;
+    } else {
+        ex = sqrtf(S2 * c / det) * 1.001f + 0.01f;
+        ey = sqrtf(S2 * a / det) * 1.001f + 0.01f;
+    }
     // in strip coordinates, so the block bounds are literals (the origin
     // shift rounds by < 2^-12 px at 1080p, far inside the 0.01 px margin)
     const float u = x - bx0, v = y - by0;
