@@ -311,7 +311,18 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
             bx = r[2];
         }
         const int id = lane < cnt ? __float_as_int(bx.y) : 0x7fffffff;
-        const int rank = rank_below(id, cnt);
+        // rank by id: the ids through LDS (the lists' bytes, free until the
+        // chunk loop), 4 per broadcast read -- 2 VALU per entry instead of the
+        // 3 of a readlane loop; padding lanes hold 0x7fffffff, below no id
+        int *s_rid = reinterpret_cast<int *>(s_list);
+        s_rid[lane] = id;
+        wave_lds_sync();
+        int rank = 0;
+        for (int k = 0; k < cnt; k += 4) {
+            const int4 q = *reinterpret_cast<const int4 *>(s_rid + k);
+            rank += (q.x < id ? 1 : 0) + (q.y < id ? 1 : 0) + (q.z < id ? 1 : 0) + (q.w < id ? 1 : 0);
+        }
+        wave_lds_sync();
         if (!kIdx) cut = A.cut && __ballot(lane < cnt && !entry_cut_ok(geo, col, bx.x)) == 0ull;
         if (lane < cnt) {
             s_geo[rank] = geo;
