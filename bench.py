@@ -34,6 +34,9 @@ Reported beside the primary value:
   cpu_baseline  the CPU restatement (oracle/oracle.py train_iter_sum, C kernels)
                 on the same settled state, k = 1 and all cores, median of 5.
   render_10k    configs[1] (render only, 10k splats) and ``video_decode``.
+  op_path       the unchanged-caller path (GSVC's own files over the gsplat
+                drop-in: autograd op by op): forward, forward + backward, render
+                fps and train-iters/s at the same trained frame.
 """
 from __future__ import annotations
 
@@ -417,6 +420,85 @@ def video_decode(device, frames=8, splats=10000, steps=50, warmup=5):
                                  load_profile("video_decode"), "rasterize_sum_forward")}
 
 
+def op_path_block(model, gt, device, steps=200, warmup=20):
+    """The unchanged-caller path: what GSVC's own
+    GaussianSplats_Represent.py runs on the drop-in package -- autograd through
+    gsplat.project_gaussians_2d / rasterize_gaussians_sum, then clamp + NCHW,
+    L2, backward, PSNR .item(), the optimizer step (:83-90, :191-207) -- and its
+    FPS loop's forward (train_video_Represent.py:101-106), on a copy of the
+    bench's trained frame (fresh optimizer state, as a P-frame starts).
+    ``train_iters_per_s`` uses gsvc_amd.adan.Adan (one fused update kernel);
+    ``train_iters_per_s_foreach_adan`` the reference optimizer's own foreach
+    sequence (tests/adan_checker.py, op for op optimizer.py:296-362), i.e.
+    GSVC's files with nothing changed but the gsplat package."""
+    import math
+    import torch.nn.functional as F
+    from gsvc_amd.frame import make_frame_model
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from adan_checker import ForeachAdan
+    n = model._xyz.shape[0]
+    op = make_frame_model(H, W, n, device, seed=0, fused_train=False, fused_render=False)
+    with torch.no_grad():
+        for k in ("_xyz", "_cholesky", "_features_dc"):
+            getattr(op, k).copy_(getattr(model, k))
+    assert not op.fused_train and not op.fused_render
+
+    def timed(fn, k, w):
+        for _ in range(w):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / k
+
+    def fwd():
+        op.forward()
+
+    def fwd_bwd():
+        for p in (op._xyz, op._cholesky, op._features_dc):
+            p.grad = None
+        img = op.forward()["render"]
+        F.mse_loss(img.squeeze(0), gt.squeeze(0)).backward()
+
+    def render():
+        with torch.no_grad():
+            op.forward()
+
+    it = [0]
+
+    def train():
+        it[0] += 1
+        op.train_iter(gt, it[0])
+
+    fopt = ForeachAdan([op._xyz, op._cholesky, op._features_dc], lr=op.lr)
+
+    def train_foreach():  # GaussianSplats_Represent.py:191-207 with optimizer.py's Adan
+        img = op.forward()["render"]
+        loss = F.mse_loss(img.squeeze(0), gt.squeeze(0))
+        loss.backward()
+        with torch.no_grad():
+            math.log10(1.0 / F.mse_loss(img, gt).item())
+        fopt.step()
+        for p in fopt.params:
+            p.grad = None
+
+    t_fwd = timed(fwd, steps, warmup)
+    t_fb = timed(fwd_bwd, steps, warmup)
+    t_render = timed(render, steps, warmup)
+    t_train = timed(train, steps, warmup)
+    t_train_fe = timed(train_foreach, steps, warmup)
+    assert op.fused_steps == 0
+    return {"workload": f"unchanged-caller op path at 1920x1080 / {n} splats (the bench's trained "
+                        "frame): autograd through gsplat.* + clamp + NCHW",
+            "fwd_us": round(t_fwd * 1e6, 1), "fwd_bwd_us": round(t_fb * 1e6, 1),
+            "render_fps": round(1.0 / t_render, 1),
+            "train_iters_per_s": round(1.0 / t_train, 1),
+            "train_iters_per_s_foreach_adan": round(1.0 / t_train_fe, 1),
+            "timing": f"wall clock over {steps} calls after {warmup} warm-ups, synchronized"}
+
+
 def dry_run(args, world, rank):
     """--dry-run: the rank plumbing without a GPU (tests/test_bench_launch.py)."""
     t0 = time.perf_counter()
@@ -565,6 +647,7 @@ def main():
         line["render"]["vs_published_1500fps"] = round(line["render"]["frames_per_s"] / 1500.0, 2)
         line["render_10k"] = render_10k(device)
         line["video_decode"] = video_decode(device)
+        line["op_path"] = op_path_block(model, gt, device)
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args.splats)
     print(json.dumps(line), flush=True)

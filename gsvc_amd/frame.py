@@ -93,6 +93,9 @@ class GaussianVideoFrame(nn.Module):
         self.opt_type = kwargs["opt_type"]
         # whole train_iter as one fused call (gsvc_amd/train.py) where it applies
         self.fused_train = kwargs.get("fused_train", str(self.device).startswith("cuda"))
+        # forward() without autograd as the one-call frame render (render.py);
+        # False: GSVC's own op sequence (project -> rasterize -> clamp -> NCHW)
+        self.fused_render = kwargs.get("fused_render", True)
         self.fused_steps = 0
         self._bound_step = None
         self._bound_render = None
@@ -125,7 +128,8 @@ class GaussianVideoFrame(nn.Module):
         return o
 
     def forward(self):
-        if not torch.is_grad_enabled() and self.BLOCK_H == 16 and self.BLOCK_W == 16:
+        if (not torch.is_grad_enabled() and self.fused_render and self.BLOCK_H == 16
+                and self.BLOCK_W == 16):
             # inference: same image from the sync-free path with the clamp +
             # NCHW epilogue fused into the rasterizer (gsvc_amd/render.py)
             # (activations fused into the frame kernel: tanh, + bound, * rgb_W)
@@ -422,8 +426,10 @@ class GaussianVideoFrame(nn.Module):
 
 def make_frame_model(H, W, num_points, device, seed=None, lr=1e-3, isremoval=False,
                      isdensity=False, removal_rate=0.1, max_num_points=None,
-                     densification_interval=100, fused_train=None):
-    """Construct like SimpleTrainer2d does (train_video_Represent.py:51-55)."""
+                     densification_interval=100, fused_train=None, fused_render=None):
+    """Construct like SimpleTrainer2d does (train_video_Represent.py:51-55).
+    fused_train / fused_render False: train_iter / forward() take GSVC's own op
+    sequence through the gsplat operators (the unchanged-caller path)."""
     if seed is not None:
         torch.manual_seed(seed)
     model = GaussianVideoFrame(
@@ -431,7 +437,8 @@ def make_frame_model(H, W, num_points, device, seed=None, lr=1e-3, isremoval=Fal
         max_num_points=max_num_points or num_points, densification_interval=densification_interval,
         iterations=30000, H=H, W=W, BLOCK_H=16, BLOCK_W=16, device=device, lr=lr, quantize=False,
         removal_rate=removal_rate, isdensity=isdensity, isremoval=isremoval,
-        **({} if fused_train is None else {"fused_train": fused_train})).to(device)
+        **({} if fused_train is None else {"fused_train": fused_train}),
+        **({} if fused_render is None else {"fused_render": fused_render})).to(device)
     return model
 
 

@@ -456,11 +456,17 @@ def rasterize_sum_backward(img_height, img_width, BLOCK_H, BLOCK_W, gaussian_ids
 
 
 DET_PAIRS_PER_SPLAT = 16  # the deterministic backward's first slot capacity per splat
-_det_ws = {}  # device index -> [workspace, capacity, pair count of the last call (device int)]
+# (device index, stream) -> [workspace, capacity, pair count of the last call (device int)]
+_det_ws = {}
 
 
 def _raster_sum_bwd_det(img_height, img_width, BLOCK_H, BLOCK_W, gaussian_ids_sorted, tile_bins,
                         xys, conics, colors, opacities, radii, final_idx, v_output):
+    """The bitwise reproducible backward: one slot per (splat, tile) pair,
+    summed in a fixed order.  If the pairs outnumber the slots (the excess
+    would fall back to float atomics) the call is repeated with room for all
+    of them, so the result is always the reproducible one; the capacity is
+    kept for later calls (keyed by device and stream)."""
     xys = _f32(xys, "xys")
     colors = _f32(colors, "colors")
     if xys.dim() != 2 or xys.shape[1] != 2:
@@ -478,21 +484,23 @@ def _raster_sum_bwd_det(img_height, img_width, BLOCK_H, BLOCK_W, gaussian_ids_so
     v_output = _f32(v_output, "v_output")
     n = xys.shape[0]
     dev = xys.device
-    st = _det_ws.get(dev.index)
-    cap = DET_PAIRS_PER_SPLAT * n
-    if st is not None:
-        # grow past the pair count an earlier call reported (a short capacity
-        # falls back to atomics for the pairs past it: correct, not reproducible)
-        cap = max(cap, st[1], int(st[2]) * 3 // 2)
-    need = L.size("gsvc_rasterize_sum_backward_det_workspace_bytes", n, cap)
-    if st is None or st[0].numel() < need or st[1] != cap:
-        st = _det_ws[dev.index] = [torch.empty((need,), dtype=torch.uint8, device=dev), cap,
-                                   torch.zeros((1,), dtype=torch.int32, device=dev)]
+    key = (dev.index, L._raw_stream(dev.index))
+    st = _det_ws.get(key)
+    cap = max(DET_PAIRS_PER_SPLAT * n, st[1] if st is not None else 0)
     rec = torch.empty((n, 16), dtype=torch.float32, device=dev)
-    _timed_call("gsvc_rasterize_sum_backward_det", h, w, int(BLOCK_H), int(BLOCK_W), n,
-                L.ptr(gids), L.ptr(bins), L.ptr(xys), L.ptr(conics), L.ptr(colors),
-                L.ptr(opacities), L.ptr(radii), L.ptr(final_idx), L.ptr(v_output), L.ptr(rec),
-                L.ptr(st[0]), st[0].numel(), cap, L.ptr(st[2]), L.stream(dev))
+    for _ in range(2):
+        need = L.size("gsvc_rasterize_sum_backward_det_workspace_bytes", n, cap)
+        if st is None or st[0].numel() < need or st[1] != cap:
+            st = _det_ws[key] = [torch.empty((need,), dtype=torch.uint8, device=dev), cap,
+                                 torch.zeros((1,), dtype=torch.int32, device=dev)]
+        _timed_call("gsvc_rasterize_sum_backward_det", h, w, int(BLOCK_H), int(BLOCK_W), n,
+                    L.ptr(gids), L.ptr(bins), L.ptr(xys), L.ptr(conics), L.ptr(colors),
+                    L.ptr(opacities), L.ptr(radii), L.ptr(final_idx), L.ptr(v_output), L.ptr(rec),
+                    L.ptr(st[0]), st[0].numel(), cap, L.ptr(st[2]), L.stream(dev))
+        pairs = int(st[2].item())
+        if pairs <= cap:
+            break
+        cap = pairs + pairs // 2  # short: every slot again, with room to spare
     return split_grad_records(rec)
 
 

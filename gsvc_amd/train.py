@@ -13,6 +13,7 @@ learning rate, so fused and op-by-op iterations interleave freely.
 from __future__ import annotations
 
 import ctypes
+import warnings
 import weakref
 from typing import Optional, Sequence
 
@@ -77,8 +78,14 @@ def _note_launch(xyz_ptr: int) -> int:
 
 
 def bump_param_epoch() -> None:
-    """Parameters changed outside the fused step: discard any projection a
-    bound step enqueued ahead."""
+    """Parameters or a training target changed outside the fused step:
+    discard any projection or tile kernel a bound step enqueued ahead.
+
+    The fused step reuses work it enqueued ahead only while the bound
+    parameters and the target keep their storage and ``_version``; torch bumps
+    ``_version`` on every in-place op.  A write that bypasses it -- through
+    ``.data``, DLPack / CuPy views or a custom kernel -- must be followed by
+    this call, or the next step may use gradients of the old values."""
     _param_epoch[0] += 1
 
 
@@ -391,9 +398,19 @@ class BoundStep:
         if self.det:
             pairs = int(self.host_u[3])
             ws = _workspace(self.dev, self.n, self.H, self.W)
-            if pairs > ws.det_cap:
-                self.det_overflows += 1
             self.det_pairs = pairs
+            if pairs > ws.det_cap:
+                # the pairs past the slot capacity were summed by float
+                # atomics: this step's gradients are not bitwise reproducible
+                # (the next step's capacity grows from this count)
+                self.det_overflows += 1
+                msg = (f"gsvc_train_step_sum: deterministic backward had {pairs} (splat, tile) "
+                       f"pairs for {ws.det_cap} slots; the excess was summed by float atomics, "
+                       "so this step is not bitwise reproducible (capacity grown for the next step)")
+                if torch.is_deterministic_algorithms_warn_only_enabled():
+                    warnings.warn(msg)
+                else:
+                    raise RuntimeError(msg)
         return self.host_f[0], self.host_f[1]
 
 

@@ -182,3 +182,66 @@ def test_op_path_backward_reproducible(cuda, deterministic):
     ga = grads()
     for k in g1:
         _close(g1[k], ga[k])
+
+
+def _overflow_model(cuda, monkeypatch):
+    """A fresh 256x256 / 2000-splat frame whose first fused step gets one slot
+    per splat (about 2.5 pairs per splat at random init: the capacity is short)."""
+    from gsvc_amd import train as T
+    from gsvc_amd.frame import make_frame_model, synthetic_gt
+    m = make_frame_model(256, 256, 2000, cuda, seed=3)
+    gt = synthetic_gt(256, 256, 4, cuda)
+    ws = T._workspace(cuda, 2000, 256, 256)
+    ws.det_buf, ws.det_cap = None, 0
+    monkeypatch.setattr(T, "DET_CAPACITY_PER_SPLAT", 1)
+    return m, gt
+
+
+def test_short_capacity_warns_under_warn_only(cuda, deterministic, monkeypatch):
+    """a fused step whose pairs outnumber the slots is not bitwise
+    reproducible -- warn_only mode says so, and the next step has room."""
+    m, gt = _overflow_model(cuda, monkeypatch)
+    with pytest.warns(UserWarning, match="not bitwise reproducible"):
+        m.train_iter(gt, 1)
+    assert m._bound_step.det_overflows == 1
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        m.train_iter(gt, 2)
+    assert m._bound_step.det_overflows == 1
+
+
+def test_short_capacity_raises_in_strict_mode(cuda, monkeypatch):
+    prev = torch.are_deterministic_algorithms_enabled()
+    prev_warn = torch.is_deterministic_algorithms_warn_only_enabled()
+    torch.use_deterministic_algorithms(True)
+    try:
+        m, gt = _overflow_model(cuda, monkeypatch)
+        with pytest.raises(RuntimeError, match="not bitwise reproducible"):
+            m.train_iter(gt, 1)
+    finally:
+        torch.use_deterministic_algorithms(prev, warn_only=prev_warn)
+
+
+def test_op_path_short_capacity_repeats(cuda, deterministic, monkeypatch):
+    """The op path's deterministic backward repeats a call whose pairs outnumber
+    the slots, so its gradients are always the reproducible ones: a one-slot-
+    per-splat start gives the bits of an ample capacity."""
+    from gsvc_amd import ops
+    from gsvc_amd.frame import synthetic_gt
+    m, z = _state_model(cuda, fused=False)
+    gt = synthetic_gt(H, W, int(z["gt_seed"]), "cpu").to(cuda)
+
+    def grads():
+        for p in m.parameters():
+            p.grad = None
+        img = m.forward()["render"]
+        torch.nn.functional.mse_loss(img, gt).backward()
+        return torch.cat([m._xyz.grad.flatten(), m._cholesky.grad.flatten(),
+                          m._features_dc.grad.flatten()])
+
+    ops._det_ws.clear()
+    ref = grads()
+    ops._det_ws.clear()
+    monkeypatch.setattr(ops, "DET_PAIRS_PER_SPLAT", 1)
+    assert torch.equal(grads(), ref)
