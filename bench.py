@@ -527,6 +527,8 @@ def main():
     torch.cuda.set_device(device)
     from gsvc_amd.frame import make_frame_model, synthetic_gt
     if args.knob:
+        # A/B knobs exist only in the diagnostic library (an A/B run, not the headline)
+        os.environ["GSVC_DIAG"] = "1"
         from gsvc_amd import _lib
         for kv in args.knob:
             k, v = kv.split("=")

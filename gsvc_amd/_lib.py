@@ -6,9 +6,18 @@ extension or JIT-compiled it with nvcc and otherwise set ``_C = None``.  Here
 the library is prebuilt in-tree for gfx950 (gsvc_amd/build.py).  There is no
 CPU fallback: if the library is missing, or a tensor is not on a HIP device,
 the call raises.
+
+Two builds of the same sources exist: the product library (libgsvc_amd.so,
+include/gsvc_amd.h) and the diagnostic one (libgsvc_amd_diag.so, -DGSVC_DIAG:
+the A/B knobs and timestamped / ablation kernel variants of
+include/gsvc_amd_diag.h).  ``load()`` returns the product library unless the
+process runs with GSVC_DIAG=1 (tools/) or inside ``with diagnostic():`` (the
+variant-comparison tests), which switches every op of this package to the
+diagnostic library for its duration.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import threading
@@ -17,6 +26,7 @@ import torch  # noqa: F401  (loads torch's libamdhip64 first; the library reuses
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libgsvc_amd.so")
+DIAG_LIB_PATH = os.path.join(_HERE, "lib", "libgsvc_amd_diag.so")
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -28,8 +38,6 @@ _SZ = ctypes.c_size_t
 _SIGS = {
     "gsvc_abi_version": [],
     "gsvc_last_error": [],
-    "gsvc_debug_set": [_I, _I],
-    "gsvc_debug_set_ptr": [_P],
     "gsvc_alpha_cut_bits": [],
     "gsvc_alpha_cut_scan": [_P, _P],
     "gsvc_stream_sync": [_P],
@@ -93,6 +101,11 @@ _SIGS = {
     "gsvc_rasterize_backward": [_U, _U, _U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                 _P, _P],
 }
+# include/gsvc_amd_diag.h: the diagnostic library's extra entry points
+_DIAG_SIGS = {
+    "gsvc_debug_set": [_I, _I],
+    "gsvc_debug_set_ptr": [_P],
+}
 _RESTYPE = {
     "gsvc_debug_set_ptr": None,
     "gsvc_alpha_cut_bits": _U,
@@ -116,36 +129,70 @@ _RESTYPE = {
 
 ABI_VERSION = 1
 
-_lib = None
+_libs = {}       # path -> loaded CDLL
+_active = None   # the library ops call (load())
 _lock = threading.Lock()
 
 
-def symbols():
-    """Names of every entry point declared in include/gsvc_amd.h."""
-    return list(_SIGS)
+def symbols(diag: bool = False):
+    """Names of every entry point declared in include/gsvc_amd.h (with
+    ``diag``: also include/gsvc_amd_diag.h)."""
+    return list(_SIGS) + (list(_DIAG_SIGS) if diag else [])
 
 
-def load():
-    """Load libgsvc_amd.so (raises if it has not been built)."""
-    global _lib
-    if _lib is not None:
-        return _lib
+def _open(path: str, diag: bool):
+    lib = _libs.get(path)
+    if lib is not None:
+        return lib
     with _lock:
-        if _lib is None:
-            if not os.path.exists(LIB_PATH):
+        lib = _libs.get(path)
+        if lib is None:
+            if not os.path.exists(path):
                 raise RuntimeError(
-                    f"gsvc_amd: {LIB_PATH} not found; build it with `python -m gsvc_amd.build` "
+                    f"gsvc_amd: {path} not found; build it with `python -m gsvc_amd.build` "
                     "(there is no CPU fallback)")
-            lib = ctypes.CDLL(LIB_PATH)
-            for name, args in _SIGS.items():
+            lib = ctypes.CDLL(path)
+            for name, args in list(_SIGS.items()) + (list(_DIAG_SIGS.items()) if diag else []):
                 fn = getattr(lib, name)
                 fn.argtypes = args
                 fn.restype = _RESTYPE.get(name, _I)
             v = lib.gsvc_abi_version()
             if v != ABI_VERSION:
                 raise RuntimeError(f"gsvc_amd: ABI version {v} != {ABI_VERSION}; rebuild the library")
-            _lib = lib
-    return _lib
+            _libs[path] = lib
+    return lib
+
+
+def load():
+    """The library the ops call: libgsvc_amd.so, or the diagnostic build when
+    GSVC_DIAG=1 or inside ``diagnostic()`` (raises if it has not been built)."""
+    global _active
+    if _active is None:
+        if os.environ.get("GSVC_DIAG") == "1":
+            _active = _open(DIAG_LIB_PATH, True)
+        else:
+            _active = _open(LIB_PATH, False)
+    return _active
+
+
+def load_product():
+    """libgsvc_amd.so itself, whatever library is active."""
+    return _open(LIB_PATH, False)
+
+
+@contextlib.contextmanager
+def diagnostic():
+    """Run this package's ops on libgsvc_amd_diag.so for the block (its A/B
+    knobs: gsvc_debug_set); yields that library.  Objects that bound a
+    library function before the block (BoundStep, BoundRender) keep theirs."""
+    global _active
+    prev = load()
+    lib = _open(DIAG_LIB_PATH, True)
+    _active = lib
+    try:
+        yield lib
+    finally:
+        _active = prev
 
 
 def call(name: str, *args) -> None:

@@ -28,9 +28,23 @@ constexpr unsigned kSigmaCutBits = 0x40b15208u;  // sigma 5.5412636 (gfx950 v_ex
 // Host-side error plumbing -------------------------------------------------
 int set_error(int code, const char *fmt, ...);
 int check_launch(const char *what);
+// A/B knobs and diagnostic kernel variants exist only in the diagnostic
+// library (built with -DGSVC_DIAG: libgsvc_amd_diag.so, include/gsvc_amd_diag.h,
+// for tools/ and the variant-comparison tests).  In the product library every
+// knob is the constant 0 -- the production choice -- and the diagnostic
+// variants are not compiled (``if constexpr (kDiag)`` around their launches).
 constexpr int kKnobs = 24;
+#ifdef GSVC_DIAG
+constexpr bool kDiag = true;
 extern int g_knobs[kKnobs];  // gsvc_debug_set(); knob 0 = sum-forward variant, 8 = training tile kernel
-extern void *g_debug_ptr;  // gsvc_debug_set_ptr(): diagnostic output buffer
+extern void *g_debug_ptr;    // gsvc_debug_set_ptr(): diagnostic output buffer
+inline int knob(int k) { return g_knobs[k]; }
+inline void *debug_ptr() { return g_debug_ptr; }
+#else
+constexpr bool kDiag = false;
+constexpr int knob(int) { return 0; }
+constexpr void *debug_ptr() { return nullptr; }
+#endif
 // timing.hip: slot, or -1 when not recording; dispatch_ev[2] = the events the
 // launch must carry itself (hipExtLaunchKernel), both null otherwise
 constexpr int kTimingComposite = 0, kTimingTrainTile = 1, kTimingProject = 2,

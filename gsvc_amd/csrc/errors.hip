@@ -27,13 +27,17 @@ int check_launch(const char *what) {
     return GSVC_OK;
 }
 
+#ifdef GSVC_DIAG
 int g_knobs[kKnobs] = {};
 void *g_debug_ptr = nullptr;
+#endif
 
 }  // namespace gsvc
 
 extern "C" int gsvc_abi_version(void) { return 1; }
 
+#ifdef GSVC_DIAG
+// include/gsvc_amd_diag.h: the diagnostic library only
 extern "C" int gsvc_debug_set(int key, int value) {
     if (key < 0 || key >= gsvc::kKnobs) return -1;
     const int old = gsvc::g_knobs[key];
@@ -42,6 +46,7 @@ extern "C" int gsvc_debug_set(int key, int value) {
 }
 
 extern "C" void gsvc_debug_set_ptr(void *p) { gsvc::g_debug_ptr = p; }
+#endif
 
 extern "C" const char *gsvc_last_error(void) { return gsvc::g_last_error; }
 

@@ -55,7 +55,7 @@ __device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, i
         for (int k = 0; k < kBatch; ++k)
             if (k < cnt && sl[k] < (unsigned)kTilePix) {
                 float4 *d = slab_rec(slab, ntiles, (int)tl[k], (int)sl[k]);
-                if (wt & 1) {
+                if (kDiag && (wt & 1)) {
                     store_wt(d, r0);
                     store_wt(d + 1, r1);
                     store_wt(d + 2, r2);
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
         for (int q = sub; q < 4; q += K) {
             if (q < 3) {
                 const float4 rq = q == 0 ? S.r0 : (q == 1 ? S.r1 : S.r2);
-                if (wt & 1)
+                if (kDiag && (wt & 1))
                     store_wt(rec + 3 * i + q, rq);
                 else
                     rec[3 * i + q] = rq;
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
         }
         if (kStamp && (threadIdx.x & 63) == 0) st[1] = proj_stamp();
         if (S.P.rad > 0) {
-            if (K == 1 && !(wt & 3))  // paired atomics unless write-through / A/B knob 2 = 4
+            if (K == 1 && !(kDiag && (wt & 3)))  // paired atomics unless write-through / A/B knob 2 = 4
                 hits = slab_insert_pairs<8>(S.P.xy.x, S.P.xy.y, S.P.rad, tbx, tby, S.r0, S.r1,
                                             S.r2, counts, slab, wt);
             else
@@ -302,13 +302,13 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
     const float hw = 0.5f * (float)img_w, hh = 0.5f * (float)img_h;
     if (ord && frames == 1 && n > 0) {
         const dim3 grid(ceil_div(n, kProjThreads));
-        if (g_knobs[5] == 1 && g_debug_ptr) {  // diagnostic: per-wave stamps
+        if constexpr (kDiag) if (knob(5) == 1 && debug_ptr()) {  // diagnostic: per-wave stamps
             hipLaunchKernelGGL(frame_project_ordered_kernel<true>, grid, dim3(kProjThreads), 0, s, n,
                                ord->order, xyz, xyz_tanh, chol, chol_bound, feat, rgb_w, opac, hw,
                                hh, tbx, tby, w.xys, w.radii, w.rec,
                                ord->carry_ids ? ord->carry_counts : f.counts, w.slab, f.m_acc,
                                f.m_clear, grad_zero, ord->key, ord->key_id, strip_key_invisible(tbx, tby),
-                               reinterpret_cast<long long *>(g_debug_ptr), ord->carry_ids,
+                               reinterpret_cast<long long *>(debug_ptr()), ord->carry_ids,
                                ord->carry_box, ord->carry_hull);
             return check_launch("frame projection (ordered)");
         }
@@ -325,7 +325,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
     }
     // lanes per splat: 1 unless gsvc_debug_set(4, k) picks 2, 4 or 8 (A/B knob;
     // measured at 1080p: equal at 10k splats, 1 lane fastest at 50k)
-    const int k = g_knobs[4] == 2 || g_knobs[4] == 4 || g_knobs[4] == 8 ? g_knobs[4] : 1;
+    const int k = knob(4) == 2 || knob(4) == 4 || knob(4) == 8 ? knob(4) : 1;
     const size_t slab_stride = slab_frame_f4(tbx * tby);
     // plain record stores; A/B knob 6 = 1 writes them through (sc1): measured
     // slower (projection 7.1 -> 9.8 us at 10k: each scattered 16-byte sc1 store
@@ -333,7 +333,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
     // bit 0: write-through record stores (A/B knob 6 = 1); bit 1: one 32-bit
     // slot atomic per tile instead of the pairs (A/B knob 2 = 4).  Measured
     // with the isolation runs of profiles/r01/paired_atomics/NOTES.md.
-    const int wt = (g_knobs[6] == 1 ? 1 : 0) | (g_knobs[2] == 4 ? 2 : 0);
+    const int wt = (knob(6) == 1 ? 1 : 0) | (knob(2) == 4 ? 2 : 0);
     if (frames > 1 && !frame_off) return set_error(GSVC_ERR_ARG, "frame projection: frame offsets");
     const int per = frames > 1 ? max_frame_n : n;
     if (frames > 1 && per <= 0) {
@@ -345,7 +345,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
     }
     if (per > 0) {
         // workgroup size: 256 unless A/B knob 1 picks 64 or 128
-        const int bs = g_knobs[1] == 64 || g_knobs[1] == 128 ? g_knobs[1] : kProjThreads;
+        const int bs = knob(1) == 64 || knob(1) == 128 ? knob(1) : kProjThreads;
         const dim3 grid(ceil_div(per, bs / k), frames > 1 ? frames : 1);
 #define GSVC_FRAME_PROJECT(K)                                                                    \
     {                                                                                            \
@@ -358,21 +358,25 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
                      f.counts_stride, f.m_stride, slab_stride, wt);                              \
         timing_end(s, tslot, kTimingProject);                                                    \
     }
-        if (g_knobs[5] == 1 && g_debug_ptr) {  // diagnostic: per-wave stamps
+        if constexpr (kDiag) if (knob(5) == 1 && debug_ptr()) {  // diagnostic: per-wave stamps
             auto kfn = frame_project_kernel<1, true>;
             hipLaunchKernelGGL(kfn, grid, dim3(bs), 0, s, n, xyz, xyz_tanh, chol,
                                chol_bound, feat, rgb_w, opac, hw, hh, tbx, tby, w.xys, w.radii,
                                w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero,
-                               reinterpret_cast<long long *>(g_debug_ptr),
+                               reinterpret_cast<long long *>(debug_ptr()),
                                frames > 1 ? frame_off : nullptr, f.counts_stride, f.m_stride,
                                slab_stride, wt);
             return check_launch("frame projection");
         }
-        switch (k) {
-            case 2: GSVC_FRAME_PROJECT(2); break;
-            case 8: GSVC_FRAME_PROJECT(8); break;
-            case 4: GSVC_FRAME_PROJECT(4); break;
-            default: GSVC_FRAME_PROJECT(1); break;
+        if constexpr (kDiag) {
+            switch (k) {
+                case 2: GSVC_FRAME_PROJECT(2); break;
+                case 8: GSVC_FRAME_PROJECT(8); break;
+                case 4: GSVC_FRAME_PROJECT(4); break;
+                default: GSVC_FRAME_PROJECT(1); break;
+            }
+        } else {
+            GSVC_FRAME_PROJECT(1);
         }
 #undef GSVC_FRAME_PROJECT
     } else if (hipMemsetAsync(f.m_acc, 0, sizeof(int), s) != hipSuccess)

@@ -330,7 +330,7 @@ extern "C" int gsvc_rasterize_forward(int tbx, int tby, int tbz, int block_x, in
                        (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacities,
                        background, out_img, final_Ts, final_idx,
                        // A/B knob 18 = v > 0: list threshold v - 1
-                       g_knobs[18] > 0 ? g_knobs[18] - 1 : kAGroupMin);
+                       knob(18) > 0 ? knob(18) - 1 : kAGroupMin);
     return check_launch("rasterize_forward");
 }
 
@@ -352,7 +352,10 @@ extern "C" int gsvc_rasterize_backward(unsigned img_height, unsigned img_width, 
     const int tbx = ceil_div((int)img_width, kTile), tby = ceil_div((int)img_height, kTile);
     const int ntiles = tbx * tby;
     if (ntiles == 0 || num_points == 0) return GSVC_OK;
-    hipLaunchKernelGGL(g_knobs[9] == 1 ? raster_alpha_bwd_kernel<false> : raster_alpha_bwd_kernel<true>,
+    auto bwd = raster_alpha_bwd_kernel<true>;  // per-row DPP sums
+    if constexpr (kDiag)
+        if (knob(9) == 1) bwd = raster_alpha_bwd_kernel<false>;  // A/B: the shuffle butterflies
+    hipLaunchKernelGGL(bwd,
                        dim3(ntiles), dim3(256), 0, s, tbx, (int)img_width,
                        (int)img_height, ntiles, gaussian_ids_sorted, (const int2 *)tile_bins,
                        (const float2 *)xys, conics, colors, opacities, background, final_Ts,

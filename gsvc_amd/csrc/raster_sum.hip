@@ -180,6 +180,7 @@ enum { kStoreNtSc1 = 0, kStorePlain = 1, kStoreSc1 = 2, kStoreSc01 = 3, kStoreNt
 
 __device__ __forceinline__ void st_f4(float *p, float a, float b, float c, float d, int policy) {
     const v4f v = {a, b, c, d};
+    if (!kDiag) policy = kStoreNtSc1;  // the product's one policy
     switch (policy) {
     case kStoreNt: __builtin_nontemporal_store(v, reinterpret_cast<v4f *>(p)); break;
     case kStoreSc1: asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory"); break;
@@ -195,6 +196,7 @@ __device__ __forceinline__ void st_f4(float *p, float a, float b, float c, float
 
 __device__ __forceinline__ void st_f2(float *p, float a, float b, int policy) {
     const v2f v = {a, b};
+    if (!kDiag) policy = kStoreNtSc1;  // the product's one policy
     switch (policy) {
     case kStoreNt: __builtin_nontemporal_store(v, reinterpret_cast<v2f *>(p)); break;
     case kStoreSc1: asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory"); break;
@@ -893,7 +895,7 @@ static int pipe_waves(int total_tiles) {
             v = 256;
         cus[dev] = v;
     }
-    const int wps = g_knobs[20] >= 1 && g_knobs[20] <= 3 ? g_knobs[20] : 2;
+    const int wps = knob(20) >= 1 && knob(20) <= 3 ? knob(20) : 2;
     const long long w = (long long)cus[dev] * 4 * wps;
     return (int)(w < total_tiles ? w : total_tiles);
 }
@@ -1073,11 +1075,11 @@ static int check_tiles(const char *what, int bx, int by, int tbx, int tby, unsig
 
 void sum_fwd_args_init(SumFwdArgs &A) {
     A = SumFwdArgs{};
-    A.sparse_max = g_knobs[3] > 0 ? g_knobs[3] : 8;
+    A.sparse_max = knob(3) > 0 ? knob(3) : 8;
     // A/B knob 10: speculative slab records per tile (default all kHeadSlots)
-    A.spec_slots = g_knobs[10] > 0 && g_knobs[10] < kHeadSlots ? g_knobs[10] : kHeadSlots;
-    A.group_min = g_knobs[15] > 0 ? g_knobs[15] - 1 : kGroupMinDefault;
-    A.cut = g_knobs[19] != 1;
+    A.spec_slots = knob(10) > 0 && knob(10) < kHeadSlots ? knob(10) : kHeadSlots;
+    A.group_min = knob(15) > 0 ? knob(15) - 1 : kGroupMinDefault;
+    A.cut = knob(19) != 1;
     A.layout = kLayoutHWC;
     A.frames = 1;
 }
@@ -1097,13 +1099,14 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
     A.vec = (A.img_w % 4 == 0) && (((uintptr_t)A.out & 15) == 0) &&
             (((uintptr_t)A.final_idx & 15) == 0) && (((uintptr_t)A.final_Ts & 15) == 0);
     A.vec_chw = A.vec && (((size_t)A.img_w * (size_t)A.img_h) % 4 == 0);
-    A.store_policy = g_knobs[7];  // kStoreNtSc1 unless an A/B run selects another (knob 7)
+    A.store_policy = knob(7);  // kStoreNtSc1 unless an A/B run selects another (knob 7)
     const int ntiles = A.ntiles;
-    int mode = g_knobs[0];
+    int mode = knob(0);
     if (mode == 0)
         mode = ((long long)density_hint > (long long)kDenseEntriesPerTile * ntiles * A.frames)
                    ? kModeBanded
                    : kModeSparse;
+    if (knob(17) == 1 && mode == kModeSparse) mode = kModeSparsePrio;  // A/B knob 17
     if (mode == kModeStamp && A.layout != kLayoutHWC)
         return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: stamp mode needs the HWC layout");
     if (A.frames > 1 && (mode == kModeStamp || mode == kModeSparseStamp))
@@ -1111,52 +1114,55 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
     hipEvent_t tev[2];
     const int tslot = timing_begin(s, tev);
     const dim3 grid(ntiles * A.frames);
-    switch (mode) {
-        case kModeSparse:
-            if (A.slab && !A.final_idx && A.layout == kLayoutCHWClamped && g_knobs[23] != 1 &&
-                g_knobs[17] != 1)  // the frame path: persistent pipelined (A/B knob 23 = 1: one round)
-                launch_fwd(A.frames > 1 ? composite_pipe_kernel<true> : composite_pipe_kernel<false>,
-                           dim3(pipe_waves(ntiles * A.frames)), dim3(64), s, tev, A);
-            else if (g_knobs[17] == 1)
+    if (mode == kModeSparse) {
+        if (A.slab && !A.final_idx && A.layout == kLayoutCHWClamped && knob(23) != 1 &&
+            knob(17) != 1)  // the frame path: persistent pipelined (A/B knob 23 = 1: one round)
+            launch_fwd(A.frames > 1 ? composite_pipe_kernel<true> : composite_pipe_kernel<false>,
+                       dim3(pipe_waves(ntiles * A.frames)), dim3(64), s, tev, A);
+        else
+            launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeSparse, true>
+                                   : raster_sum_fwd_kernel<kModeSparse, false>,
+                       grid, dim3(64), s, tev, A);
+    } else if (mode == kModeBanded) {
+        launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeBanded, true>
+                               : raster_sum_fwd_kernel<kModeBanded, false>,
+                   grid, dim3(128), s, tev, A);
+    } else if constexpr (kDiag) {
+        // diagnostic variants (libgsvc_amd_diag.so only)
+        switch (mode) {
+            case kModeStamp:
+                A.stamps = reinterpret_cast<long long *>(A.final_Ts);
+                A.final_Ts = nullptr;
+                launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeStamp, true> : raster_sum_fwd_kernel<kModeStamp, false>, grid,
+                           dim3(128), s, tev, A);
+                break;
+            case kModeNoBlend:
+                launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeNoBlend, true> : raster_sum_fwd_kernel<kModeNoBlend, false>, grid,
+                           dim3(128), s, tev, A);
+                break;
+            case kModeNoStore:
+                launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeNoStore, true> : raster_sum_fwd_kernel<kModeNoStore, false>, grid,
+                           dim3(128), s, tev, A);
+                break;
+            case kModeAdaptive:
+                launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeAdaptive, true> : raster_sum_fwd_kernel<kModeAdaptive, false>, grid,
+                           dim3(128), s, tev, A);
+                break;
+            case kModeSparseStamp:
+                if (!debug_ptr())
+                    return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: mode 7 needs gsvc_debug_set_ptr");
+                A.stamps = reinterpret_cast<long long *>(debug_ptr());
+                launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeSparseStamp, true> : raster_sum_fwd_kernel<kModeSparseStamp, false>, grid,
+                           dim3(64), s, tev, A);
+                break;
+            case kModeSparsePrio:
                 launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeSparsePrio, true>
                                        : raster_sum_fwd_kernel<kModeSparsePrio, false>,
                            grid, dim3(64), s, tev, A);
-            else
-                launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeSparse, true>
-                                       : raster_sum_fwd_kernel<kModeSparse, false>,
-                           grid, dim3(64), s, tev, A);
-            break;
-        case kModeBanded:
-            launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeBanded, true> : raster_sum_fwd_kernel<kModeBanded, false>, grid,
-                       dim3(128), s, tev, A);
-            break;
-        case kModeStamp:
-            A.stamps = reinterpret_cast<long long *>(A.final_Ts);
-            A.final_Ts = nullptr;
-            launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeStamp, true> : raster_sum_fwd_kernel<kModeStamp, false>, grid,
-                       dim3(128), s, tev, A);
-            break;
-        case kModeNoBlend:
-            launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeNoBlend, true> : raster_sum_fwd_kernel<kModeNoBlend, false>, grid,
-                       dim3(128), s, tev, A);
-            break;
-        case kModeNoStore:
-            launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeNoStore, true> : raster_sum_fwd_kernel<kModeNoStore, false>, grid,
-                       dim3(128), s, tev, A);
-            break;
-        case kModeAdaptive:
-            launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeAdaptive, true> : raster_sum_fwd_kernel<kModeAdaptive, false>, grid,
-                       dim3(128), s, tev, A);
-            break;
-        case kModeSparseStamp:
-            if (!g_debug_ptr)
-                return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: mode 7 needs gsvc_debug_set_ptr");
-            A.stamps = reinterpret_cast<long long *>(g_debug_ptr);
-            launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeSparseStamp, true> : raster_sum_fwd_kernel<kModeSparseStamp, false>, grid,
-                       dim3(64), s, tev, A);
-            break;
-        default:
-            return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: unknown kernel mode %d", mode);
+                break;
+            default:
+                return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: unknown kernel mode %d", mode);
+        }
     }
     timing_end(s, tslot);
     return check_launch("rasterize_sum_forward");

@@ -472,6 +472,10 @@ constexpr int kBChunk = 64;   // entries staged at a time
 // laid out by length (tools/item_sim.py models it)
 constexpr int kBRun = 16;
 constexpr int kBThreads = 128;
+// The band kernel's speculative slab records and work-item split width: the
+// constants in the product library, A/B knobs 12 / 11 in the diagnostic one.
+__device__ __forceinline__ int spec_of(const TrainTileArgs &A) { return kDiag ? A.spec : kBSpec; }
+__device__ __forceinline__ int brun_of(const TrainTileArgs &A) { return kDiag ? A.brun : kBRun; }
 
 typedef float v2f __attribute__((ext_vector_type(2)));
 
@@ -745,7 +749,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     // grows from 2.6 us for the first workgroups of a CU to 11.7 us for its
     // 13th-16th, profiles/r03/stamps).  Raised over the order phase, a young
     // tile gets its round trips going while its elders compute.
-    if (A.prio) __builtin_amdgcn_s_setprio(3);
+    if (!kDiag || A.prio) __builtin_amdgcn_s_setprio(3);
     const int tile = xcd_remap(blockIdx.x, A.ntiles);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     long long *st = kStamp ? A.stamps + 8 * (size_t)tile : nullptr;
@@ -771,9 +775,9 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     int cid = 0;  // carried bins: the lane's candidate id
     const int *tcids = carry ? A.cids + (size_t)tile * kTilePix : nullptr;
     if (carry) {
-        cid = tcids[tid < A.spec ? tid : 0];
+        cid = tcids[tid < spec_of(A) ? tid : 0];
     } else {
-        const float4 *h0 = slab_rec(A.slab, A.ntiles, tile, tid < A.spec ? tid : 0);
+        const float4 *h0 = slab_rec(A.slab, A.ntiles, tile, tid < spec_of(A) ? tid : 0);
         r0 = h0[0];
         r1 = h0[1];
         r2 = h0[2];
@@ -818,7 +822,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
         // <= 64 candidates: wave 0 gathers their records and boxes by id, keeps
         // the tile's entries and ranks them by id (the others rank last)
         if (w == 0) {
-            if (lane >= A.spec && lane < n) cid = tcids[lane];
+            if (lane >= spec_of(A) && lane < n) cid = tcids[lane];
             bool mem = false;
             if (lane < n) {
                 const uint2 b = A.cbox[cid];
@@ -839,7 +843,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             if (lane == 0) S.nsel = nm;
         }
     } else if (!dense) {
-        if (tid >= A.spec && tid < n) {
+        if (tid >= spec_of(A) && tid < n) {
             const float4 *h = slab_rec(A.slab, A.ntiles, tile, tid);
             r0 = h[0];
             r1 = h[1];
@@ -890,7 +894,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     }
     __syncthreads();
     if (carry && (!dense || brute)) n = S.nsel;
-    if (A.prio) __builtin_amdgcn_s_setprio(0);
+    if (!kDiag || A.prio) __builtin_amdgcn_s_setprio(0);
     if (kStamp && tid == 0) st[1] = tstamp();
 
     // 2. forward: this wave's band against the entries that can reach it
@@ -928,7 +932,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             stage_chunk(s_key + c0, cnt);
             __syncthreads();
         }
-        if (A.grouped) {
+        if (!kDiag || A.grouped) {
             // lane groups: 8 groups of 8 lanes, each a 4-row x 4-column block of
             // the band (grp); every group walks, in rank order, only the
             // entries whose rectangle reaches its block (lists[it][grp], padded
@@ -951,7 +955,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                 fin = __builtin_isfinite(C.y) && __builtin_isfinite(C.z) && __builtin_isfinite(C.w);
                 cutok = fin && geo_cut_ok(S.geo[lane], C.x);
             }
-            if (A.diag & 4) gm = 0u;  // diagnostic: no forward blending (wrong results)
+            if (kDiag && (A.diag & 4)) gm = 0u;  // diagnostic: no forward blending (wrong results)
             // row `lane` of the lists: the sentinel, then the entries
             *reinterpret_cast<unsigned long long *>(wlist + 8 * lane) = 0x4040404040404040ull;
             __builtin_amdgcn_wave_barrier();
@@ -1014,7 +1018,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             fin = __builtin_isfinite(C.y) && __builtin_isfinite(C.z) && __builtin_isfinite(C.w);
         }
         unsigned long long m = __ballot(keep);
-        if (A.diag & 4) m = 0ull;  // diagnostic: no forward blending (wrong results)
+        if (kDiag && (A.diag & 4)) m = 0ull;  // diagnostic: no forward blending (wrong results)
         const unsigned long long fm = __ballot(fin);  // entries with a finite colour
         if (m && (m & ~fm) == 0) {
             // every colour finite (the rule): the select-free blend
@@ -1111,7 +1115,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     }
     if (kStamp && tid == 0) st[3] = tstamp();
 
-    if (A.diag & 2) return;  // diagnostic: no backward (wrong results)
+    if (kDiag && (A.diag & 2)) return;  // diagnostic: no backward (wrong results)
     // 4. backward, kBChunk entries at a time (sparse tiles: the forward's staging).
     // Each wave takes the rectangle rows of its own band -- the v_out rows it
     // wrote itself -- so the waves need no barrier until the chunk's flush.
@@ -1138,8 +1142,8 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                 const int ry0 = max((int)((rc >> 8) & 15u), y_lo), ry1 = min((int)((rc >> 12) & 15u), y_hi);
                 const int rw = (int)((rc >> 4) & 15u) - (int)(rc & 15u) + 1;
                 if (ry0 <= ry1) {
-                    items = (ry1 - ry0 + 1) * (rw > A.brun ? 2 : 1);
-                    ilen = rw > A.brun ? (rw + 1) >> 1 : rw;
+                    items = (ry1 - ry0 + 1) * (rw > brun_of(A) ? 2 : 1);
+                    ilen = rw > brun_of(A) ? (rw + 1) >> 1 : rw;
                 }
             }
         }
@@ -1151,7 +1155,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             const unsigned long long below = (1ull << lane) - 1ull;
             int rank = 0, seen = 0;
             unsigned long long left = __ballot(true);
-            if (A.diag & 64) {  // A/B: entry order
+            if (kDiag && (A.diag & 64)) {  // A/B: entry order
                 rank = lane;
                 left = 0ull;
             }
@@ -1200,14 +1204,14 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                 const int j = item - eoff;  // item index within the entry
                 const int rx0 = (int)(ro & 15u), rx1 = (int)((ro >> 4) & 15u);
                 const int rwid = rx1 - rx0 + 1;
-                const int ipr = rwid > A.brun ? 2 : 1;
+                const int ipr = rwid > brun_of(A) ? 2 : 1;
                 const int jr = ipr == 1 ? j : (j >> 1);
                 const int row = max((int)((ro >> 8) & 15u), y_lo) + jr;
                 const int half = (rwid + 1) >> 1;
                 const int cs = ipr == 1 ? rx0 : rx0 + half * (j & 1);
                 const int ce = min(ipr == 1 ? rx1 : min(cs + half - 1, rx1), A.img_w - 1 - (int)tx0);
                 const float pyf = ty0 + (float)row;
-                if ((int)pyf < A.img_h && !(A.diag & 8)) {  // diag 8: no pixel work
+                if ((int)pyf < A.img_h && !(kDiag && (A.diag & 8))) {  // diag 8: no pixel work
                     const float ex = G.x, eha = G.z, eb = G.w;
                     const float dy = G.y - pyf;
                     const float cq = (C.x * dy) * dy;  // splat_sigma_h's row terms
@@ -1271,8 +1275,8 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             // an entry has at most 8 items in a band unless rows split in two
             // (brun < 16): runs of <= 8 lanes need no row_shr:8 step (a run
             // crossing a 16-lane row still takes the row broadcast)
-            if (!(A.diag & 16)) {  // diag 16: no run sums (wrong)
-                if (A.brun < 16)
+            if (!(kDiag && (A.diag & 16))) {  // diag 16: no run sums (wrong)
+                if (brun_of(A) < 16)
                     wave_seg_sums<true>(g, own);
                 else
                     wave_seg_sums<false>(g, own);
@@ -1303,7 +1307,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                     unsafeAtomicAdd(A.grad + (size_t)g * 16 + c, v);
             }
         } else {
-            for (int q = tid; q < gn * 8 && !(A.diag & 32); q += kBThreads) {  // diag 32: no atomics
+            for (int q = tid; q < gn * 8 && !(kDiag && (A.diag & 32)); q += kBThreads) {  // diag 32: no atomics
                 const int e = q >> 3, c = q & 7;
                 const float *ea = &S.part[0][0];
                 unsafeAtomicAdd(A.grad + (size_t)S.gid[e] * 16 + c,
@@ -1832,12 +1836,12 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     T.err = w.err;
     T.out = render_out;
     // A/B knob 11: the band kernel's work-item split width (default kBRun)
-    T.brun = g_knobs[11] >= 4 && g_knobs[11] <= 16 ? g_knobs[11] : kBRun;
+    T.brun = knob(11) >= 4 && knob(11) <= 16 ? knob(11) : kBRun;
     // A/B knob 12: speculative slab records per tile (default kBSpec)
-    T.spec = g_knobs[12] > 0 && g_knobs[12] <= 64 ? g_knobs[12] : kBSpec;
-    T.diag = g_knobs[13];
-    T.grouped = g_knobs[14] != 1;
-    T.prio = g_knobs[16] != 1;  // A/B knob 16 = 1: no raised priority
+    T.spec = knob(12) > 0 && knob(12) <= 64 ? knob(12) : kBSpec;
+    T.diag = knob(13);
+    T.grouped = knob(14) != 1;
+    T.prio = knob(16) != 1;  // A/B knob 16 = 1: no raised priority
     T.det_off = det_off;
     T.det_part = det_part;
     T.det_cap = det_capacity;
@@ -1851,35 +1855,45 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
         T.counts_clear = fs.counts_next;
         T.m_dev = fs.m_acc;
         T.m_clear = carry ? fs.m_clear : nullptr;
-        if (g_knobs[5] == 2 && g_debug_ptr && !carry) {  // diagnostic: per-tile stamps
-            T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
-            auto kfn = train_tile_kernel<true>;
-            hipLaunchKernelGGL(kfn, dim3(ntiles), dim3(kT), 0, s, T);
-        } else if (g_knobs[5] == 3 && g_debug_ptr) {  // diagnostic: per-tile stamps, band kernel
-            T.stamps = reinterpret_cast<long long *>(g_debug_ptr);
-            if (carry)
-                hipLaunchKernelGGL((train_tile_band_kernel<true, false, true>), dim3(ntiles),
-                                   dim3(kBThreads), 0, s, T);
-            else
-                hipLaunchKernelGGL(train_tile_band_kernel<true>, dim3(ntiles), dim3(kBThreads), 0, s, T);
-        } else {
-            // knob 8 = 1: the 256-thread workgroup-per-tile kernel (A/B; atomics only)
-            const bool old_kernel = g_knobs[8] == 1 && !det && !carry;
-            const dim3 grid(ntiles);
-            hipEvent_t tev[2];
-            const int tslot = timing_begin(s, tev, kTimingTrainTile);
-            if (old_kernel)
-                launch_timed(train_tile_kernel<false>, dim3(ntiles), dim3(kT), 0, s, tev, T);
-            else if (det && carry)
-                launch_timed(train_tile_band_kernel<false, true, true>, grid, dim3(kBThreads), 0, s, tev, T);
-            else if (det)
-                launch_timed(train_tile_band_kernel<false, true>, grid, dim3(kBThreads), 0, s, tev, T);
-            else if (carry)
-                launch_timed(train_tile_band_kernel<false, false, true>, grid, dim3(kBThreads), 0, s, tev, T);
-            else
-                launch_timed(train_tile_band_kernel<false>, grid, dim3(kBThreads), 0, s, tev, T);
-            timing_end(s, tslot, kTimingTrainTile);
+        if constexpr (kDiag) {
+            if (knob(5) == 2 && debug_ptr() && !carry) {  // diagnostic: per-tile stamps
+                T.stamps = reinterpret_cast<long long *>(debug_ptr());
+                auto kfn = train_tile_kernel<true>;
+                hipLaunchKernelGGL(kfn, dim3(ntiles), dim3(kT), 0, s, T);
+                return check_launch("train_step_sum: tiles");
+            }
+            if (knob(5) == 3 && debug_ptr()) {  // diagnostic: per-tile stamps, band kernel
+                T.stamps = reinterpret_cast<long long *>(debug_ptr());
+                if (carry)
+                    hipLaunchKernelGGL((train_tile_band_kernel<true, false, true>), dim3(ntiles),
+                                       dim3(kBThreads), 0, s, T);
+                else
+                    hipLaunchKernelGGL(train_tile_band_kernel<true>, dim3(ntiles), dim3(kBThreads), 0, s, T);
+                return check_launch("train_step_sum: tiles");
+            }
         }
+        const dim3 grid(ntiles);
+        hipEvent_t tev[2];
+        const int tslot = timing_begin(s, tev, kTimingTrainTile);
+        bool launched = false;
+        if constexpr (kDiag) {
+            // knob 8 = 1: the 256-thread workgroup-per-tile kernel (A/B; atomics only)
+            if (knob(8) == 1 && !det && !carry) {
+                launch_timed(train_tile_kernel<false>, dim3(ntiles), dim3(kT), 0, s, tev, T);
+                launched = true;
+            }
+        }
+        if (launched)
+            ;
+        else if (det && carry)
+            launch_timed(train_tile_band_kernel<false, true, true>, grid, dim3(kBThreads), 0, s, tev, T);
+        else if (det)
+            launch_timed(train_tile_band_kernel<false, true>, grid, dim3(kBThreads), 0, s, tev, T);
+        else if (carry)
+            launch_timed(train_tile_band_kernel<false, false, true>, grid, dim3(kBThreads), 0, s, tev, T);
+        else
+            launch_timed(train_tile_band_kernel<false>, grid, dim3(kBThreads), 0, s, tev, T);
+        timing_end(s, tslot, kTimingTrainTile);
         return check_launch("train_step_sum: tiles");
     };
     if (!tiled) {
@@ -1917,7 +1931,7 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     P.loss = loss;
     if (carry && update) {
         // 2: M as a flag (A/B knob 22 = 1: the exact count by atomics)
-        P.carry = g_knobs[22] == 1 ? 1 : 2;
+        P.carry = knob(22) == 1 ? 1 : 2;
         P.tbx = tbx;
         P.tby = tby;
         P.xys = (float2 *)w.f.xys;
@@ -1930,26 +1944,31 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     P.loss_seq = loss_seq;
     // one extra (first) workgroup sums the loss, beside the splat workgroups
     // A/B knob 21 = 64, 128, 192 or 512: other splat workgroup sizes
-    const int sb = g_knobs[21] == 64 || g_knobs[21] == 128 || g_knobs[21] == 192 || g_knobs[21] == 512
-                       ? g_knobs[21]
+    const int sb = knob(21) == 64 || knob(21) == 128 || knob(21) == 192 || knob(21) == 512
+                       ? knob(21)
                        : 256;
     const int blocks = (num_points > 0 ? ceil_div(num_points, sb) : 0) + 1;
     hipEvent_t tev[2];
     const int tslot = timing_begin(s, tev, kTimingTrainSplat);
-    if (g_knobs[5] == 4 && g_debug_ptr) {  // diagnostic: per-wave stamps of the splat kernel
-        P.stamps = reinterpret_cast<long long *>(g_debug_ptr);
-        hipLaunchKernelGGL(train_splat_kernel<true>, dim3(ceil_div(num_points, 256) + 1), dim3(256), 0, s, P);
-    } else if (sb == 64) {
-        launch_timed(train_splat_kernel<false, 64>, dim3(blocks), dim3(64), 0, s, tev, P);
-    } else if (sb == 128) {
-        launch_timed(train_splat_kernel<false, 128>, dim3(blocks), dim3(128), 0, s, tev, P);
-    } else if (sb == 192) {
-        launch_timed(train_splat_kernel<false, 192>, dim3(blocks), dim3(192), 0, s, tev, P);
-    } else if (sb == 512) {
-        launch_timed(train_splat_kernel<false, 512>, dim3(blocks), dim3(512), 0, s, tev, P);
-    } else {
-        launch_timed(train_splat_kernel<false>, dim3(blocks), dim3(256), 0, s, tev, P);
+    bool launched = false;
+    if constexpr (kDiag) {
+        launched = true;
+        if (knob(5) == 4 && debug_ptr()) {  // diagnostic: per-wave stamps of the splat kernel
+            P.stamps = reinterpret_cast<long long *>(debug_ptr());
+            hipLaunchKernelGGL(train_splat_kernel<true>, dim3(ceil_div(num_points, 256) + 1), dim3(256), 0, s, P);
+        } else if (sb == 64) {
+            launch_timed(train_splat_kernel<false, 64>, dim3(blocks), dim3(64), 0, s, tev, P);
+        } else if (sb == 128) {
+            launch_timed(train_splat_kernel<false, 128>, dim3(blocks), dim3(128), 0, s, tev, P);
+        } else if (sb == 192) {
+            launch_timed(train_splat_kernel<false, 192>, dim3(blocks), dim3(192), 0, s, tev, P);
+        } else if (sb == 512) {
+            launch_timed(train_splat_kernel<false, 512>, dim3(blocks), dim3(512), 0, s, tev, P);
+        } else {
+            launched = false;
+        }
     }
+    if (!launched) launch_timed(train_splat_kernel<false>, dim3(blocks), dim3(256), 0, s, tev, P);
     timing_end(s, tslot, kTimingTrainSplat);
     rc = check_launch("train_step_sum: splats");
     if (rc) return rc;

@@ -101,16 +101,11 @@ def _ptr_f32(t: Optional[Tensor], name: str, numel: int, keep: list) -> int:
     return t.data_ptr()
 
 
-_render_fn = None
-
-
 def _render_frame_fn():
-    """gsvc_render_frame_sum_ex: the frame render with the training path's
-    splat order (projection in spatial order, windowed slot atomics)."""
-    global _render_fn
-    if _render_fn is None:
-        _render_fn = L.load().gsvc_render_frame_sum_ex
-    return _render_fn
+    """gsvc_render_frame_sum_ex of the active library: the frame render with the
+    training path's splat order (projection in spatial order, windowed slot
+    atomics)."""
+    return L.load().gsvc_render_frame_sum_ex
 
 
 class BoundRender:
@@ -132,7 +127,8 @@ class BoundRender:
                   _ptr_f32(cholesky_bound, "cholesky_bound", 3, keep), _ptr_f32(rgb_w, "rgb_w", n, keep))
         if keep:  # a converted copy would go stale: bind only tensors used in place
             raise ValueError("BoundRender needs contiguous float32 CUDA tensors")
-        self.fn = _render_frame_fn()
+        self.lib = L.load()
+        self.fn = self.lib.gsvc_render_frame_sum_ex
 
     def matches(self, tensors) -> bool:
         return (len(tensors) == len(self.tensors)
@@ -149,7 +145,7 @@ class BoundRender:
                      _order_flags(fw))
         if rc != 0:
             fw.dirty = True
-            msg = L.load().gsvc_last_error().decode(errors="replace")
+            msg = self.lib.gsvc_last_error().decode(errors="replace")
             raise RuntimeError(f"gsvc_render_frame_sum failed (status {rc}): {msg}")
         fw.frame += 1
         fw.hint.update(fw.meta)

@@ -252,7 +252,8 @@ class BoundStep:
         a.adan_state = ctypes.addressof(self.state)
         a.adan_hparams = ctypes.addressof(self.hp)
         self.args_ref = ctypes.byref(a)
-        self.fn = L.load().gsvc_train_step_sum_args
+        self.lib = L.load()  # bound once: the library of every call of this step
+        self.fn = self.lib.gsvc_train_step_sum_args
         self.host = None  # coherent host words: mse, l1, sequence, (det) pairs
         self.seq = 0
         self.stream = None
@@ -268,7 +269,7 @@ class BoundStep:
     def __del__(self):
         if getattr(self, "host", None) is not None:
             try:
-                L.load().gsvc_host_free(self.host)
+                self.lib.gsvc_host_free(self.host)
             except Exception:  # interpreter shutdown
                 pass
             self.host = None
@@ -295,7 +296,7 @@ class BoundStep:
         for k, x in enumerate(adan_hparams):
             hp[k] = x
         ws = _workspace(self.dev, self.n, self.H, self.W)
-        lib = L.load()
+        lib = self.lib
         a = self.args
         if self.host is None:
             self.host = lib.gsvc_host_alloc(16)

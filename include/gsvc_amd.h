@@ -92,11 +92,6 @@ int gsvc_timing_collect(float *ms, int max_out, int *count);
 int gsvc_timing_enable_channel(int channel, int max_launches, int every, int how);
 int gsvc_timing_collect_channel(int channel, float *ms, int max_out, int *count);
 
-/* Tuning / A-B knob for kernel variants (tools/kbench.py).  key 0 forces the
- * sum-forward kernel mode (0 = automatic), key 3 the per-tile threshold of
- * mode 6; returns the previous value.  Not part of the reference interface;
- * results are identical for every value (modes 4/5 are ablations). */
-int gsvc_debug_set(int key, int value);
 /* The unit-opacity alpha cut as a sigma threshold (alpha_cut.hip): the
  * kernels' constant, and a device scan over all 2^31 non-negative float
  * patterns of the reference predicate (forward.cu:598-606 at opacity 1) into
@@ -120,8 +115,6 @@ int gsvc_host_free(void *p);
  * reports a failed kernel, and then require it.  The fused training step's
  * early loss read-back (GSVC_TRAIN_LOSS_SEQ).  Not part of the reference. */
 int gsvc_wait_host_seq(const unsigned *word, unsigned seq, void *stream, int spin_us);
-/* Diagnostic device buffer for timestamp kernel variants (int64 per tile x 4). */
-void gsvc_debug_set_ptr(void *ptr);
 
 /* ---------------------------------------------------------------------------
  * 2D projection.

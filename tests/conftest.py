@@ -1,3 +1,4 @@
+import contextlib
 import glob
 import os
 import sys
@@ -24,6 +25,25 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "cuda" in getattr(item, "fixturenames", ()) and item.get_closest_marker("gpu") is None:
             item.add_marker(pytest.mark.gpu)
+
+
+@contextlib.contextmanager
+def knobs(*pairs):
+    """Run the block with A/B knobs (key, value) set: on the product library
+    when every value is 0 (the product's own choices), else on the diagnostic
+    library (gsvc_amd._lib.diagnostic(), the only one with knobs).  Yields the
+    library the block's ops use."""
+    from gsvc_amd import _lib
+    if all(v == 0 for _, v in pairs):
+        yield _lib.load()
+        return
+    with _lib.diagnostic() as lib:
+        olds = [(k, lib.gsvc_debug_set(k, v)) for k, v in pairs]
+        try:
+            yield lib
+        finally:
+            for k, v in reversed(olds):
+                lib.gsvc_debug_set(k, v)
 
 
 def load_golden(name):

@@ -11,10 +11,11 @@ import torch
 from conftest import REPO
 
 HEADER = os.path.join(REPO, "include", "gsvc_amd.h")
+DIAG_HEADER = os.path.join(REPO, "include", "gsvc_amd_diag.h")
 
 
-def _declared():
-    src = open(HEADER).read()
+def _declared(header=HEADER):
+    src = open(header).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(gsvc_[a-z0-9_]+)\s*\(", src)))
 
@@ -32,6 +33,30 @@ def test_library_exports_all_symbols():
     assert not missing, missing
     # the ctypes signature table covers exactly the declared ABI
     assert sorted(_lib.symbols()) == _declared()
+
+
+def test_product_library_has_no_diagnostics():
+    """the A/B knobs and diagnostic kernel variants live only in
+    libgsvc_amd_diag.so (include/gsvc_amd_diag.h); the product library exports
+    none of its entry points and carries none of its kernel variants."""
+    import subprocess
+    from gsvc_amd import _lib
+    diag = _declared(DIAG_HEADER)
+    assert diag == ["gsvc_debug_set", "gsvc_debug_set_ptr"]
+    prod = ctypes.CDLL(_lib.LIB_PATH)
+    assert not [n for n in diag if hasattr(prod, n)]
+    dlib = ctypes.CDLL(_lib.DIAG_LIB_PATH)
+    assert not [n for n in _declared() + diag if not hasattr(dlib, n)]
+    assert sorted(_lib.symbols(diag=True)) == sorted(_declared() + diag)
+
+    # the timestamped / ablation / A/B variants are diagnostic-only symbols
+    names = subprocess.run(["nm", "-C", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    dnames = subprocess.run(["nm", "-C", _lib.DIAG_LIB_PATH], capture_output=True, text=True).stdout
+    for variant in ("raster_sum_fwd_kernel<7,", "raster_sum_fwd_kernel<3,", "train_tile_kernel<",
+                    "train_tile_band_kernel<true", "frame_project_kernel<1, true>",
+                    "train_splat_kernel<true"):
+        assert variant not in names, variant
+        assert variant in dnames, variant
 
 
 def test_abi_version_and_queries():

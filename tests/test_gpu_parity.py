@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden_names, load_golden
+from conftest import golden_names, knobs, load_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -390,20 +390,15 @@ def test_raster_sum_forward_nonfinite_colours(cuda, oracle, name):
 def test_render_frame_nonfinite_colours(cuda, oracle, mode):
     """The same through the frame path (both composite variants: 1 sparse,
     2 banded) with its fused clamp: torch.clamp keeps NaN, clamps +-inf."""
-    from gsvc_amd import _lib
     from gsvc_amd.render import render_frame_sum
     z = load_golden("sum_64x96_n300")
     H, W = int(z["H"]), int(z["W"])
     colors = _nonfinite_colours(z["colors"], np.random.default_rng(6))
     # the fixture's means2d / L / colours as the frame inputs (no tanh, zero bound)
     bound = torch.zeros(3, device="cuda")
-    lib = _lib.load()
-    prev = lib.gsvc_debug_set(0, mode)
-    try:
+    with knobs((0, mode)):
         out = render_frame_sum(T(z["means2d"]), T(z["L"]), T(colors), H, W,
                                torch.ones(3, device="cuda"), xyz_tanh=False, cholesky_bound=bound)
-    finally:
-        lib.gsvc_debug_set(0, prev)
     r = oracle.render_sum(z["means2d"], z["L"], colors, np.ones((len(colors), 1), np.float32), H, W)
     ref = np.clip(r["out"], 0, 1).transpose(2, 0, 1)[None]
     g = N(out)

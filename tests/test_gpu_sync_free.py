@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden_names, load_golden
+from conftest import golden_names, knobs, load_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -221,7 +221,6 @@ def _op_path_frame(means, L, colors, opac, H, W, bg):
 @pytest.mark.parametrize("case", ["sum_37x53_n120", "sum_stress_48x48_n700", "1080p_10k",
                                   "1080p_50k"])
 def test_render_frame_matches_op_path(cuda, oracle, mode, case):
-    from gsvc_amd import _lib
     from gsvc_amd.render import render_sum_frame
     if case.startswith("sum_"):
         z = load_golden(case)
@@ -232,12 +231,8 @@ def test_render_frame_matches_op_path(cuda, oracle, mode, case):
         n = 10000 if case.endswith("10k") else 50000
         means, L, colors, opac = oracle.synthetic_frame(n, seed=n + 1, rgb_w=2.0)
     bg = torch.ones(3, device="cuda")
-    lib = _lib.load()
-    prev = lib.gsvc_debug_set(0, mode)
-    try:
+    with knobs((0, mode)):
         fast = render_sum_frame(T(means), T(L), T(colors), T(opac), H, W, _tb(H, W), bg)
-    finally:
-        lib.gsvc_debug_set(0, prev)
     with torch.no_grad():
         ref = _op_path_frame(T(means), T(L), T(colors), T(opac), H, W, bg)
     assert fast.shape == (1, 3, H, W) and fast.is_contiguous()
@@ -386,15 +381,12 @@ def test_render_frames_batch_matches_single(cuda, mode, H, W, sizes, cluster):
     """gsvc_render_frames_sum: every frame of the batch bit-identical to its
     own one-frame render -- empty frames, an all-background frame, tiles past
     256 entries (the id-range brute rebuild of the frame's own splats)."""
-    from gsvc_amd import _lib
     from gsvc_amd.render import render_frame_sum, render_frames_sum
     xyz, chol, feat = _frame_models(sizes, H, W, seed=len(sizes) + H, cluster_frame=cluster)
     bound = torch.tensor([0.5, 0.0, 0.5], device="cuda")
     rgbw = torch.rand(sum(sizes), 1, device="cuda") + 0.5
     bg = torch.tensor([0.3, 0.6, 0.9], device="cuda")
-    lib = _lib.load()
-    prev = lib.gsvc_debug_set(0, mode)
-    try:
+    with knobs((0, mode)):
         outs = [render_frames_sum(xyz, chol, feat, sizes, H, W, bg, cholesky_bound=bound,
                                   rgb_w=rgbw) for _ in range(3)]  # parity slots reused
         off = 0
@@ -405,7 +397,5 @@ def test_render_frames_batch_matches_single(cuda, mode, H, W, sizes, cluster):
             for o in outs:
                 assert torch.equal(o[b], one[0]), (b, n)
             off += n
-    finally:
-        lib.gsvc_debug_set(0, prev)
     if sizes[2] == 0:  # a frame without splats is the background
         assert torch.equal(outs[0][2], bg.view(3, 1, 1).expand(3, H, W))

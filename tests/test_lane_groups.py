@@ -9,6 +9,8 @@ import numpy as np
 import pytest
 import torch
 
+from conftest import knobs
+
 pytestmark = pytest.mark.gpu
 
 H, W = 1080, 1920
@@ -22,32 +24,18 @@ def _tb(h, w):
     return ((w + 15) // 16, (h + 15) // 16, 1)
 
 
-def _knobs(lib, pairs):
-    return [(k, lib.gsvc_debug_set(k, v)) for k, v in pairs]
-
-
-def _restore(lib, olds):
-    for k, v in reversed(olds):
-        lib.gsvc_debug_set(k, v)
-
-
 @pytest.mark.parametrize("n,chol", [(10000, 1.0), (50000, 1.0), (50000, 3.0), (20000, 8.0)])
 def test_composite_lists_bit_identical(cuda, oracle, n, chol):
-    from gsvc_amd import _lib
     from gsvc_amd.render import render_sum_frame
-    lib = _lib.load()
     means, L, colors, opac = oracle.synthetic_frame(n, seed=n + 17, rgb_w=2.0, chol_scale=chol)
     bg = torch.ones(3, device="cuda")
     outs = {}
     # mode 1 sparse / 2 banded; knob 15 = 1: lists on every chunk, 65: never
     for mode in (1, 2):
         for lists in (0, 1, 65):
-            olds = _knobs(lib, [(0, mode), (15, lists)])
-            try:
+            with knobs((0, mode), (15, lists)):
                 outs[(mode, lists)] = render_sum_frame(T(means), T(L), T(colors), T(opac), H, W,
                                                        _tb(H, W), bg)
-            finally:
-                _restore(lib, olds)
     ref = outs[(1, 65)]
     for key, out in outs.items():
         assert torch.equal(out, ref), key
@@ -71,17 +59,14 @@ def test_train_forward_lists_bit_identical(cuda, chol):
     """The fused step's render with the band kernel's lists (default) and
     without (knob 14 = 1) is the same image; the gradients agree to the float
     atomics' summation order."""
-    from gsvc_amd import _lib
     from gsvc_amd.frame import make_frame_model, synthetic_gt
-    lib = _lib.load()
     gt = synthetic_gt(256, 384, 3, cuda)
     res = []
     for knob in (0, 1):
         model = make_frame_model(256, 384, 6000, cuda, seed=21)
         with torch.no_grad():
             model._cholesky.mul_(chol)
-        olds = _knobs(lib, [(14, knob)])
-        try:
+        with knobs((14, knob)):
             render = torch.empty(3, 256, 384, device=cuda)
             g = torch.empty(6000, 9, device=cuda)
             from gsvc_amd.train import train_step_sum
@@ -90,8 +75,6 @@ def test_train_forward_lists_bit_identical(cuda, chol):
                                     gt.reshape(3, 256, 384).contiguous(), 256, 384, "L2", render_out=render, grads_out=g)
             torch.cuda.synchronize()
             res.append((render.clone(), g.clone(), losses.cpu().clone()))
-        finally:
-            _restore(lib, olds)
     assert torch.equal(res[0][0], res[1][0])
     torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(res[0][2], res[1][2], rtol=0, atol=0)
@@ -108,9 +91,7 @@ def test_composite_sigma_cut_bit_identical(cuda, oracle, case):
     gives the same bits as the test as written -- including chunks that hold a
     NaN or infinite colour, an overflowing conic or a non-unit opacity, which
     must keep the written test (bitwise compare: NaN pixels included)."""
-    from gsvc_amd import _lib
     from gsvc_amd.render import render_sum_frame
-    lib = _lib.load()
     n = 30000 if case == "unit_dense" else 8000
     means, L, colors, opac = oracle.synthetic_frame(
         n, seed=7, rgb_w=2.0, chol_scale=3.0 if case == "unit_dense" else 1.0)
@@ -127,11 +108,8 @@ def test_composite_sigma_cut_bit_identical(cuda, oracle, case):
     bg = torch.ones(3, device="cuda")
     outs = []
     for knob in (0, 1):
-        olds = _knobs(lib, [(0, 1), (19, knob)])
-        try:
+        with knobs((0, 1), (19, knob)):
             outs.append(render_sum_frame(T(means), T(L), T(colors), T(opac), H, W, _tb(H, W), bg))
-        finally:
-            _restore(lib, olds)
     assert torch.equal(_bits(outs[0]), _bits(outs[1])), case
     if case == "unit_dense":
         ref = oracle.render_sum(means, L, colors, opac, H, W)["out"]

@@ -21,7 +21,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import load_golden
+from conftest import knobs, load_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -30,11 +30,8 @@ pytestmark = pytest.mark.gpu
 def tile_kernel(request, cuda):
     """The fused step's tile kernel: two 8-row band waves per tile (production)
     or the 256-thread workgroup per tile (gsvc_debug_set(8, 1), A/B)."""
-    from gsvc_amd import _lib
-    lib = _lib.load()
-    old = lib.gsvc_debug_set(8, 1 if request.param == "wg256" else 0)
-    yield request.param
-    lib.gsvc_debug_set(8, old)
+    with knobs((8, 1 if request.param == "wg256" else 0)):
+        yield request.param
 
 
 def _model(H, W, n, dev, seed, chol_scale=1.0, **kw):

@@ -15,6 +15,9 @@ import time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
+# A/B knobs and timestamped variants: the diagnostic library (gsvc_amd/_lib.py)
+os.environ.setdefault("GSVC_DIAG", "1")
+
 import torch  # noqa: E402
 
 H, W = 1080, 1920

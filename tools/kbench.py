@@ -22,6 +22,9 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 import numpy as np  # noqa: E402
+# A/B knobs and timestamped variants: the diagnostic library (gsvc_amd/_lib.py)
+os.environ.setdefault("GSVC_DIAG", "1")
+
 import torch  # noqa: E402
 
 from gsvc_amd import _lib as L  # noqa: E402

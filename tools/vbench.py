@@ -11,6 +11,9 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
+# A/B knobs and timestamped variants: the diagnostic library (gsvc_amd/_lib.py)
+os.environ.setdefault("GSVC_DIAG", "1")
+
 import torch  # noqa: E402
 
 import bench  # noqa: E402
