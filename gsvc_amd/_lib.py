@@ -180,6 +180,36 @@ def load_product():
     return _open(LIB_PATH, False)
 
 
+TORCH_EXT_PATH = os.path.join(_HERE, "lib", "_torch_ops.so")
+_ext = None
+
+
+def torch_ops():
+    """The C++ autograd Functions of the drop-in operators (csrc/torch_ops.cpp,
+    a torch extension module over libgsvc_amd.so); raises if it has not been
+    built -- there is no silent fallback."""
+    global _ext
+    if _ext is None:
+        with _lock:
+            if _ext is None:
+                if not os.path.exists(TORCH_EXT_PATH):
+                    raise RuntimeError(f"gsvc_amd: {TORCH_EXT_PATH} not found; build it with "
+                                       "`python -m gsvc_amd.build`")
+                import importlib.util
+                spec = importlib.util.spec_from_file_location("_torch_ops", TORCH_EXT_PATH)
+                mod = importlib.util.module_from_spec(spec)
+                spec.loader.exec_module(mod)
+                if mod.abi_version() != ABI_VERSION:
+                    raise RuntimeError("gsvc_amd: _torch_ops.so was built for another ABI; rebuild")
+                _ext = mod
+    return _ext
+
+
+def product_active() -> bool:
+    """Whether the ops run on the product library (not inside diagnostic())."""
+    return load() is _libs.get(LIB_PATH)
+
+
 @contextlib.contextmanager
 def diagnostic():
     """Run this package's ops on libgsvc_amd_diag.so for the block (its A/B

@@ -31,6 +31,10 @@ ARCH = "gfx950"
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC", "-std=c++17",
          "-Wall", "-Wno-unused-result"]
 VARIANTS = {LIB: ("obj", []), LIB_DIAG: ("obj_diag", ["-DGSVC_DIAG"])}
+# the C++ autograd Functions of the drop-in operators (csrc/torch_ops.cpp),
+# a torch extension module linked against the product library
+TORCH_EXT = os.path.join(LIBDIR, "_torch_ops.so")
+TORCH_EXT_SRC = os.path.join(CSRC, "torch_ops.cpp")
 
 
 def _deps():
@@ -64,14 +68,47 @@ def build(force: bool = False, verbose: bool = False) -> str:
         mine = [o for l, o in objs if l == lib]
         if force or not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(o) for o in mine):
             tmp = lib + ".tmp"
-            cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *mine]
+            cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC",
+                   f"-Wl,-soname,{os.path.basename(lib)}", "-o", tmp, *mine]
             r = subprocess.run(cmd, capture_output=True, text=True)
             if r.returncode != 0:
                 raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
             os.replace(tmp, lib)
         if verbose:
             print(lib)
+    _build_torch_ext(force, verbose)
     return LIB
+
+
+def _build_torch_ext(force: bool, verbose: bool) -> None:
+    """hipcc (host C++ only) against torch's headers and libraries, with an
+    rpath to this directory for libgsvc_amd.so."""
+    if (not force and os.path.exists(TORCH_EXT) and os.path.getmtime(TORCH_EXT) >= max(
+            os.path.getmtime(TORCH_EXT_SRC), os.path.getmtime(LIB), _deps())):
+        if verbose:
+            print(TORCH_EXT)
+        return
+    import sysconfig
+
+    import torch
+    tdir = os.path.dirname(torch.__file__)
+    inc = [os.path.join(tdir, "include"), os.path.join(tdir, "include", "torch", "csrc", "api", "include"),
+           sysconfig.get_paths()["include"]]
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    tmp = TORCH_EXT + ".tmp"
+    cmd = [HIPCC, "-O2", "-fPIC", "-shared", "-std=c++17", "-w",
+           "-DTORCH_EXTENSION_NAME=_torch_ops", "-DTORCH_API_INCLUDE_EXTENSION_H",
+           f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+           *[f"-I{d}" for d in inc], TORCH_EXT_SRC,
+           f"-L{os.path.join(tdir, 'lib')}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
+           "-ltorch_hip", "-ltorch_python", f"-L{LIBDIR}", "-lgsvc_amd",
+           "-Wl,-rpath,$ORIGIN", "-o", tmp]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"torch extension build failed:\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, TORCH_EXT)
+    if verbose:
+        print(TORCH_EXT)
 
 
 if __name__ == "__main__":

@@ -2,7 +2,10 @@
 
 ``project_gaussians_2d`` (reference :12-57) and its autograd Function
 (reference :59-141) keep the signature, saved tensors and gradient routing of
-the reference; the kernels are gsvc_amd/csrc/project2d.hip.
+the reference; the kernels are gsvc_amd/csrc/project2d.hip.  The Function runs
+as C++ (csrc/torch_ops.cpp, ProjectFn: one call into the C ABI per forward,
+no Python in the backward); ``_ProjectGaussians2d`` below is the same in
+Python over ctypes, which the diagnostic library (its A/B knobs) uses.
 """
 from __future__ import annotations
 
@@ -11,6 +14,7 @@ from typing import Tuple
 from torch import Tensor
 from torch.autograd import Function
 
+from . import _lib
 from . import ops as _C
 
 
@@ -30,6 +34,14 @@ def project_gaussians_2d(
     Returns (xys [N,2], depths [N] (zeros), radii [N] int32, conics [N,3],
     num_tiles_hit [N] int32).
     """
+    if _lib.product_active():
+        tb = tile_bounds
+        xys, depths, radii, conics, nth = _lib.torch_ops().project_gaussians_2d(
+            means2d, L_elements, int(img_height), int(img_width), int(tb[0]), int(tb[1]),
+            int(tb[2]), float(clip_thresh))
+        # the 2D projection writes depth 0 for every splat (foward2d.cu:67,122)
+        depths._gsvc_zero_version = depths._version
+        return xys, depths, radii, conics, nth
     return _ProjectGaussians2d.apply(
         means2d.contiguous(),
         L_elements.contiguous(),

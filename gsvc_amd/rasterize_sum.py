@@ -4,6 +4,12 @@
 (reference :89-254) keep the reference's argument checks, M < 1 background
 branch, saved tensors and gradient routing.  Binning uses the fused hot path of
 ``utils.bin_and_sort_for_raster``; the blend is gsvc_amd/csrc/raster_sum.hip.
+
+The common case -- depths known to be zero (project_gaussians_2d's output),
+16x16 tiles, 3 channels, the bounded id buffers, no deterministic mode -- runs
+the Function as C++ (csrc/torch_ops.cpp, RasterSumFn: sync-free binning and
+composite in one call into the C ABI, backward without Python); every other
+case, and the diagnostic library, take ``_RasterizeGaussiansSum`` below.
 """
 from __future__ import annotations
 
@@ -13,8 +19,9 @@ import torch
 from torch import Tensor
 from torch.autograd import Function
 
+from . import _lib
 from . import ops as _C
-from .utils import bin_for_raster
+from .utils import BIN_CAPACITY_BUDGET, TILE_KEEP, bin_for_raster, depths_known_zero
 
 
 def rasterize_gaussians_sum(
@@ -54,6 +61,18 @@ def rasterize_gaussians_sum(
 
     if colors.ndimension() != 2:
         raise ValueError("colors must have dimensions (N, D)")
+
+    if (BLOCK_H == 16 and BLOCK_W == 16 and colors.shape[-1] == 3 and depths_known_zero(depths)
+            and min(xys.shape[0], TILE_KEEP) * ((img_width + 15) // 16) * ((img_height + 15) // 16)
+            <= BIN_CAPACITY_BUDGET
+            and not torch.are_deterministic_algorithms_enabled() and _lib.product_active()):
+        out_img, m_dev = _lib.torch_ops().rasterize_sum(xys, radii, conics, colors, opacity,
+                                                        background, int(img_height), int(img_width))
+        if return_alpha:
+            # final_Ts is identically 1 (0 when M < 1): out_alpha = 1 - final_Ts
+            final_Ts = (m_dev > 0).to(torch.float32).view(1, 1).expand(img_height, img_width)
+            return out_img, 1 - final_Ts
+        return out_img
 
     return _RasterizeGaussiansSum.apply(
         xys.contiguous(),

@@ -1,0 +1,111 @@
+"""The C++ autograd Functions of the drop-in operators (csrc/torch_ops.cpp):
+what GSVC's unchanged files run.  They must be the Python Functions'
+(project_gaussians_2d.py / rasterize_sum.py, ctypes over the same C ABI) bit
+for bit in the forward and in the projection backward, and within the float
+atomics' summation order in the rasterizer backward; the general cases keep
+the Python Functions.  Reference: project_gaussians_2d.py:59-141,
+rasterize_sum.py:89-254."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import knobs
+
+
+def test_cpu_tensors_raise():
+    """No CPU path (CPU suite: the argument check precedes any HIP call)."""
+    from gsvc_amd import _lib
+    ext = _lib.torch_ops()
+    x = torch.zeros(4, 2)
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        ext.project_gaussians_2d(x, torch.zeros(4, 3), 16, 16, 1, 1, 1, 0.01)
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        ext.rasterize_sum(x, torch.zeros(4, dtype=torch.int32), torch.zeros(4, 3), torch.zeros(4, 3),
+                          torch.ones(4, 1), torch.ones(3), 16, 16)
+
+
+def _inputs(n, H, W, seed, dev, chol=1.0):
+    g = torch.Generator().manual_seed(seed)
+    means = (2 * torch.rand(n, 2, generator=g) - 1).to(dev)
+    L = (torch.rand(n, 3, generator=g) * chol + torch.tensor([0.5, 0, 0.5]) * chol).to(dev)
+    col = torch.rand(n, 3, generator=g).to(dev)
+    return means, L, col
+
+
+def _run(means, L, col, H, W, python_path, v_out):
+    from gsplat.project_gaussians_2d import project_gaussians_2d
+    from gsplat.rasterize_sum import rasterize_gaussians_sum
+    m = means.clone().requires_grad_(True)
+    l = L.clone().requires_grad_(True)
+    c = col.clone().requires_grad_(True)
+    o = torch.ones(m.shape[0], 1, device=m.device)
+    tb = ((W + 15) // 16, (H + 15) // 16, 1)
+
+    def go():
+        xys, depths, radii, conics, nth = project_gaussians_2d(m, l, H, W, tb)
+        out = rasterize_gaussians_sum(xys, depths, radii, conics, nth, c, o, H, W, 16, 16,
+                                      background=torch.ones(3, device=m.device))
+        (out * v_out).sum().backward()
+        return out, xys, radii, conics, nth
+
+    if python_path:
+        with knobs((0, 1)):  # the diagnostic library: the Python Functions over ctypes
+            res = go()
+    else:
+        res = go()
+    torch.cuda.synchronize()
+    return [r.detach() for r in res], (m.grad, l.grad, c.grad)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,H,W,chol", [(1000, 256, 256, 1.0), (300, 37, 53, 1.0),
+                                        (50000, 1080, 1920, 1.0), (20000, 1080, 1920, 6.0)])
+def test_cpp_functions_match_python_functions(cuda, n, H, W, chol):
+    means, L, col = _inputs(n, H, W, n + H, cuda, chol)
+    v_out = torch.randn(H, W, 3, generator=torch.Generator().manual_seed(3)).to(cuda)
+    fast, gf = _run(means, L, col, H, W, False, v_out)
+    ref, gr = _run(means, L, col, H, W, True, v_out)
+    for a, b in zip(fast, ref):
+        assert torch.equal(a, b)
+    for a, b in zip(gf, gr):
+        scale = float(b.abs().max())
+        assert float((a - b).abs().max()) <= 1e-5 * max(scale, 1e-30)
+
+
+@pytest.mark.gpu
+def test_cpp_function_return_alpha_and_background(cuda):
+    """return_alpha (1 - final_Ts: 0 with intersections) and the M < 1 branch
+    (every splat off-screen: the background, alpha 1 - 0 = 1)."""
+    from gsplat.project_gaussians_2d import project_gaussians_2d
+    from gsplat.rasterize_sum import rasterize_gaussians_sum
+    H, W = 64, 80
+    tb = ((W + 15) // 16, (H + 15) // 16, 1)
+    means, L, col = _inputs(200, H, W, 5, cuda)
+    bg = torch.tensor([0.2, 0.4, 0.6], device=cuda)
+    for shift, alpha in ((0.0, 0.0), (50.0, 1.0)):
+        xys, depths, radii, conics, nth = project_gaussians_2d(means + shift, L, H, W, tb)
+        out, a = rasterize_gaussians_sum(xys, depths, radii, conics, nth, col,
+                                         torch.ones(200, 1, device=cuda), H, W, background=bg,
+                                         return_alpha=True)
+        assert a.shape == (H, W) and torch.all(a == alpha)
+        if shift:
+            assert torch.equal(out, bg.expand(H, W, 3))
+
+
+@pytest.mark.gpu
+def test_unchanged_caller_train_step_matches_fused(cuda):
+    """GaussianVideoFrame with fused_train / fused_render off (GSVC's own op
+    sequence over the C++ Functions) takes the same steps as the fused model:
+    PSNR per iteration within float-atomics reassociation."""
+    from gsvc_amd.frame import make_frame_model, synthetic_gt
+    H, W = 128, 192
+    gt = synthetic_gt(H, W, 2, cuda)
+    a = make_frame_model(H, W, 3000, cuda, seed=7)
+    b = make_frame_model(H, W, 3000, cuda, seed=7, fused_train=False, fused_render=False)
+    pa = [a.train_iter(gt, it)[1] for it in range(1, 21)]
+    pb = [b.train_iter(gt, it)[1] for it in range(1, 21)]
+    assert a.fused_steps == 20 and b.fused_steps == 0
+    assert np.allclose(pa, pb, rtol=0, atol=2e-3), (pa, pb)
+    with torch.no_grad():
+        ra, rb = a()["render"], b()["render"]
+    assert float((ra - rb).abs().max()) < 1e-3
