@@ -743,163 +743,6 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
     }
 }
 
-// ---------------------------------------------------------------------------
-// Persistent, software-pipelined composite of the frame path.
-//
-// The one-round kernel above launches one wave per tile (8160 waves for the
-// chip's 8192 slots at 1080p): every wave loads, then blends, then stores, all
-// at about the same time, so the ~25 MB of plane stores only start once the
-// loads and blends are done.  Here a grid of a few one-wave workgroups per
-// SIMD stays resident and wave j of XCD x blends the tiles first_x + j,
-// + W_x, + 2 W_x, ... of the contiguous tile range its XCD owns (xcd_remap's
-// ranges: the waves blending at one moment are neighbours, their row stores
-// meet in one L2).  One tile ahead of its blend a wave has the next tile's
-// slab records in flight, and the count after that: both are issued BEFORE
-// this tile's plane stores, and vector memory operations retire in issue
-// order, so the wait for them never waits for the stores -- the stores stream
-// out while the next tiles load and blend.  Per tile the work is the
-// one-round kernel's (sum_fwd_sparse: rank by id, lane-group lists, blend,
-// clamped plane stores), so the image is bit-identical.
-struct PipeRec {
-    float4 g, c, x;  // the lane's slab record (slot = lane)
-};
-
-__device__ __forceinline__ int pipe_frame(const SumFwdArgs &A, int g, int &tile) {
-    if (A.frames > 1) {
-        const int b = g / A.ntiles;
-        tile = g - b * A.ntiles;
-        return b;
-    }
-    tile = g;
-    return 0;
-}
-
-// Tile g's count (x) and its frame's M (y).
-__device__ __forceinline__ int2 pipe_load_count(const SumFwdArgs &A, int g) {
-    int tile;
-    const int b = pipe_frame(A, g, tile);
-    return make_int2((int)A.slab_counts[(size_t)b * A.counts_stride + tile],
-                     A.m_dev[(size_t)b * A.m_stride]);
-}
-
-// Tile g's first min(n, 64) slab records, one per lane.
-__device__ __forceinline__ PipeRec pipe_load_recs(const SumFwdArgs &A, int g, int n) {
-    int tile;
-    const int b = pipe_frame(A, g, tile);
-    PipeRec r;
-    r.g = r.c = r.x = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int lane = threadIdx.x & 63;
-    if (lane < n) {
-        const float4 *p = slab_rec(A.slab + b * A.slab_stride, A.ntiles, tile, lane);
-        r.g = p[0];
-        r.c = p[1];
-        r.x = p[2];
-    }
-    return r;
-}
-
-// One tile of the pipelined kernel: n_all entries (m = its frame's M), the
-// first min(n_all, 64) records in rc.  kBatch: frames > 1.
-template <bool kBatch>
-__device__ __forceinline__ void pipe_tile(const SumFwdArgs &A0, int g, int n_all, int m,
-                                          const PipeRec &rc, float4 *s_buf, int *s_ids) {
-    SumFwdArgs A = A0;
-    int tile = g;
-    if (kBatch) {
-        const int b = pipe_frame(A, g, tile);
-        A.slab += b * A.slab_stride;
-        A.slab_counts_clear += (size_t)b * A.counts_stride;
-        A.meta_out += (size_t)b * A.m_stride;
-        A.out += b * A.out_stride;
-        A.splat_begin = A.frame_off[b];
-        A.num_points = A.frame_off[b + 1];
-    }
-    if ((threadIdx.x & 63) == 0) {
-        A.slab_counts_clear[tile] = 0u;  // the next frame's counts
-        if (tile == 0) {
-            A.meta_out[0] = m;
-            A.meta_out[1] = 0;
-        }
-    }
-    // rasterize_sum.py:121-127: a frame without intersections is the background
-    float3 init = make_float3(0.f, 0.f, 0.f);
-    if (m < 1) {
-        n_all = 0;
-        init = make_float3(A.bg[0], A.bg[1], A.bg[2]);
-    }
-    const float4 *recs = slab_rec(A.slab, A.ntiles, tile, kHeadSlots) - 3 * kHeadSlots;
-    const float4 *head = slab_rec(A.slab, A.ntiles, tile, 0);
-    // more than 64 entries: the ids sorted in LDS (more than 256: the first
-    // 256 rebuilt from the bboxes), the records gathered by id
-    const bool by_ids = n_all > kChunk;
-    int n = n_all;
-    if (by_ids) {
-        SegIds seg;
-        seg.ids = nullptr;
-        seg.recs = recs;
-        seg.head = head;
-        n = n_all > kTilePix ? wave_brute_tile_ids(A, tile, s_ids)
-                             : wave_sorted_tile_ids(seg, n_all, s_ids, reinterpret_cast<unsigned *>(s_buf));
-    }
-    sum_fwd_sparse<kModeSparse, false>(A, tile, make_int2(0, n_all), n, s_buf, init, by_ids, s_ids,
-                                       (by_ids || n_all == 0) ? nullptr : recs, head, rc.g, rc.c,
-                                       rc.x, kChunk);
-}
-
-template <bool kBatch>
-__global__ __launch_bounds__(64, 3) void composite_pipe_kernel(SumFwdArgs A) {
-    __shared__ float4 s_buf[kSlice];
-    __shared__ int s_ids[kTilePix];
-    const int total = kBatch ? A.ntiles * A.frames : A.ntiles;
-    const int nw = (int)gridDim.x;
-    // this wave's XCD range [first, end) and its stride wx (waves on the XCD)
-    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-    const int q = total >> 3, r = total & 7;
-    const int first = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-    const int end = first + q + (xcd < r ? 1 : 0);
-    const int wx = (nw >> 3) + (xcd < (nw & 7) ? 1 : 0);
-    int g = first + j;
-    if (g >= end) return;
-    // prologue: the first two tiles' counts, then the first tile's records
-    const int2 c0 = pipe_load_count(A, g);
-    int2 c1 = make_int2(0, 1);
-    if (g + wx < end) c1 = pipe_load_count(A, g + wx);
-    int n = __builtin_amdgcn_readfirstlane(c0.x), m = __builtin_amdgcn_readfirstlane(c0.y);
-    PipeRec rc = pipe_load_recs(A, g, n);
-    for (; g < end; g += wx) {
-        const int g1 = g + wx, g2 = g + 2 * wx;
-        const int n1 = __builtin_amdgcn_readfirstlane(c1.x), m1 = __builtin_amdgcn_readfirstlane(c1.y);
-        // in flight during this tile: the next tile's records, the count after
-        PipeRec rn;
-        rn.g = rn.c = rn.x = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (g1 < end) rn = pipe_load_recs(A, g1, n1);
-        int2 c2 = make_int2(0, 1);
-        if (g2 < end) c2 = pipe_load_count(A, g2);
-        pipe_tile<kBatch>(A, g, n, m, rc, s_buf, s_ids);
-        rc = rn;
-        n = n1;
-        m = m1;
-        c1 = c2;
-    }
-}
-
-// Waves of the pipelined composite: wps per SIMD of the device's CUs
-// (A/B knob 20 = w sets wps = w; default 2), at most one per tile.
-static int pipe_waves(int total_tiles) {
-    static int cus[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-    if (cus[dev] <= 0) {
-        int v = 0;
-        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
-            v = 256;
-        cus[dev] = v;
-    }
-    const int wps = knob(20) >= 1 && knob(20) <= 3 ? knob(20) : 2;
-    const long long w = (long long)cus[dev] * 4 * wps;
-    return (int)(w < total_tiles ? w : total_tiles);
-}
-
 __device__ __forceinline__ int ceil_log2(int n) { return n <= 1 ? 0 : 32 - __clz(n - 1); }
 
 // det_off (deterministic backward, det.h): each (splat, tile) sum goes to
@@ -1115,14 +958,9 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
     const int tslot = timing_begin(s, tev);
     const dim3 grid(ntiles * A.frames);
     if (mode == kModeSparse) {
-        if (A.slab && !A.final_idx && A.layout == kLayoutCHWClamped && knob(23) != 1 &&
-            knob(17) != 1)  // the frame path: persistent pipelined (A/B knob 23 = 1: one round)
-            launch_fwd(A.frames > 1 ? composite_pipe_kernel<true> : composite_pipe_kernel<false>,
-                       dim3(pipe_waves(ntiles * A.frames)), dim3(64), s, tev, A);
-        else
-            launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeSparse, true>
-                                   : raster_sum_fwd_kernel<kModeSparse, false>,
-                       grid, dim3(64), s, tev, A);
+        launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeSparse, true>
+                               : raster_sum_fwd_kernel<kModeSparse, false>,
+                   grid, dim3(64), s, tev, A);
     } else if (mode == kModeBanded) {
         launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeBanded, true>
                                : raster_sum_fwd_kernel<kModeBanded, false>,

@@ -147,9 +147,9 @@ def _kframe_worker(rank, world, port, q):
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
     sys.path.insert(0, REPO)
+    import gsvc_amd.video as V
+    real = V.FrameTrainer
     try:
-        import gsvc_amd.video as V
-
         class ProbeStub:
             def __init__(self, image, frame_num, loss_type, num_points, max_num_points, iterations,
                          lr, densification_interval=100, trained_model=None, isdensity=False,
@@ -168,6 +168,7 @@ def _kframe_worker(rank, world, port, q):
         ks = V.detect_k_frames(lambda i: torch.zeros(1, 3, 4, 4), 20, rank, world, "L2", 1e-3, seed=3)
         q.put((rank, ks))
     finally:
+        V.FrameTrainer = real  # (called in-process too: leave the module as it was)
         if world > 1:
             dist.destroy_process_group()
 
