@@ -52,6 +52,12 @@ _SIGS = {
     "gsvc_prune_lowest": [_I, _I, _P, _I, _P, _P, _P, _P, _SZ, _P],
     "gsvc_project_gaussians_2d_forward": [_I, _P, _P, _U, _U, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P],
     "gsvc_project_gaussians_2d_backward": [_I, _P, _P, _U, _U, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "gsvc_project_gaussians_2d_backward_strided": [_I, _P, _U, _U, _P, _P, _P, _I, _P, _I, _P, _P,
+                                                   _P, _P],
+    "gsvc_rasterize_sum_slabs_workspace_bytes": [_I],
+    "gsvc_rasterize_sum_forward_slabs": [_I, _P, _P, _P, _P, _P, _P, _U, _U, _I, _I, _P, _SZ, _P,
+                                         _P, _P, _P, _P, _P, _P],
+    "gsvc_rasterize_sum_backward_zeroed": [_U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "gsvc_compute_cov2d_bounds": [_I, _P, _P, _P, _P],
     "gsvc_cumsum_workspace_bytes": [_I],
     "gsvc_compute_cumulative_intersects": [_I, _P, _P, _P, _P, _P, _SZ, _P],
@@ -117,6 +123,7 @@ _RESTYPE = {
     "gsvc_bin_tiles_workspace_bytes": _SZ,
     "gsvc_bin_tiles_counted_workspace_bytes": _SZ,
     "gsvc_render_frame_workspace_bytes": _SZ,
+    "gsvc_rasterize_sum_slabs_workspace_bytes": _SZ,
     "gsvc_render_frame_zeroed_bytes": _SZ,
     "gsvc_train_step_workspace_bytes": _SZ,
     "gsvc_train_step_det_workspace_bytes": _SZ,

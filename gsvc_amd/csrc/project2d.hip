@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void project2d_fwd_kernel(
 __global__ __launch_bounds__(256) void project2d_bwd_kernel(
     int n, const float *__restrict__ L, float hw, float hh,
     const int *__restrict__ radii, const float *__restrict__ conics,
-    const float2 *__restrict__ v_xy, const float *__restrict__ v_conic,
+    const float *__restrict__ v_xy, int sxy, const float *__restrict__ v_conic, int sc,
     float *__restrict__ v_cov2d, float2 *__restrict__ v_mean2d, float *__restrict__ v_L) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -46,7 +46,8 @@ __global__ __launch_bounds__(256) void project2d_bwd_kernel(
     float2 vm = make_float2(0.0f, 0.0f);
     if (radii[i] > 0) {
         const float X00 = conics[3 * i], X01 = conics[3 * i + 1], X10 = X01, X11 = conics[3 * i + 2];
-        const float G00 = v_conic[3 * i], G01 = v_conic[3 * i + 1], G10 = G01, G11 = v_conic[3 * i + 2];
+        const float *vc = v_conic + (size_t)sc * i;  // row i (row stride sc floats)
+        const float G00 = vc[0], G01 = vc[1], G10 = G01, G11 = vc[2];
         const float N00 = -X00, N01 = -X01, N10 = -X10, N11 = -X11;
         const float P00 = N00 * G00 + N10 * G01;
         const float P01 = N01 * G00 + N11 * G01;
@@ -63,8 +64,8 @@ __global__ __launch_bounds__(256) void project2d_bwd_kernel(
         vl0 = 2.0f * l11 * g11 + 2.0f * g12 * l21;  // doubled cross term: backward2d.cu:39
         vl1 = 2.0f * l11 * g12 + 2.0f * l21 * g22;
         vl2 = 2.0f * l22 * g22;
-        const float2 vx = v_xy[i];
-        vm = make_float2(vx.x * hw, vx.y * hh);
+        const float *vx = v_xy + (size_t)sxy * i;
+        vm = make_float2(vx[0] * hw, vx[1] * hh);
     }
     v_cov2d[3 * i] = g11;
     v_cov2d[3 * i + 1] = g12;
@@ -111,6 +112,22 @@ extern "C" int gsvc_project_gaussians_2d_forward(
     return check_launch("project_gaussians_2d_forward");
 }
 
+extern "C" int gsvc_project_gaussians_2d_backward_strided(
+    int num_points, const float *L_elements, unsigned img_height, unsigned img_width,
+    const int *radii, const float *conics, const float *v_xy, int v_xy_stride,
+    const float *v_conic, int v_conic_stride, float *v_cov2d, float *v_mean2d,
+    float *v_L_elements, void *stream) {
+    if (num_points < 0 || v_xy_stride < 2 || v_conic_stride < 3)
+        return set_error(GSVC_ERR_ARG, "project_gaussians_2d_backward: bad size or stride");
+    if (num_points == 0) return GSVC_OK;
+    const float hw = 0.5f * (float)img_width, hh = 0.5f * (float)img_height;
+    hipLaunchKernelGGL(project2d_bwd_kernel, dim3(ceil_div(num_points, 256)), dim3(256), 0,
+                       (hipStream_t)stream, num_points, L_elements, hw, hh, radii, conics, v_xy,
+                       v_xy_stride, v_conic, v_conic_stride, v_cov2d, (float2 *)v_mean2d,
+                       v_L_elements);
+    return check_launch("project_gaussians_2d_backward");
+}
+
 extern "C" int gsvc_project_gaussians_2d_backward(
     int num_points, const float *means2d, const float *L_elements, unsigned img_height,
     unsigned img_width, const int *radii, const float *conics, const float *v_xy,
@@ -118,13 +135,9 @@ extern "C" int gsvc_project_gaussians_2d_backward(
     float *v_L_elements, void *stream) {
     (void)means2d;
     (void)v_depth;
-    if (num_points < 0) return set_error(GSVC_ERR_ARG, "project_gaussians_2d_backward: bad size");
-    if (num_points == 0) return GSVC_OK;
-    const float hw = 0.5f * (float)img_width, hh = 0.5f * (float)img_height;
-    hipLaunchKernelGGL(project2d_bwd_kernel, dim3(ceil_div(num_points, 256)), dim3(256), 0,
-                       (hipStream_t)stream, num_points, L_elements, hw, hh, radii, conics,
-                       (const float2 *)v_xy, v_conic, v_cov2d, (float2 *)v_mean2d, v_L_elements);
-    return check_launch("project_gaussians_2d_backward");
+    return gsvc_project_gaussians_2d_backward_strided(num_points, L_elements, img_height,
+                                                      img_width, radii, conics, v_xy, 2, v_conic,
+                                                      3, v_cov2d, v_mean2d, v_L_elements, stream);
 }
 
 extern "C" int gsvc_compute_cov2d_bounds(int num_pts, const float *covs2d, float *conics,

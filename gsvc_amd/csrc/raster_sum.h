@@ -55,6 +55,16 @@ struct SumFwdArgs {
     int *final_idx;
     float *final_Ts;
     long long *stamps;  // kModeStamp only
+    // op path with unsorted id slabs (gsvc_rasterize_sum_forward_slabs): tile
+    // t's ids at ids_rw[t * 256 + j], j < min(count, 256), its count in
+    // id_counts[t]; the kernel sorts them (more than 256: the first 256 rebuilt
+    // from cull_xys / cull_radii), writes them back in order and the tile's
+    // bins row [t * 256, t * 256 + n) for the backward, and zeroes
+    // id_counts_clear[t] (the next call's counts)
+    const unsigned *id_counts;
+    unsigned *id_counts_clear;
+    int *ids_rw;
+    int2 *bins_out;
 };
 
 // sum_fwd_args_init zeroes every field (rec, stamps, m_dev NULL; HWC layout);

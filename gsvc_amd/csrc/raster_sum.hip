@@ -43,6 +43,7 @@
 #include "cull.h"
 #include "det.h"
 #include "frame.h"
+#include "frame_dev.h"
 #include "raster_sum.h"
 #include "tile_ids.h"
 
@@ -638,6 +639,15 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
             store_pixel(A, (size_t)pi * (size_t)A.img_w + (size_t)(pj + q), rr[q], gg[q], bb[q], ll[q]);
 }
 
+// Op path with id slabs: the tile's sorted ids back in place (the backward's
+// gaussian_ids_sorted) and its bins row [begin, begin + n).
+__device__ __forceinline__ void write_sorted_ids(const SumFwdArgs &A, int tile, int begin, int n,
+                                                 const int *s_ids) {
+    const int lane = threadIdx.x & 63;
+    for (int j = lane; j < n; j += 64) A.ids_rw[(size_t)tile * kTilePix + j] = s_ids[j];
+    if (lane == 0) A.bins_out[tile] = make_int2(begin, begin + n);
+}
+
 // kModeSparse launches 64-thread workgroups (one wave per tile); every other
 // mode 128-thread workgroups (two waves per tile).
 // kIdx: final_idx is written (the autograd forward); the render paths launch
@@ -698,6 +708,21 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         seg.recs = recs;
         seg.head = slab_rec(A.slab, A.ntiles, tile, 0);
         if (n_all <= kChunk) seg_rec = recs;  // slots past the head, at their index
+    } else if (kIdx && A.id_counts) {
+        // op path, unsorted id slabs (its autograd forward: kIdx instances
+        // only): this call's count (M from the insertion)
+        n_all = (int)__builtin_amdgcn_readfirstlane(A.id_counts[tile]);
+        if (threadIdx.x == 0) {
+            A.id_counts_clear[tile] = 0u;  // the next call's counts
+            if (tile == 0) {
+                A.meta_out[0] = *A.m_dev;
+                A.meta_out[1] = 0;
+            }
+        }
+        range = make_int2(tile * kTilePix, tile * kTilePix + (n_all < kTilePix ? n_all : kTilePix));
+        seg.ids = A.ids_rw + (size_t)tile * kTilePix;
+        seg.recs = nullptr;
+        seg.head = nullptr;
     } else {
         range = A.bins[tile];
         n_all = range.y - range.x;
@@ -722,17 +747,19 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
     if (sparse) {
         if (w != 0) return;
         if (by_ids)
-            n = (A.slab && n_all > kTilePix)
+            n = ((A.slab || (kIdx && A.id_counts)) && n_all > kTilePix)
                     ? wave_brute_tile_ids(A, tile, s_ids[0])
                     : wave_sorted_tile_ids(seg, n_all, s_ids[0], reinterpret_cast<unsigned *>(s_buf[0]));
+        if (kIdx && A.id_counts) write_sorted_ids(A, tile, range.x, n, s_ids[0]);
         sum_fwd_sparse<kMode, kIdx>(A, tile, range, n, s_buf[0], init, by_ids, s_ids[0], seg_rec,
                                     seg.head, spec0, spec1, spec2, A.spec_slots);
     } else {
         if (ty * kTile + w * 8 >= A.img_h) return;  // band below the image
         if (by_ids)
-            n = (A.slab && n_all > kTilePix)
+            n = ((A.slab || (kIdx && A.id_counts)) && n_all > kTilePix)
                     ? wave_brute_tile_ids(A, tile, s_ids[w])
                     : wave_sorted_tile_ids(seg, n_all, s_ids[w], reinterpret_cast<unsigned *>(s_buf[w]));
+        if (kIdx && A.id_counts && w == 0) write_sorted_ids(A, tile, range.x, n, s_ids[0]);
         sum_fwd_band<kMode, kIdx>(A, tile, w, range, n, s_buf[w], init, by_ids, s_ids[w], seg_rec,
                                   seg.head, spec0, spec1, spec2);
     }
@@ -916,6 +943,40 @@ static int check_tiles(const char *what, int bx, int by, int tbx, int tby, unsig
     return GSVC_OK;
 }
 
+// Op path binning in one kernel (gsvc_rasterize_sum_forward_slabs): every
+// visible splat appends its id to the 256-slot id slab of each tile of its
+// bbox (slot = device atomic count, paired for adjacent tiles; ids past 256
+// dropped, the composite rebuilds such a tile), the block's hit total goes
+// into this call's M, and -- optionally -- the splat's gradient record is
+// zeroed for the backward's atomics.  Replaces utils.py:99-167's cumsum,
+// map, sort and bin edges (and this library's count / scan / fill /
+// segment-sort kernels): the composite sorts each tile's <= 256 ids in LDS.
+__global__ __launch_bounds__(kProjThreads) void tile_insert_ids_kernel(
+    int n, const float2 *__restrict__ xys, const int *__restrict__ radii, int tbx, int tby,
+    unsigned *__restrict__ counts, int *__restrict__ ids, int *__restrict__ m_acc,
+    int *__restrict__ m_clear, float4 *__restrict__ rec_zero) {
+    __shared__ int s_hits[kProjThreads / 64];
+    const int i = blockIdx.x * kProjThreads + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *m_clear = 0;  // the next call's M
+    int hits = 0;
+    if (i < n) {
+        if (rec_zero) {
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rec_zero[4 * (size_t)i + q] = z;
+        }
+        const int r = radii[i];
+        if (r > 0) {
+            const float2 c = xys[i];
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            hits = slab_insert_pairs<8>(c.x, c.y, r, tbx, tby, z, z,
+                                        make_float4(0.f, __int_as_float(i), 0.f, 0.f), counts,
+                                        nullptr, 0, ids);
+        }
+    }
+    add_hits(hits, s_hits, m_acc);
+}
+
 void sum_fwd_args_init(SumFwdArgs &A) {
     A = SumFwdArgs{};
     A.sparse_max = knob(3) > 0 ? knob(3) : 8;
@@ -1058,6 +1119,81 @@ extern "C" int gsvc_rasterize_sum_forward(int tbx, int tby, int tbz, int block_x
                                          img_height, img_depth, gaussian_ids_sorted, tile_bins, xys,
                                          conics, colors, opacities, background, nullptr, 0, kLayoutHWC,
                                          out_img, final_Ts, final_idx, stream);
+}
+
+extern "C" size_t gsvc_rasterize_sum_slabs_workspace_bytes(int num_tiles) {
+    // counts [2][T] and the M slots [2]: two parities, used on alternate calls
+    return sizeof(unsigned) * (2 * (size_t)(num_tiles > 0 ? num_tiles : 0) + 2);
+}
+
+extern "C" int gsvc_rasterize_sum_forward_slabs(
+    int num_points, const float *xys, const int *radii, const float *conics, const float *colors,
+    const float *opacities, const float *background, unsigned img_height, unsigned img_width,
+    int call_index, int density_hint, void *workspace, size_t workspace_bytes,
+    int *gaussian_ids, int *tile_bins, int *meta, float *grad_records_zero, float *out_img,
+    int *final_idx, void *stream) {
+    if (num_points < 0 || img_height == 0 || img_width == 0)
+        return set_error(GSVC_ERR_ARG, "rasterize_sum_forward_slabs: bad sizes");
+    const int tbx = ceil_div((int)img_width, kTile), tby = ceil_div((int)img_height, kTile);
+    const int ntiles = tbx * tby;
+    if (!workspace || workspace_bytes < gsvc_rasterize_sum_slabs_workspace_bytes(ntiles))
+        return set_error(GSVC_ERR_WORKSPACE, "rasterize_sum_forward_slabs: workspace too small");
+    if (!gaussian_ids || !tile_bins || !meta || !out_img || !final_idx || !background ||
+        (num_points > 0 && (!xys || !radii || !conics || !colors || !opacities)))
+        return set_error(GSVC_ERR_ARG, "rasterize_sum_forward_slabs: missing input");
+    hipStream_t s = (hipStream_t)stream;
+    const int par = call_index & 1;
+    unsigned *counts = (unsigned *)workspace;
+    int *m_slots = (int *)(counts + 2 * (size_t)ntiles);
+    if (num_points > 0) {
+        hipLaunchKernelGGL(tile_insert_ids_kernel, dim3(ceil_div(num_points, kProjThreads)),
+                           dim3(kProjThreads), 0, s, num_points, (const float2 *)xys, radii, tbx,
+                           tby, counts + (size_t)par * ntiles, gaussian_ids, m_slots + par,
+                           m_slots + (par ^ 1), (float4 *)grad_records_zero);
+    } else if (hipMemsetAsync(m_slots, 0, 2 * sizeof(int), s) != hipSuccess) {
+        return set_error(GSVC_ERR_HIP, "rasterize_sum_forward_slabs: memset failed");
+    }
+    SumFwdArgs A;
+    sum_fwd_args_init(A);
+    A.tbx = tbx;
+    A.img_w = (int)img_width;
+    A.img_h = (int)img_height;
+    A.ntiles = ntiles;
+    A.layout = kLayoutHWC;
+    A.m_dev = m_slots + par;
+    A.meta_out = meta;
+    A.bg = background;
+    A.sort_ids = true;
+    A.id_counts = counts + (size_t)par * ntiles;
+    A.id_counts_clear = counts + (size_t)(par ^ 1) * ntiles;
+    A.ids_rw = gaussian_ids;
+    A.bins_out = (int2 *)tile_bins;
+    A.cull_xys = (const float2 *)xys;
+    A.cull_radii = radii;
+    A.num_points = num_points;
+    A.xys = (const float2 *)xys;
+    A.conics = conics;
+    A.colors = colors;
+    A.opac = opacities;
+    A.out = out_img;
+    A.final_idx = final_idx;
+    return sum_forward_launch(A, density_hint, s);
+}
+
+extern "C" int gsvc_rasterize_sum_backward_zeroed(
+    unsigned img_height, unsigned img_width, int num_points, const int *gaussian_ids_sorted,
+    const int *tile_bins, const float *xys, const float *conics, const float *colors,
+    const float *opacities, const int *final_idx, const float *v_output, float *grad_records,
+    void *stream) {
+    const int tbx = ceil_div((int)img_width, kTile), tby = ceil_div((int)img_height, kTile);
+    if (num_points < 0) return set_error(GSVC_ERR_ARG, "rasterize_sum_backward_zeroed: bad num_points");
+    const int ntiles = tbx * tby;
+    if (ntiles == 0 || num_points == 0) return GSVC_OK;
+    hipLaunchKernelGGL(raster_sum_bwd_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, tbx,
+                       (int)img_width, (int)img_height, ntiles, gaussian_ids_sorted,
+                       (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacities,
+                       final_idx, v_output, grad_records, nullptr, nullptr, nullptr, 0ll);
+    return check_launch("rasterize_sum_backward_zeroed");
 }
 
 extern "C" int gsvc_rasterize_sum_backward(unsigned img_height, unsigned img_width, unsigned block_h,

@@ -12,13 +12,15 @@
 // keep the reference's argument checks and route here; the general paths
 // (sorted binning for non-zero depths, the deterministic backward) stay in
 // their Python Functions.  Semantics are those of the Python Functions:
-//   project: saves (means2d, L, radii, conics); radii and num_tiles_hit are
+//   project: saves (L, radii, conics); radii and num_tiles_hit are
 //            not differentiable; backward = the projection VJP (backward2d.cu).
-//   rasterize_sum: the sync-free binning (each tile's first 256 entries in
-//            (tile, splat id) order, M on the device) + the sum composite with
-//            final_idx; the M < 1 background branch in the kernel; backward =
-//            backward.cu:696-862 into one [N, 16] record (the returned
-//            gradients are its views).
+//   rasterize_sum: two kernels (gsvc_rasterize_sum_forward_slabs): id slabs
+//            per tile by device atomics, then the composite sorting each
+//            tile's ids in LDS (its first 256 in (tile, splat id) order, M on
+//            the device, the M < 1 background branch in the kernel) and
+//            writing them back for the backward = backward.cu:696-862 into one
+//            [N, 16] record zeroed by the forward (the returned gradients are
+//            its views, which the projection backward reads in place).
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime_api.h>
@@ -74,30 +76,45 @@ struct LazyCount {
 LazyCount g_counts[64];
 std::mutex g_count_lock;
 
-int density_hint(const Tensor &m_dev, void *stream) {
-    const int d = m_dev.device().index();
+int hint_value(int d) {
     if (d < 0 || d >= 64) return 0;
     std::lock_guard<std::mutex> g(g_count_lock);
     LazyCount &c = g_counts[d];
-    if ((c.calls++ & 15u) != 0) return c.value;
     if (c.pending && hipEventQuery(c.ev) == hipSuccess) {
         c.value = *c.pinned;
         c.pending = false;
     }
-    if (!c.pending) {
-        if (!c.pinned) {
-            if (hipHostMalloc((void **)&c.pinned, sizeof(int), hipHostMallocDefault) != hipSuccess ||
-                hipEventCreateWithFlags(&c.ev, hipEventDisableTiming) != hipSuccess) {
-                c.pinned = nullptr;
-                return c.value;
-            }
-        }
-        if (hipMemcpyAsync(c.pinned, m_dev.data_ptr<int>(), sizeof(int), hipMemcpyDeviceToHost,
-                           (hipStream_t)stream) == hipSuccess &&
-            hipEventRecord(c.ev, (hipStream_t)stream) == hipSuccess)
-            c.pending = true;
-    }
     return c.value;
+}
+
+// After the call that wrote m_dev: every 16th call copies it (no wait).
+void hint_refresh(const Tensor &m_dev, void *stream) {
+    const int d = m_dev.device().index();
+    if (d < 0 || d >= 64) return;
+    std::lock_guard<std::mutex> g(g_count_lock);
+    LazyCount &c = g_counts[d];
+    if ((c.calls++ & 15u) != 0 || c.pending) return;
+    if (!c.pinned) {
+        if (hipHostMalloc((void **)&c.pinned, sizeof(int), hipHostMallocDefault) != hipSuccess ||
+            hipEventCreateWithFlags(&c.ev, hipEventDisableTiming) != hipSuccess) {
+            c.pinned = nullptr;
+            return;
+        }
+    }
+    if (hipMemcpyAsync(c.pinned, m_dev.data_ptr<int>(), sizeof(int), hipMemcpyDeviceToHost,
+                       (hipStream_t)stream) == hipSuccess &&
+        hipEventRecord(c.ev, (hipStream_t)stream) == hipSuccess)
+        c.pending = true;
+}
+
+// A [N, C] float gradient as (pointer, row stride in floats): rows may be
+// strided views of the rasterizer backward's [N, 16] records (no copy).
+const float *rows(Tensor &g, int64_t cols, int &stride, const char *name) {
+    if (!(g.dim() == 2 && g.size(1) == cols && g.stride(1) == 1 && g.stride(0) >= cols &&
+          g.is_cuda() && g.scalar_type() == at::kFloat))
+        g = dev_f32(g, name);
+    stride = (int)g.stride(0);
+    return g.data_ptr<float>();
 }
 
 // project_gaussians_2d.py:59-141 (bindings.cu:781-839, 902-949).
@@ -116,7 +133,7 @@ struct ProjectFn : public torch::autograd::Function<ProjectFn> {
                                                 fp(depths), ip(radii), fp(conics), ip(nth),
                                                 stream_of(means2d)),
               "gsvc_project_gaussians_2d_forward");
-        ctx->save_for_backward({means2d, L, radii, conics});
+        ctx->save_for_backward({L, radii, conics});
         ctx->saved_data["H"] = H;
         ctx->saved_data["W"] = W;
         ctx->mark_non_differentiable({radii, nth});
@@ -125,30 +142,63 @@ struct ProjectFn : public torch::autograd::Function<ProjectFn> {
 
     static variable_list backward(AutogradContext *ctx, variable_list g) {
         const auto s = ctx->get_saved_variables();
-        const Tensor &means2d = s[0], &L = s[1], &radii = s[2], &conics = s[3];
-        const int64_t n = means2d.size(-2);
+        const Tensor &L = s[0], &radii = s[1], &conics = s[2];
+        const int64_t n = L.size(0);
         const auto f = L.options();
-        Tensor v_xy = g[0].defined() ? dev_f32(g[0], "v_xy") : at::zeros({n, 2}, f);
-        Tensor v_conic = g[3].defined() ? dev_f32(g[3], "v_conic") : at::zeros({n, 3}, f);
+        Tensor v_xy = g[0].defined() ? g[0] : at::zeros({n, 2}, f);
+        Tensor v_conic = g[3].defined() ? g[3] : at::zeros({n, 3}, f);
+        int sxy = 2, sc = 3;
+        const float *pxy = rows(v_xy, 2, sxy, "v_xy");
+        const float *pc = rows(v_conic, 3, sc, "v_conic");
         Tensor v_cov2d = at::empty({n, 3}, f), v_mean = at::empty({n, 2}, f), v_L = at::empty({n, 3}, f);
-        check(gsvc_project_gaussians_2d_backward(
-                  (int)n, fp(means2d), fp(L), (unsigned)ctx->saved_data["H"].toInt(),
-                  (unsigned)ctx->saved_data["W"].toInt(), ip(radii), fp(conics), fp(v_xy), nullptr,
-                  fp(v_conic), fp(v_cov2d), fp(v_mean), fp(v_L), stream_of(L)),
-              "gsvc_project_gaussians_2d_backward");
+        check(gsvc_project_gaussians_2d_backward_strided(
+                  (int)n, fp(L), (unsigned)ctx->saved_data["H"].toInt(),
+                  (unsigned)ctx->saved_data["W"].toInt(), ip(radii), fp(conics), pxy, sxy, pc, sc,
+                  fp(v_cov2d), fp(v_mean), fp(v_L), stream_of(L)),
+              "gsvc_project_gaussians_2d_backward_strided");
         return {v_mean, v_L, Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
     }
 };
 
 constexpr int kTileKeep = 256;  // entries per tile the sum rasterizer blends (config.h BLOCK_SIZE)
 
-// rasterize_sum.py:89-254 on the sync-free binning (utils.bin_for_raster's
-// counted path; the caller checked that it applies).  Returns (out_img [H,W,3],
-// M [1] on the device).
+// The id-slab counters of gsvc_rasterize_sum_forward_slabs, per device and
+// stream (zeroed once; each call leaves them ready for the next).
+struct SlabWs {
+    Tensor buf;
+    int tiles = -1;
+    int calls = 0;
+};
+std::mutex g_ws_lock;
+std::vector<std::pair<std::pair<int, void *>, SlabWs>> g_ws;
+
+SlabWs &slab_ws(const Tensor &like, void *stream, int ntiles) {
+    std::lock_guard<std::mutex> g(g_ws_lock);
+    const std::pair<int, void *> key(like.device().index(), stream);
+    SlabWs *w = nullptr;
+    for (auto &kv : g_ws)
+        if (kv.first == key) w = &kv.second;
+    if (!w) {
+        g_ws.emplace_back(key, SlabWs());
+        w = &g_ws.back().second;
+    }
+    if (w->tiles != ntiles) {
+        const size_t bytes = gsvc_rasterize_sum_slabs_workspace_bytes(ntiles);
+        w->buf = at::zeros({(int64_t)((bytes + 3) / 4)}, like.options().dtype(at::kInt));
+        w->tiles = ntiles;
+        w->calls = 0;
+    }
+    return *w;
+}
+
+// rasterize_sum.py:89-254 with the binning of gsvc_rasterize_sum_forward_slabs
+// (two kernels, no host sync; the caller checked that the depths are zero).
+// Returns (out_img [H,W,3], M [1] on the device).  need_grad: the gradient
+// records are allocated (and zeroed by the forward) for the backward.
 struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
     static variable_list forward(AutogradContext *ctx, Tensor xys, Tensor radii, Tensor conics,
                                  Tensor colors, Tensor opacity, Tensor background, int64_t H,
-                                 int64_t W) {
+                                 int64_t W, bool need_grad) {
         xys = dev_f32(xys, "xys");
         radii = dev_i32(radii, "radii");
         conics = dev_f32(conics, "conics");
@@ -156,29 +206,27 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
         opacity = dev_f32(opacity, "opacities");
         background = dev_f32(background, "background");
         TORCH_CHECK(colors.dim() == 2 && colors.size(1) == 3, "colors must have shape (N, 3)");
+        TORCH_CHECK(xys.dim() == 2 && xys.size(1) == 2, "xys must have dimensions (num_points, 2)");
         const int64_t n = xys.size(0);
         const int tbx = (int)((W + 15) / 16), tby = (int)((H + 15) / 16), nt = tbx * tby;
-        const long long cap = (long long)std::min<int64_t>(n, kTileKeep) * nt;
         const auto f = xys.options();
         const auto i = f.dtype(at::kInt);
         void *st = stream_of(xys);
-        Tensor scratch = at::empty({cap}, i), gids = at::empty({cap}, i);
-        Tensor bins = at::empty({nt, 2}, i), meta = at::empty({2}, i);
-        const size_t wsb = gsvc_bin_tiles_counted_workspace_bytes(nt);
-        Tensor ws = at::empty({(int64_t)(wsb / 4 + 1)}, i);
-        check(gsvc_bin_tiles_counted((int)n, fp(xys), ip(radii), tbx, tby, cap,
-                                     n > kTileKeep ? kTileKeep : 0, ip(scratch), ip(gids), ip(bins),
-                                     ip(meta), ws.data_ptr(), 4 * (size_t)ws.numel(), st),
-              "gsvc_bin_tiles_counted");
-        const int hint = density_hint(meta, st);
-        Tensor out = at::empty({H, W, 3}, f), idx = at::empty({H, W}, i);
-        check(gsvc_rasterize_sum_forward_ex(tbx, tby, 1, 16, 16, 1, (unsigned)W, (unsigned)H, 1,
-                                            ip(gids), ip(bins), fp(xys), fp(conics), fp(colors),
-                                            fp(opacity), fp(background), ip(meta), hint, 0,
-                                            fp(out), nullptr, ip(idx), st),
-              "gsvc_rasterize_sum_forward_ex");
+        SlabWs &ws = slab_ws(xys, st, nt);
+        Tensor gids = at::empty({(int64_t)nt * kTileKeep}, i), bins = at::empty({nt, 2}, i);
+        Tensor meta = at::empty({2}, i), out = at::empty({H, W, 3}, f), idx = at::empty({H, W}, i);
+        Tensor rec = need_grad ? at::empty({n, 16}, f) : Tensor();
+        const int hint = hint_value(xys.device().index());  // M of an earlier call
+        check(gsvc_rasterize_sum_forward_slabs(
+                  (int)n, fp(xys), ip(radii), fp(conics), fp(colors), fp(opacity), fp(background),
+                  (unsigned)H, (unsigned)W, ws.calls++, hint, ws.buf.data_ptr(),
+                  4 * (size_t)ws.buf.numel(), ip(gids), ip(bins), ip(meta), fp(rec), fp(out),
+                  ip(idx), st),
+              "gsvc_rasterize_sum_forward_slabs");
+        hint_refresh(meta, st);
         Tensor m_dev = meta.narrow(0, 0, 1);
-        ctx->save_for_backward({gids, bins, xys, conics, colors, opacity, background, idx});
+        ctx->save_for_backward({gids, bins, xys, conics, colors, opacity, idx});
+        ctx->saved_data["rec"] = rec;  // zeroed: the first backward adds into it
         ctx->saved_data["H"] = H;
         ctx->saved_data["W"] = W;
         ctx->mark_non_differentiable({m_dev});
@@ -188,20 +236,25 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
     static variable_list backward(AutogradContext *ctx, variable_list g) {
         const auto s = ctx->get_saved_variables();
         const Tensor &gids = s[0], &bins = s[1], &xys = s[2], &conics = s[3], &colors = s[4];
-        const Tensor &opacity = s[5], &background = s[6], &idx = s[7];
+        const Tensor &opacity = s[5], &idx = s[6];
         const int64_t H = ctx->saved_data["H"].toInt(), W = ctx->saved_data["W"].toInt();
         const int64_t n = xys.size(0);
         Tensor v_out = g[0].defined() ? dev_f32(g[0], "v_output") : at::zeros({H, W, 3}, xys.options());
-        Tensor rec = at::empty({n, 16}, xys.options());
-        check(gsvc_rasterize_sum_backward((unsigned)H, (unsigned)W, 16, 16, (int)n, ip(gids),
-                                          ip(bins), fp(xys), fp(conics), fp(colors), fp(opacity),
-                                          fp(background), nullptr, ip(idx), fp(v_out), nullptr,
-                                          fp(rec), stream_of(xys)),
-              "gsvc_rasterize_sum_backward");
+        Tensor rec = ctx->saved_data["rec"].toTensor();
+        if (rec.defined()) {
+            ctx->saved_data["rec"] = Tensor();  // a second backward (retain_graph) zeroes its own
+        } else {
+            rec = at::zeros({n, 16}, xys.options());
+        }
+        check(gsvc_rasterize_sum_backward_zeroed((unsigned)H, (unsigned)W, (int)n, ip(gids),
+                                                 ip(bins), fp(xys), fp(conics), fp(colors),
+                                                 fp(opacity), ip(idx), fp(v_out), fp(rec),
+                                                 stream_of(xys)),
+              "gsvc_rasterize_sum_backward_zeroed");
         Tensor v_opac = rec.narrow(1, 8, 1);
         if (opacity.dim() != 2) v_opac = v_opac.reshape(opacity.sizes());
         return {rec.narrow(1, 0, 2), Tensor(), rec.narrow(1, 2, 3), rec.narrow(1, 5, 3), v_opac,
-                Tensor(), Tensor(), Tensor()};
+                Tensor(), Tensor(), Tensor(), Tensor()};
     }
 };
 
@@ -212,7 +265,10 @@ std::vector<Tensor> project_gaussians_2d(Tensor means2d, Tensor L, int64_t H, in
 
 std::vector<Tensor> rasterize_sum(Tensor xys, Tensor radii, Tensor conics, Tensor colors,
                                   Tensor opacity, Tensor background, int64_t H, int64_t W) {
-    return RasterSumFn::apply(xys, radii, conics, colors, opacity, background, H, W);
+    const bool need_grad = at::GradMode::is_enabled() &&
+                           (xys.requires_grad() || conics.requires_grad() ||
+                            colors.requires_grad() || opacity.requires_grad());
+    return RasterSumFn::apply(xys, radii, conics, colors, opacity, background, H, W, need_grad);
 }
 
 }  // namespace

@@ -143,6 +143,17 @@ int gsvc_project_gaussians_2d_backward(
     float *v_cov2d, float *v_mean2d, float *v_L_elements,
     void *stream);
 
+/* The same backward with row strides for v_xy and v_conic (>= 2 and >= 3
+ * floats): the rasterizer backward's gradient records ([N,16], v_xy at 0,
+ * v_conic at 2) are read in place, without a contiguous copy.  means2d and
+ * v_depth, unused by the reference kernel, are not taken.  Not part of the
+ * reference (the autograd Function of csrc/torch_ops.cpp calls it). */
+int gsvc_project_gaussians_2d_backward_strided(
+    int num_points, const float *L_elements, unsigned img_height, unsigned img_width,
+    const int *radii, const float *conics, const float *v_xy, int v_xy_stride,
+    const float *v_conic, int v_conic_stride, float *v_cov2d, float *v_mean2d,
+    float *v_L_elements, void *stream);
+
 /* Replaces _C.compute_cov2d_bounds (bindings.cu:41-60 -> :21-39).
  * covs2d [N,3] upper-triangular in; conics [N,3], radii [N] float out. */
 int gsvc_compute_cov2d_bounds(int num_pts, const float *covs2d, float *conics,
@@ -261,6 +272,38 @@ int gsvc_rasterize_sum_forward_ex(
     const float *opacities, const float *background,
     const int *num_intersects_dev, int density_hint, int out_layout,
     float *out_img, float *final_Ts, int *final_idx, void *stream);
+
+/* The op path's binning and composite in two kernels, no host sync and no
+ * sort kernels: rasterize_sum.py:110-136's cumsum + map + sort + bin edges
+ * (utils.py:99-167; forward.cu:100-163) and rasterize_forward_sum
+ * (forward.cu:512-627).  Every visible splat appends its id to a 256-slot id
+ * slab of each tile of its bbox (device atomics); the composite sorts a
+ * tile's ids in LDS -- the first <= 256 in (tile, splat id) order, as the
+ * reference's stable sort of (tile << 32 | depth 0) keys gives -- blends them
+ * and writes them back sorted: gaussian_ids [T * 256] (tile t's at t * 256)
+ * and tile_bins [T, 2] = [t * 256, t * 256 + n) are then the inputs of the
+ * backward, final_idx (required) indexes gaussian_ids.  meta[0] <- M (device), meta[1] <-
+ * 0; M < 1 renders the background (rasterize_sum.py:121-127).
+ * grad_records_zero (optional, [N, 16]) is zeroed for
+ * gsvc_rasterize_sum_backward_zeroed.  workspace: the first
+ * gsvc_rasterize_sum_slabs_workspace_bytes(T) bytes must be zero before the
+ * first call with it; each call (call_index = a counter, alternate parities)
+ * leaves them ready for the next.  Requires every splat's depth to be 0
+ * (project_gaussians_2d's output).  Not part of the reference. */
+size_t gsvc_rasterize_sum_slabs_workspace_bytes(int num_tiles);
+int gsvc_rasterize_sum_forward_slabs(
+    int num_points, const float *xys, const int *radii, const float *conics,
+    const float *colors, const float *opacities, const float *background,
+    unsigned img_height, unsigned img_width, int call_index, int density_hint,
+    void *workspace, size_t workspace_bytes, int *gaussian_ids, int *tile_bins,
+    int *meta, float *grad_records_zero, float *out_img, int *final_idx, void *stream);
+/* gsvc_rasterize_sum_backward (backward.cu:696-862) into grad_records that
+ * the caller has zeroed (gsvc_rasterize_sum_forward_slabs did): no memset. */
+int gsvc_rasterize_sum_backward_zeroed(
+    unsigned img_height, unsigned img_width, int num_points,
+    const int *gaussian_ids_sorted, const int *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacities,
+    const int *final_idx, const float *v_output, float *grad_records, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Whole-frame render of GSVC's per-frame model (GaussianSplats_Represent.py:
