@@ -59,7 +59,9 @@ struct TrainTileArgs {
     int diag;         // diagnostic knob 13 (timing experiments only; wrong results):
                       // bits 2 no backward, 4 no forward
                       // blending, 8 no backward pixel work, 16 no run sums, 32 no atomics;
-                      // 64 (A/B, exact): items in entry order, not longest first
+                      // 64 (A/B, exact): items in entry order, not longest first;
+                      // 128 (A/B, exact): the carried candidates ranked by a
+                      // readlane loop instead of LDS broadcast reads
     float *out;       // optional [3, H, W] clamped render
     long long *stamps;  // diagnostic: int64[ntiles][8]
     // GSVC_TRAIN_DETERMINISTIC (band kernel): the (splat, tile) sums go to
@@ -832,7 +834,22 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                 mem = box_has(b, (unsigned)tx, (unsigned)ty);
             }
             const int id = mem ? cid : 0x7fffffff;
-            const int rank = rank_below(id, n);
+            int rank = 0;
+            if (kDiag && (A.diag & 128)) {
+                rank = rank_below(id, n);
+            } else {
+                // rank by id with the ids through LDS (part row 0, free during the
+                // order), four per broadcast read: 2 VALU per candidate instead of
+                // a readlane loop's 3 (lanes past n hold 0x7fffffff, below no id)
+                int *s_rid = reinterpret_cast<int *>(&S.part[0][0]);
+                s_rid[lane] = id;
+                wave_lds_sync();
+                for (int k = 0; k < n; k += 4) {
+                    const int4 q = *reinterpret_cast<const int4 *>(s_rid + k);
+                    rank += (q.x < id ? 1 : 0) + (q.y < id ? 1 : 0) + (q.z < id ? 1 : 0) +
+                            (q.w < id ? 1 : 0);
+                }
+            }
             if (mem) {
                 S.geo[rank] = r0;
                 S.col[rank] = make_float4(r1.x, r1.z, r1.w, r2.x);
