@@ -352,6 +352,11 @@ class GaussianVideoFrame(nn.Module):
         return loss, psnr
 
     def train_iter(self, gt_image, iter):
+        """GaussianSplats_Represent.py:191-207: one training iteration on
+        ``gt_image``; returns (loss, psnr).  The fused step may enqueue work of
+        the NEXT iteration against this target and these parameters: writes to
+        either that bypass torch's version counter (``.data``, DLPack views, a
+        custom kernel) must be followed by ``gsvc_amd.train.bump_param_epoch()``."""
         controls = (((iter == 1 or iter % self.densification_interval == 0) and self.isdensity)
                     or (iter % self.densification_interval == 0 and self.isremoval))
         rgbw_train = None if controls else self._fused_train_params(gt_image)
