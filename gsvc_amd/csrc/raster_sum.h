@@ -19,7 +19,6 @@ struct SumFwdArgs {
     int spec_slots;    // frame path: slab records loaded with the count (<= kHeadSlots)
     int group_min;     // sparse chunks of <= this many entries skip the lane-group lists
     int cut;           // sparse render chunks may take the sigma-threshold blend (knob 19 = 1: never)
-    int pack_blu;      // cut chunks: blue in the colour record's opacity slot (A/B knob 20 = 1: off)
     const int *m_dev;  // device num_intersects (NULL: > 0); 0 -> background
     const float *bg;
     const int *ids;

@@ -289,7 +289,6 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         s_blu[kChunk] = 0.0f;
     }
     const int kGroupMin = A.group_min;
-    const bool pack = !kDiag || A.pack_blu;  // cut chunks stage blue in the opacity slot
     const int ty = tile / A.tbx, tx = tile - ty * A.tbx;
     const int pi = ty * kTile + (lane >> 2);
     const int pj = tx * kTile + ((lane & 3) << 2);
@@ -330,7 +329,7 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         if (!kIdx) cut = A.cut && __ballot(lane < cnt && !entry_cut_ok(geo, col, bx.x)) == 0ull;
         if (lane < cnt) {
             s_geo[rank] = geo;
-            s_col[rank] = (cut && pack) ? make_float4(col.x, bx.x, col.z, col.w) : col;
+            s_col[rank] = col;
             s_blu[rank] = bx.x;
             if (n > kGroupMin)
                 s_gm[rank] = (unsigned short)ellipse_blocks<16>(
@@ -351,7 +350,7 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
             if (!kIdx) cut = A.cut && __ballot(!ok) == 0ull;
             if (lane < cnt) {
                 s_geo[lane] = geo;
-                s_col[lane] = (cut && pack) ? make_float4(col.x, blu, col.z, col.w) : col;
+                s_col[lane] = col;
                 s_blu[lane] = blu;
                 if (cnt > kGroupMin)
                     s_gm[lane] = (unsigned short)ellipse_blocks<16>(
@@ -368,8 +367,7 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
             const float cq = (C.x * dy) * dy;
             const float bdy = G.w * dy;
             if constexpr (decltype(cutc)::value) {
-                // (unit opacity: the record carries blue in its opacity slot)
-                const float bl = pack ? C.y : s_blu[t];
+                const float bl = s_blu[t];
                 blend_pair_cut(G.x, G.z, bdy, cq, C.z, C.w, bl, px01, ar01, ag01, ab01);
                 blend_pair_cut(G.x, G.z, bdy, cq, C.z, C.w, bl, px23, ar23, ag23, ab23);
             } else {
@@ -989,7 +987,6 @@ void sum_fwd_args_init(SumFwdArgs &A) {
     A.spec_slots = knob(10) > 0 && knob(10) < kHeadSlots ? knob(10) : kHeadSlots;
     A.group_min = knob(15) > 0 ? knob(15) - 1 : kGroupMinDefault;
     A.cut = knob(19) != 1;
-    A.pack_blu = knob(20) != 1;
     A.layout = kLayoutHWC;
     A.frames = 1;
 }
