@@ -54,13 +54,17 @@ __device__ __forceinline__ unsigned ellipse_blocks(float x, float y, float a, fl
 // An entry's geometry is small enough that its sigma at any pixel centre of
 // an image up to 2^16 wide is finite: |x|, |y| < 2^20 and |a/2|, |b|, |c/2| <
 // 2^40 bound dx, dy < 2^21 and every product and sum of the sigma
-// evaluation below 2^85, so no inf - inf or 0 * inf -- sigma is never NaN,
-// the one value the sigma-threshold alpha cut (kSigmaCutBits) decides
-// differently from the reference's test.  NaN fails every comparison here.
+// evaluation below 2^85, so no inf - inf or 0 * inf -- sigma is never NaN --
+// and c/2 carries no sign bit (c/2 in [+0, 2^40)), so (c/2 dy) dy is +0 or
+// positive and sigma = fma(q, dx, that) is never -0: NaN and -0 are the two
+// values the sigma-threshold alpha cut (kSigmaCutBits, an unsigned compare of
+// the bits) decides differently from the reference's test (which keeps both).
+// The projection's conics always pass the sign test (c = l11^2 / det, det > 0);
+// an operator caller's conics might not.  NaN fails every comparison here.
 __device__ __forceinline__ bool geo_bounded(float x, float y, float ha, float b, float hc) {
     constexpr float kPos = 1048576.0f, kCon = 1099511627776.0f;  // 2^20, 2^40
     return fabsf(x) < kPos && fabsf(y) < kPos && fabsf(ha) < kCon && fabsf(b) < kCon &&
-           fabsf(hc) < kCon;
+           (__float_as_uint(hc) >> 31) == 0u && hc < kCon;
 }
 
 }  // namespace gsvc

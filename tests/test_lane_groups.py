@@ -115,3 +115,31 @@ def test_composite_sigma_cut_bit_identical(cuda, oracle, case):
         ref = oracle.render_sum(means, L, colors, opac, H, W)["out"]
         ref = np.clip(ref, 0, 1).reshape(H, W, 3).transpose(2, 0, 1)[None]
         np.testing.assert_allclose(outs[0].cpu().numpy(), ref, rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("want_idx", [False, True])
+def test_sigma_cut_keeps_negative_zero_sigma(cuda, oracle, want_idx):
+    """sigma = -0.0 passes the reference's test (!(sigma < 0), alpha = 1,
+    forward.cu:598-606) while its bits fail the unsigned threshold compare of
+    the sigma cut: an operator caller's conic with c = -0.0 and b < 0 gives it
+    one pixel above the centre.  The cut must not take such an entry
+    (cull.h geo_bounded: c/2 without sign bit), on the render instance
+    (want_idx False, the cut) and the autograd one alike."""
+    from gsvc_amd import ops
+    H = W = 16
+    xys = np.array([[8.0, 8.0], [3.0, 12.0]], np.float32)
+    conics = np.array([[0.5, -1.0, -0.0], [0.3, 0.05, 0.4]], np.float32)
+    colors = np.array([[0.25, 0.5, 0.75], [0.1, 0.2, 0.3]], np.float32)
+    opac = np.ones((2, 1), np.float32)
+    gids = np.array([0, 1], np.int32)
+    bins = np.array([[0, 2]], np.int32)
+    tb = (1, 1, 1)
+    out, _ = ops.rasterize_sum_forward_ex(tb, (16, 16, 1), (W, H, 1), T(gids), T(bins), T(xys),
+                                          T(conics), T(colors), T(opac),
+                                          torch.ones(3, device=cuda), want_idx=want_idx)
+    ref, _, _ = oracle.raster_sum_forward(tb, H, W, gids, bins, xys, conics, colors, opac)
+    g = out.cpu().numpy()
+    assert np.all(ref[7, 8] >= colors[0] - 1e-6)  # the sigma = -0 pixel (alpha 1) is in
+    np.testing.assert_array_equal(np.isnan(g), np.isnan(ref))
+    fin = np.isfinite(ref)
+    np.testing.assert_allclose(g[fin], ref[fin], rtol=0, atol=1e-5)
