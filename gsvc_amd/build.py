@@ -34,6 +34,9 @@ VARIANTS = {LIB: ("obj", []), LIB_DIAG: ("obj_diag", ["-DGSVC_DIAG"])}
 # the C++ autograd Functions of the drop-in operators (csrc/torch_ops.cpp),
 # a torch extension module linked against the product library
 TORCH_EXT = os.path.join(LIBDIR, "_torch_ops.so")
+# the CPU dispatch of the two operators (csrc/cpu_ops.cpp): host code only
+CPU_LIB = os.path.join(LIBDIR, "libgsvc_amd_cpu.so")
+CPU_SRC = os.path.join(CSRC, "cpu_ops.cpp")
 TORCH_EXT_SRC = os.path.join(CSRC, "torch_ops.cpp")
 
 
@@ -77,7 +80,26 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if verbose:
             print(lib)
     _build_torch_ext(force, verbose)
+    _build_cpu_lib(force, verbose)
     return LIB
+
+
+def _build_cpu_lib(force: bool, verbose: bool) -> None:
+    """g++ with OpenMP, -ffp-contract=off and no fast math (the kernels' op
+    sequence)."""
+    if not force and os.path.exists(CPU_LIB) and os.path.getmtime(CPU_LIB) >= os.path.getmtime(CPU_SRC):
+        if verbose:
+            print(CPU_LIB)
+        return
+    tmp = CPU_LIB + ".tmp"
+    cmd = ["g++", "-O2", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+           "-fopenmp", "-Wall", CPU_SRC, "-o", tmp]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"CPU library build failed:\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, CPU_LIB)
+    if verbose:
+        print(CPU_LIB)
 
 
 def _build_torch_ext(force: bool, verbose: bool) -> None:

@@ -34,6 +34,10 @@ def project_gaussians_2d(
     Returns (xys [N,2], depths [N] (zeros), radii [N] int32, conics [N,3],
     num_tiles_hit [N] int32).
     """
+    if means2d.device.type == "cpu":  # CPU tensors: the CPU dispatch (gsvc_amd/cpu.py)
+        from . import cpu
+        return cpu.project_gaussians_2d(means2d, L_elements, img_height, img_width, tile_bounds,
+                                        clip_thresh)
     if _lib.product_active():
         tb = tile_bounds
         xys, depths, radii, conics, nth = _lib.torch_ops().project_gaussians_2d(

@@ -1,6 +1,7 @@
 """CPU: the C-ABI library loads, exports every symbol include/gsvc_amd.h
-declares, shares torch's HIP runtime, and the product path refuses CPU tensors
-(there is no CPU fallback)."""
+declares, shares torch's HIP runtime, and the HIP op table refuses CPU tensors
+(no GPU call falls back to the CPU; CPU tensors have their own dispatch,
+tests/test_cpu_path.py)."""
 import ctypes
 import os
 import re
@@ -121,11 +122,13 @@ def test_single_hip_runtime_loaded():
 
 
 def test_product_path_rejects_cpu_tensors():
-    from gsplat.project_gaussians_2d import project_gaussians_2d
+    """The HIP op table (the reference's `_C` ops) takes device tensors only;
+    the two operators dispatch CPU tensors to the CPU library (test_cpu_path)."""
+    from gsvc_amd import ops
     means = torch.zeros(4, 2)
     L = torch.ones(4, 3)
     with pytest.raises(RuntimeError, match="CUDA tensor"):
-        project_gaussians_2d(means, L, 32, 32, (2, 2, 1))
+        ops.project_gaussians_2d_forward(4, means, L, 32, 32, (2, 2, 1), 0.01)
 
 
 def test_dropin_package_surface():
