@@ -4,7 +4,10 @@ sequence over the gsplat drop-in -- at the bench's trained 1080p / 50k state
 (tests/golden/train_state_1080p_n50k.npz) and at a 16x16 / 16-splat frame
 (host cost alone).  Prints wall time per call for forward, forward +
 backward, no-grad render and train_iter, then a cProfile of forward +
-backward.  Run it under ``rocprofv3 --kernel-trace --stats`` for the kernels.
+backward and a torch.profiler table (host time per op and per autograd node,
+so the drop-in's own share -- project / rasterize forward and their backward
+nodes -- reads apart from the caller's ops).  Run it under
+``rocprofv3 --kernel-trace --stats`` for the kernels.
 
     python tools/opprof.py [--calls 200] [--no-profile]
 """
@@ -98,6 +101,13 @@ def main():
     s = io.StringIO()
     pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
     print(s.getvalue()[:5000])
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU]) as prof:
+        for _ in range(a.calls):
+            fb()
+        torch.cuda.synchronize()
+    print(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=30,
+                                    max_name_column_width=60), flush=True)
 
 
 if __name__ == "__main__":
