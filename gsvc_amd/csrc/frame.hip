@@ -173,9 +173,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
 // The slab then holds the same set of entries per tile (the order of slots
 // within a tile is arbitrary either way: the consumers rank by id).
 // ``key`` (optional): each splat's strip key and id, for the next order.
-// kHalf: lanes 32..63 of every wave idle (32 splats per wave, twice the
-// workgroups) -- more waves per SIMD to hide each one's dependency chain.
-template <bool kStamp, bool kHalf = false>
+template <bool kStamp>
 __global__ __launch_bounds__(kProjThreads) void frame_project_ordered_kernel(
     int n, const int *__restrict__ order, const float *__restrict__ xyz, int xyz_tanh,
     const float *__restrict__ chol, const float *__restrict__ chol_bound,
@@ -190,13 +188,11 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_ordered_kernel(
     __shared__ unsigned s_cnt[kAggWin];
     __shared__ int s_box[4][kProjThreads / 64];
     const int tid = threadIdx.x, lane = tid & 63;
-    const int t = kHalf ? blockIdx.x * (kProjThreads / 2) + (tid >> 6) * 32 + lane
-                        : blockIdx.x * blockDim.x + tid;
+    const int t = blockIdx.x * blockDim.x + tid;
     long long *st = kStamp ? stamps + 8 * (size_t)((blockIdx.x * blockDim.x + tid) >> 6) : nullptr;
     if (kStamp && lane == 0) st[0] = proj_stamp();
     if (blockIdx.x == 0 && tid == 0) *m_clear = 0;  // the next frame's slot
-    const bool mine = t < n && (!kHalf || lane < 32);
-    const int i = mine ? (order ? order[t] : t) : n;  // order NULL: identity
+    const int i = t < n ? (order ? order[t] : t) : n;  // order NULL: identity
     const bool have = i < n;
     SplatOut S;
     S.P.rad = 0;
@@ -318,9 +314,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
         }
         hipEvent_t tev[2];
         const int tslot = timing_begin(s, tev, kTimingProject);
-        const bool half = kDiag && knob(23) == 1;  // A/B: 32 splats per wave
-        launch_timed(half ? frame_project_ordered_kernel<false, true> : frame_project_ordered_kernel<false>,
-                     half ? dim3(ceil_div(n, kProjThreads / 2)) : grid, dim3(kProjThreads), 0, s, tev, n,
+        launch_timed(frame_project_ordered_kernel<false>, grid, dim3(kProjThreads), 0, s, tev, n,
                      ord->order, xyz, xyz_tanh, chol, chol_bound, feat, rgb_w, opac, hw, hh, tbx,
                      tby, w.xys, w.radii, w.rec, ord->carry_ids ? ord->carry_counts : f.counts,
                      w.slab, f.m_acc, f.m_clear, grad_zero, ord->key, ord->key_id,

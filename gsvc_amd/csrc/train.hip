@@ -1617,10 +1617,7 @@ __device__ __forceinline__ int splat_step(const TrainSplatArgs &A, int i, long l
     return hits;
 }
 
-// kHalf: lanes 32..63 of every wave idle, 32 splats per wave -- twice the
-// waves (two per SIMD, or a wave on the otherwise idle CUs) for the same
-// splats, so one wave's dependency stalls hide behind another's.
-template <bool kStamp, int kBlock = 256, bool kHalf = false>
+template <bool kStamp, int kBlock = 256>
 __global__ __launch_bounds__(kBlock) void train_splat_kernel(TrainSplatArgs A) {
     long long *st = kStamp ? A.stamps + 8 * (size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6))
                            : nullptr;
@@ -1633,10 +1630,8 @@ __global__ __launch_bounds__(kBlock) void train_splat_kernel(TrainSplatArgs A) {
         if (kStamp) splat_stamp(st, 5);
         return;
     }
-    const int lane = threadIdx.x & 63;
-    const int t = kHalf ? (blockIdx.x - 1) * (kBlock / 2) + (threadIdx.x >> 6) * 32 + lane
-                        : (blockIdx.x - 1) * blockDim.x + threadIdx.x;
-    const int hits = (t < A.n && (!kHalf || lane < 32)) ? splat_step<kStamp>(A, t, st) : 0;
+    const int t = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
+    const int hits = t < A.n ? splat_step<kStamp>(A, t, st) : 0;
     if (A.carry == 2) {
         // the next frame's M is read only as M >= 1 (the tile kernel's background
         // branch, rasterize_sum.py:121-127): one plain store of 1 per wave that
@@ -1970,7 +1965,6 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
                        ? knob(21)
                        : 256;
     const int blocks = (num_points > 0 ? ceil_div(num_points, sb) : 0) + 1;
-    const int blocks_half = (num_points > 0 ? ceil_div(num_points, 128) : 0) + 1;
     hipEvent_t tev[2];
     const int tslot = timing_begin(s, tev, kTimingTrainSplat);
     bool launched = false;
@@ -1987,8 +1981,6 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
             launch_timed(train_splat_kernel<false, 192>, dim3(blocks), dim3(192), 0, s, tev, P);
         } else if (sb == 512) {
             launch_timed(train_splat_kernel<false, 512>, dim3(blocks), dim3(512), 0, s, tev, P);
-        } else if (knob(21) == 1000) {  // A/B: 32 splats per wave
-            launch_timed(train_splat_kernel<false, 256, true>, dim3(blocks_half), dim3(256), 0, s, tev, P);
         } else {
             launched = false;
         }
