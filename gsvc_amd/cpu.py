@@ -85,6 +85,7 @@ class ProjectGaussians2dCPU(Function):
         ctx.img_height, ctx.img_width = int(img_height), int(img_width)
         ctx.save_for_backward(L_elements, radii, conics)
         ctx.mark_non_differentiable(radii, nth)
+        ctx.set_materialize_grads(False)  # depths' gradient: None, not zeros
         return xys, depths, radii, conics, nth
 
     @staticmethod

@@ -134,6 +134,9 @@ struct ProjectFn : public torch::autograd::Function<ProjectFn> {
                                                 stream_of(means2d)),
               "gsvc_project_gaussians_2d_forward");
         ctx->save_for_backward({L, radii, conics});
+        // no zero-filled gradients for depths / radii / num_tiles_hit (three
+        // fill launches per backward): an undefined gradient stays undefined
+        ctx->set_materialize_grads(false);
         ctx->saved_data["H"] = H;
         ctx->saved_data["W"] = W;
         ctx->mark_non_differentiable({radii, nth});
@@ -226,6 +229,7 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
         hint_refresh(meta, st);
         Tensor m_dev = meta.narrow(0, 0, 1);
         ctx->save_for_backward({gids, bins, xys, conics, colors, opacity, idx});
+        ctx->set_materialize_grads(false);  // M's gradient (always undefined): no fill
         ctx->saved_data["rec"] = rec;  // zeroed: the first backward adds into it
         ctx->saved_data["H"] = H;
         ctx->saved_data["W"] = W;

@@ -109,3 +109,39 @@ def test_unchanged_caller_train_step_matches_fused(cuda):
     with torch.no_grad():
         ra, rb = a()["render"], b()["render"]
     assert float((ra - rb).abs().max()) < 1e-3
+
+
+@pytest.mark.gpu
+def test_cpp_functions_partial_gradients(cuda):
+    """Gradient materialisation is off in both C++ Functions (no zero-fill
+    launches for depths / radii / num_tiles_hit / M): a loss on xys alone, on
+    conics alone, or on depths, takes the undefined-gradient branches and
+    gives the Python Functions' gradients."""
+    from gsplat.project_gaussians_2d import project_gaussians_2d
+    H, W = 64, 96
+    tb = ((W + 15) // 16, (H + 15) // 16, 1)
+    means, L, _ = _inputs(500, H, W, 11, cuda)
+    w_xy = torch.randn(500, 2, generator=torch.Generator().manual_seed(1)).to(cuda)
+    w_c = torch.randn(500, 3, generator=torch.Generator().manual_seed(2)).to(cuda)
+
+    def grads(python_path, which):
+        m = means.clone().requires_grad_(True)
+        l = L.clone().requires_grad_(True)
+
+        def go():
+            xys, depths, radii, conics, nth = project_gaussians_2d(m, l, H, W, tb)
+            loss = {"xys": (xys * w_xy).sum(), "conics": (conics * w_c).sum(),
+                    "depths": depths.sum() + (xys * w_xy).sum()}[which]
+            loss.backward()
+        if python_path:
+            with knobs((0, 1)):
+                go()
+        else:
+            go()
+        torch.cuda.synchronize()
+        return m.grad, l.grad
+
+    for which in ("xys", "conics", "depths"):
+        for a, b in zip(grads(False, which), grads(True, which)):
+            assert a is not None and b is not None
+            assert torch.equal(a, b), which
