@@ -33,6 +33,7 @@ _I = ctypes.c_int
 _U = ctypes.c_uint
 _F = ctypes.c_float
 _SZ = ctypes.c_size_t
+_LL = ctypes.c_longlong
 
 # name -> argtypes (restype int unless listed in _RESTYPE)
 _SIGS = {
@@ -58,6 +59,8 @@ _SIGS = {
     "gsvc_rasterize_sum_forward_slabs": [_I, _P, _P, _P, _P, _P, _P, _U, _U, _I, _I, _P, _SZ, _P,
                                          _P, _P, _P, _P, _P, _P],
     "gsvc_rasterize_sum_backward_zeroed": [_U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "gsvc_rasterize_sum_backward_zeroed_strided": [_U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _LL,
+                                                   _LL, _LL, _P, _P],
     "gsvc_compute_cov2d_bounds": [_I, _P, _P, _P, _P],
     "gsvc_cumsum_workspace_bytes": [_I],
     "gsvc_compute_cumulative_intersects": [_I, _P, _P, _P, _P, _P, _SZ, _P],

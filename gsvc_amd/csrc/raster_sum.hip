@@ -775,6 +775,17 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
 
 __device__ __forceinline__ int ceil_log2(int n) { return n <= 1 ? 0 : 32 - __clz(n - 1); }
 
+// v_out element (row i, column j, channel c) at v_out[i * h + j * w + c * c_]
+// (in floats): the HWC layout is {3 W, 3, 1}; the op path also takes the
+// autograd engine's strided gradients as they come (e.g. channel planes after
+// the caller's permute), without a copy.
+struct VStrides {
+    long long h, w, c;
+};
+__host__ __device__ inline VStrides hwc_strides(unsigned img_w) {
+    return VStrides{3ll * (long long)img_w, 3ll, 1ll};
+}
+
 // det_off (deterministic backward, det.h): each (splat, tile) sum goes to
 // det_part[9 * slot ...] instead of the record's atomics (slots past det_cap:
 // atomics); det_radii: the splats' radii for the slot's bbox.
@@ -782,7 +793,7 @@ __global__ __launch_bounds__(256) void raster_sum_bwd_kernel(
     int tbx, int img_w, int img_h, int ntiles, const int *__restrict__ ids,
     const int2 *__restrict__ bins, const float2 *__restrict__ xys, const float *__restrict__ conics,
     const float *__restrict__ colors, const float *__restrict__ opac,
-    const int *__restrict__ final_idx, const float *__restrict__ v_out,
+    const int *__restrict__ final_idx, const float *__restrict__ v_out, VStrides vs,
     float *__restrict__ grad, const int *__restrict__ det_off, const int *__restrict__ det_radii,
     float *__restrict__ det_part, long long det_cap) {
     __shared__ float4 s_pix[kTilePix];  // v_out rgb, final_idx bits
@@ -800,7 +811,8 @@ __global__ __launch_bounds__(256) void raster_sum_bwd_kernel(
     float4 pd = make_float4(0.f, 0.f, 0.f, __int_as_float(-2147483647 - 1));
     if (inside) {
         const size_t p = (size_t)pi * (size_t)img_w + (size_t)pj;
-        pd = make_float4(v_out[3 * p], v_out[3 * p + 1], v_out[3 * p + 2], __int_as_float(final_idx[p]));
+        const float *v = v_out + (long long)pi * vs.h + (long long)pj * vs.w;
+        pd = make_float4(v[0], v[vs.c], v[2 * vs.c], __int_as_float(final_idx[p]));
     }
     s_pix[tid] = pd;
     int f = __float_as_int(pd.w);
@@ -1183,20 +1195,33 @@ extern "C" int gsvc_rasterize_sum_forward_slabs(
     return sum_forward_launch(A, density_hint, s);
 }
 
-extern "C" int gsvc_rasterize_sum_backward_zeroed(
+extern "C" int gsvc_rasterize_sum_backward_zeroed_strided(
     unsigned img_height, unsigned img_width, int num_points, const int *gaussian_ids_sorted,
     const int *tile_bins, const float *xys, const float *conics, const float *colors,
-    const float *opacities, const int *final_idx, const float *v_output, float *grad_records,
-    void *stream) {
+    const float *opacities, const int *final_idx, const float *v_output, long long v_stride_h,
+    long long v_stride_w, long long v_stride_c, float *grad_records, void *stream) {
+    const VStrides vs{v_stride_h, v_stride_w, v_stride_c};
     const int tbx = ceil_div((int)img_width, kTile), tby = ceil_div((int)img_height, kTile);
-    if (num_points < 0) return set_error(GSVC_ERR_ARG, "rasterize_sum_backward_zeroed: bad num_points");
+    if (num_points < 0)
+        return set_error(GSVC_ERR_ARG, "rasterize_sum_backward_zeroed_strided: bad num_points");
     const int ntiles = tbx * tby;
     if (ntiles == 0 || num_points == 0) return GSVC_OK;
     hipLaunchKernelGGL(raster_sum_bwd_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, tbx,
                        (int)img_width, (int)img_height, ntiles, gaussian_ids_sorted,
                        (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacities,
-                       final_idx, v_output, grad_records, nullptr, nullptr, nullptr, 0ll);
-    return check_launch("rasterize_sum_backward_zeroed");
+                       final_idx, v_output, vs, grad_records, nullptr, nullptr, nullptr, 0ll);
+    return check_launch("rasterize_sum_backward_zeroed_strided");
+}
+
+extern "C" int gsvc_rasterize_sum_backward_zeroed(
+    unsigned img_height, unsigned img_width, int num_points, const int *gaussian_ids_sorted,
+    const int *tile_bins, const float *xys, const float *conics, const float *colors,
+    const float *opacities, const int *final_idx, const float *v_output, float *grad_records,
+    void *stream) {
+    const VStrides vs = hwc_strides(img_width);
+    return gsvc_rasterize_sum_backward_zeroed_strided(
+        img_height, img_width, num_points, gaussian_ids_sorted, tile_bins, xys, conics, colors,
+        opacities, final_idx, v_output, vs.h, vs.w, vs.c, grad_records, stream);
 }
 
 extern "C" int gsvc_rasterize_sum_backward(unsigned img_height, unsigned img_width, unsigned block_h,
@@ -1222,7 +1247,7 @@ extern "C" int gsvc_rasterize_sum_backward(unsigned img_height, unsigned img_wid
     hipLaunchKernelGGL(raster_sum_bwd_kernel, dim3(ntiles), dim3(256), 0, s, tbx, (int)img_width,
                        (int)img_height, ntiles, gaussian_ids_sorted, (const int2 *)tile_bins,
                        (const float2 *)xys, conics, colors, opacities, final_idx, v_output,
-                       grad_records, nullptr, nullptr, nullptr, 0ll);
+                       hwc_strides(img_width), grad_records, nullptr, nullptr, nullptr, 0ll);
     return check_launch("rasterize_sum_backward");
 }
 
@@ -1265,7 +1290,7 @@ extern "C" int gsvc_rasterize_sum_backward_det(
     hipLaunchKernelGGL(raster_sum_bwd_kernel, dim3(ntiles), dim3(256), 0, s, tbx, (int)img_width,
                        (int)img_height, ntiles, gaussian_ids_sorted, (const int2 *)tile_bins,
                        (const float2 *)xys, conics, colors, opacities, final_idx, v_output,
-                       grad_records, off, radii, part, det_capacity);
+                       hwc_strides(img_width), grad_records, off, radii, part, det_capacity);
     hipLaunchKernelGGL(det_gather_kernel, dim3(ceil_div(num_points, 256)), dim3(256), 0, s,
                        num_points, off, part, det_capacity, grad_records);
     if (pairs_out &&

@@ -243,18 +243,26 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
         const Tensor &opacity = s[5], &idx = s[6];
         const int64_t H = ctx->saved_data["H"].toInt(), W = ctx->saved_data["W"].toInt();
         const int64_t n = xys.size(0);
-        Tensor v_out = g[0].defined() ? dev_f32(g[0], "v_output") : at::zeros({H, W, 3}, xys.options());
+        // the gradient at its own strides (after GSVC's clamp + permute it
+        // arrives as channel planes; .contiguous() would copy the frame)
+        Tensor v_out = g[0];
+        if (!v_out.defined()) {
+            v_out = at::zeros({H, W, 3}, xys.options());
+        } else if (!(v_out.is_cuda() && v_out.scalar_type() == at::kFloat && v_out.dim() == 3 &&
+                     v_out.size(0) == H && v_out.size(1) == W && v_out.size(2) == 3)) {
+            v_out = dev_f32(v_out, "v_output");
+        }
         Tensor rec = ctx->saved_data["rec"].toTensor();
         if (rec.defined()) {
             ctx->saved_data["rec"] = Tensor();  // a second backward (retain_graph) zeroes its own
         } else {
             rec = at::zeros({n, 16}, xys.options());
         }
-        check(gsvc_rasterize_sum_backward_zeroed((unsigned)H, (unsigned)W, (int)n, ip(gids),
-                                                 ip(bins), fp(xys), fp(conics), fp(colors),
-                                                 fp(opacity), ip(idx), fp(v_out), fp(rec),
-                                                 stream_of(xys)),
-              "gsvc_rasterize_sum_backward_zeroed");
+        check(gsvc_rasterize_sum_backward_zeroed_strided(
+                  (unsigned)H, (unsigned)W, (int)n, ip(gids), ip(bins), fp(xys), fp(conics),
+                  fp(colors), fp(opacity), ip(idx), v_out.data_ptr<float>(), v_out.stride(0),
+                  v_out.stride(1), v_out.stride(2), fp(rec), stream_of(xys)),
+              "gsvc_rasterize_sum_backward_zeroed_strided");
         Tensor v_opac = rec.narrow(1, 8, 1);
         if (opacity.dim() != 2) v_opac = v_opac.reshape(opacity.sizes());
         return {rec.narrow(1, 0, 2), Tensor(), rec.narrow(1, 2, 3), rec.narrow(1, 5, 3), v_opac,

@@ -304,6 +304,17 @@ int gsvc_rasterize_sum_backward_zeroed(
     const int *gaussian_ids_sorted, const int *tile_bins, const float *xys,
     const float *conics, const float *colors, const float *opacities,
     const int *final_idx, const float *v_output, float *grad_records, void *stream);
+/* The same with v_output at any strides (in floats; element (row i, column j,
+ * channel c) at v_output[i * v_stride_h + j * v_stride_w + c * v_stride_c]):
+ * the autograd engine's gradient as it arrives -- after GSVC's
+ * permute(0, 3, 1, 2) it is channel planes -- read without a copy
+ * (rasterize_sum.py:189-254 calls .contiguous()).  Not part of the reference. */
+int gsvc_rasterize_sum_backward_zeroed_strided(
+    unsigned img_height, unsigned img_width, int num_points,
+    const int *gaussian_ids_sorted, const int *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacities,
+    const int *final_idx, const float *v_output, long long v_stride_h,
+    long long v_stride_w, long long v_stride_c, float *grad_records, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Whole-frame render of GSVC's per-frame model (GaussianSplats_Represent.py:

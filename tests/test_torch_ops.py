@@ -145,3 +145,40 @@ def test_cpp_functions_partial_gradients(cuda):
         for a, b in zip(grads(False, which), grads(True, which)):
             assert a is not None and b is not None
             assert torch.equal(a, b), which
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["planes", "expanded", "transposed"])
+def test_cpp_rasterize_backward_takes_strided_gradients(cuda, layout):
+    """The rasterizer backward reads the output gradient at its own strides
+    (channel planes after GSVC's permute, a broadcast, a transpose) with no
+    .contiguous() copy: the gradients equal those of the contiguous gradient
+    (within the float atomics' summation order)."""
+    from gsplat.project_gaussians_2d import project_gaussians_2d
+    from gsplat.rasterize_sum import rasterize_gaussians_sum
+    H, W = 72, 104
+    tb = ((W + 15) // 16, (H + 15) // 16, 1)
+    means, L, col = _inputs(800, H, W, 21, cuda)
+    g = torch.Generator().manual_seed(4)
+    if layout == "planes":
+        v = torch.randn(3, H, W, generator=g).to(cuda).permute(1, 2, 0)
+    elif layout == "expanded":
+        v = torch.randn(3, generator=g).to(cuda).expand(H, W, 3)
+    else:
+        v = torch.randn(W, H, 3, generator=g).to(cuda).transpose(0, 1)
+    assert not v.is_contiguous()
+
+    def grads(v_out):
+        m = means.clone().requires_grad_(True)
+        l = L.clone().requires_grad_(True)
+        c = col.clone().requires_grad_(True)
+        xys, depths, radii, conics, nth = project_gaussians_2d(m, l, H, W, tb)
+        out = rasterize_gaussians_sum(xys, depths, radii, conics, nth, c,
+                                      torch.ones(800, 1, device=cuda), H, W,
+                                      background=torch.ones(3, device=cuda))
+        out.backward(v_out)
+        torch.cuda.synchronize()
+        return m.grad, l.grad, c.grad
+
+    for a, b in zip(grads(v), grads(v.contiguous())):
+        assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max())
