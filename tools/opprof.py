@@ -9,7 +9,7 @@ so the drop-in's own share -- project / rasterize forward and their backward
 nodes -- reads apart from the caller's ops).  Run it under
 ``rocprofv3 --kernel-trace --stats`` for the kernels.
 
-    python tools/opprof.py [--calls 200] [--no-profile]
+    python tools/opprof.py [--calls 200] [--no-profile] [--only 1080p_50k_trained]
 """
 import argparse
 import cProfile
@@ -75,6 +75,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=200)
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--only", default=None, help="run one size: 1080p_50k_trained or tiny_16x16_16")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     from gsvc_amd.frame import synthetic_gt
@@ -82,6 +83,8 @@ def main():
     res = {}
     for tag, (H, W, n, st) in {"1080p_50k_trained": (1080, 1920, int(z["n"]), z),
                                "tiny_16x16_16": (16, 16, 16, None)}.items():
+        if a.only and tag != a.only:
+            continue
         m = model_at(H, W, n, dev, st)
         gt = synthetic_gt(H, W, 8, "cpu").to(dev)
         res[tag] = {k: round(timed(f, a.calls), 1) for k, f in calls(m, gt).items()}
