@@ -532,7 +532,8 @@ def main():
         from gsvc_amd import _lib
         for kv in args.knob:
             k, v = kv.split("=")
-            _lib.load().gsvc_debug_set(int(k), int(v))
+            if _lib.load().gsvc_debug_set(int(k), int(v)) < 0:
+                raise ValueError("unknown A/B knob key (gsvc_debug_set returned -1)")
 
     if args.deterministic:
         torch.use_deterministic_algorithms(True, warn_only=True)

@@ -36,7 +36,7 @@ int check_launch(const char *what);
 // for tools/ and the variant-comparison tests).  In the product library every
 // knob is the constant 0 -- the production choice -- and the diagnostic
 // variants are not compiled (``if constexpr (kDiag)`` around their launches).
-constexpr int kKnobs = 24;
+constexpr int kKnobs = 32;
 #ifdef GSVC_DIAG
 constexpr bool kDiag = true;
 extern int g_knobs[kKnobs];  // gsvc_debug_set(); knob 0 = sum-forward variant, 8 = training tile kernel

@@ -85,7 +85,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
                          const float *opac, unsigned img_h, unsigned img_w, const FrameWs &w,
                          const FrameSlots &f, float4 *grad_zero, hipStream_t s, int frames = 1,
                          const int *frame_off = nullptr, int max_frame_n = 0,
-                         const SplatOrder *ord = nullptr);
+                         const SplatOrder *ord = nullptr, int *id_slab = nullptr);
 // Bits of the strip keys at this image size (invisible splats: the largest).
 int strip_key_bits(int tbx, int tby);
 // Sort the keys a refreshing projection wrote into w.order (F = 1 workspaces).

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
     unsigned *__restrict__ counts, float4 *__restrict__ slab, int *__restrict__ m_acc,
     int *__restrict__ m_clear, float4 *__restrict__ grad_zero, long long *stamps,
     const int *__restrict__ frame_off, int counts_stride, int m_stride, size_t slab_stride,
-    int wt) {
+    int wt, int *__restrict__ ids) {
     __shared__ int s_hits[kProjThreads / 64];
     // batched frames (grid.y): this block's frame owns splats [begin, end)
     int begin = 0, end = n;
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
         if (S.P.rad > 0) {
             if (K == 1 && !(kDiag && (wt & 3)))  // paired atomics unless write-through / A/B knob 2 = 4
                 hits = slab_insert_pairs<8>(S.P.xy.x, S.P.xy.y, S.P.rad, tbx, tby, S.r0, S.r1,
-                                            S.r2, counts, slab, wt);
+                                            S.r2, counts, slab, wt, ids);
             else
                 hits = slab_insert<K>(S.P.xy.x, S.P.xy.y, S.P.rad, tbx, tby, sub, S.r0, S.r1,
                                       S.r2, counts, slab, wt);
@@ -297,7 +297,8 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
                          const float *chol_bound, const float *feat, const float *rgb_w,
                          const float *opac, unsigned img_h, unsigned img_w, const FrameWs &w,
                          const FrameSlots &f, float4 *grad_zero, hipStream_t s, int frames,
-                         const int *frame_off, int max_frame_n, const SplatOrder *ord) {
+                         const int *frame_off, int max_frame_n, const SplatOrder *ord,
+                         int *id_slab) {
     const int tbx = ceil_div((int)img_w, kTile), tby = ceil_div((int)img_h, kTile);
     const float hw = 0.5f * (float)img_w, hh = 0.5f * (float)img_h;
     if (ord && frames == 1 && n > 0) {
@@ -325,7 +326,8 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
     }
     // lanes per splat: 1 unless gsvc_debug_set(4, k) picks 2, 4 or 8 (A/B knob;
     // measured at 1080p: equal at 10k splats, 1 lane fastest at 50k)
-    const int k = knob(4) == 2 || knob(4) == 4 || knob(4) == 8 ? knob(4) : 1;
+    // id_slab (A/B knob 24): 4-byte ids instead of the 48-byte records, paired atomics
+    const int k = !id_slab && (knob(4) == 2 || knob(4) == 4 || knob(4) == 8) ? knob(4) : 1;
     const size_t slab_stride = slab_frame_f4(tbx * tby);
     // plain record stores; A/B knob 6 = 1 writes them through (sc1): measured
     // slower (projection 7.1 -> 9.8 us at 10k: each scattered 16-byte sc1 store
@@ -333,7 +335,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
     // bit 0: write-through record stores (A/B knob 6 = 1); bit 1: one 32-bit
     // slot atomic per tile instead of the pairs (A/B knob 2 = 4).  Measured
     // with the isolation runs of profiles/r01/paired_atomics/NOTES.md.
-    const int wt = (knob(6) == 1 ? 1 : 0) | (knob(2) == 4 ? 2 : 0);
+    const int wt = id_slab ? 0 : (knob(6) == 1 ? 1 : 0) | (knob(2) == 4 ? 2 : 0);
     if (frames > 1 && !frame_off) return set_error(GSVC_ERR_ARG, "frame projection: frame offsets");
     const int per = frames > 1 ? max_frame_n : n;
     if (frames > 1 && per <= 0) {
@@ -355,7 +357,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
                      xyz_tanh, chol, chol_bound, feat, rgb_w, opac, hw, hh, tbx, tby, w.xys,     \
                      w.radii, w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero,            \
                      (long long *)nullptr, frames > 1 ? frame_off : (const int *)nullptr,        \
-                     f.counts_stride, f.m_stride, slab_stride, wt);                              \
+                     f.counts_stride, f.m_stride, slab_stride, wt, id_slab);                     \
         timing_end(s, tslot, kTimingProject);                                                    \
     }
         if constexpr (kDiag) if (knob(5) == 1 && debug_ptr()) {  // diagnostic: per-wave stamps
@@ -365,7 +367,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
                                w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero,
                                reinterpret_cast<long long *>(debug_ptr()),
                                frames > 1 ? frame_off : nullptr, f.counts_stride, f.m_stride,
-                               slab_stride, wt);
+                               slab_stride, wt, id_slab);
             return check_launch("frame projection");
         }
         if constexpr (kDiag) {
@@ -425,9 +427,16 @@ static int render_frames(int frames, const int *frame_off_host, const int *frame
         ord.key = w.okey;
         ord.key_id = w.okey_id;
     }
+    // A/B knob 24 = 1 (diagnostic library): id slabs -- the projection appends each
+    // splat's id (4 B) in place of its 48-byte record, the composite gathers the
+    // records by id from w.rec (the slab memory holds the T x 256 ids)
+    int *id_slab = nullptr;
+    if constexpr (kDiag)
+        if (knob(24) == 1 && frames == 1 && !use_order && !refresh) id_slab = reinterpret_cast<int *>(w.slab);
     int rc = frame_project_launch(num_points, xyz, xyz_tanh, cholesky, cholesky_bound, features,
                                   rgb_w, opacity, img_height, img_width, w, f, nullptr, s, frames,
-                                  frame_off_dev, max_n, (use_order || refresh) ? &ord : nullptr);
+                                  frame_off_dev, max_n, (use_order || refresh) ? &ord : nullptr,
+                                  id_slab);
     if (rc) return rc;
     SumFwdArgs A;
     sum_fwd_args_init(A);
@@ -440,9 +449,15 @@ static int render_frames(int frames, const int *frame_off_host, const int *frame
     A.meta_out = meta;
     A.bg = background;
     A.sort_ids = true;
-    A.slab = w.slab;
-    A.slab_counts = f.counts;
-    A.slab_counts_clear = f.counts_next;
+    if (id_slab) {
+        A.id_counts = f.counts;
+        A.id_counts_clear = f.counts_next;
+        A.ids_rw = id_slab;
+    } else {
+        A.slab = w.slab;
+        A.slab_counts = f.counts;
+        A.slab_counts_clear = f.counts_next;
+    }
     A.cull_xys = w.xys;
     A.cull_radii = w.radii;
     A.num_points = num_points;

@@ -73,7 +73,10 @@ constexpr int kSlice = 220;  // float4s of LDS per wave (3.4 KB; sum_fwd_sparse'
 // mode: a 128-thread workgroup whose second wave exits at once still halves
 // the dispatch rate of sparse tiles.
 enum { kModeAdaptive = 6, kModeSparse = 1, kModeBanded = 2, kModeStamp = 3, kModeNoBlend = 4,
-       kModeNoStore = 5, kModeSparseStamp = 7, kModeSparsePrio = 8 };
+       kModeNoStore = 5, kModeSparseStamp = 7, kModeSparsePrio = 8, kModeSparseIds = 9 };
+// kModeSparseIds: kModeSparse over 4-byte id slabs (A.id_counts / A.ids_rw, the
+// entries' records gathered by id from A.rec) for the render paths -- the
+// projection appends ids instead of 48-byte records (A/B knob 24 = 1)
 // kModeSparsePrio: kModeSparse with the wave priority raised over the staging
 // (s_setprio 3 until the blend; A/B knob 17 = 1 selects it for the sparse launches)
 // Banded (two waves per tile) only past this many entries per tile on average.
@@ -656,9 +659,13 @@ __device__ __forceinline__ void write_sorted_ids(const SumFwdArgs &A, int tile, 
 // kIdx: final_idx is written (the autograd forward); the render paths launch
 // the kIdx = false instance, which tracks no indices.
 template <int kMode, bool kIdx>
-__global__ __launch_bounds__(kMode == kModeSparse || kMode == kModeSparseStamp || kMode == kModeSparsePrio ? 64 : 128, 8) void
+__global__ __launch_bounds__(kMode == kModeSparse || kMode == kModeSparseStamp || kMode == kModeSparsePrio ||
+                              kMode == kModeSparseIds ? 64 : 128, 8) void
 raster_sum_fwd_kernel(SumFwdArgs A) {
-    constexpr bool kOneWave = kMode == kModeSparse || kMode == kModeSparseStamp || kMode == kModeSparsePrio;
+    constexpr bool kOneWave = kMode == kModeSparse || kMode == kModeSparseStamp || kMode == kModeSparsePrio ||
+                              kMode == kModeSparseIds;
+    // id slabs: the op path's autograd forward (kIdx) and the render A/B mode
+    constexpr bool kIds = kIdx || kMode == kModeSparseIds;
     __shared__ float4 s_buf[kOneWave ? 1 : 2][kSlice];
     __shared__ int s_ids[kOneWave ? 1 : 2][kTilePix];
     // raised wave priority over the staging (loads, ranking, lists): the
@@ -711,7 +718,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         seg.recs = recs;
         seg.head = slab_rec(A.slab, A.ntiles, tile, 0);
         if (n_all <= kChunk) seg_rec = recs;  // slots past the head, at their index
-    } else if (kIdx && A.id_counts) {
+    } else if (kIds && A.id_counts) {
         // op path, unsorted id slabs (its autograd forward: kIdx instances
         // only): this call's count (M from the insertion)
         n_all = (int)__builtin_amdgcn_readfirstlane(A.id_counts[tile]);
@@ -744,13 +751,14 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
     const int ty = tile / A.tbx;
     if (kMode == kModeSparseStamp && threadIdx.x == 0) A.stamps[4 * (size_t)tile] = t0;
     const bool sparse = kMode == kModeSparse || kMode == kModeSparseStamp || kMode == kModeSparsePrio ||
+                        kMode == kModeSparseIds ||
                         ((kMode == kModeAdaptive || kMode == kModeStamp) && n <= A.sparse_max);
     if (n == 0) seg_rec = nullptr;
     const bool by_ids = A.sort_ids && !seg_rec;  // ids sorted into s_ids first
     if (sparse) {
         if (w != 0) return;
         if (by_ids)
-            n = ((A.slab || (kIdx && A.id_counts)) && n_all > kTilePix)
+            n = ((A.slab || (kIds && A.id_counts)) && n_all > kTilePix)
                     ? wave_brute_tile_ids(A, tile, s_ids[0])
                     : wave_sorted_tile_ids(seg, n_all, s_ids[0], reinterpret_cast<unsigned *>(s_buf[0]));
         if (kIdx && A.id_counts) write_sorted_ids(A, tile, range.x, n, s_ids[0]);
@@ -759,7 +767,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
     } else {
         if (ty * kTile + w * 8 >= A.img_h) return;  // band below the image
         if (by_ids)
-            n = ((A.slab || (kIdx && A.id_counts)) && n_all > kTilePix)
+            n = ((A.slab || (kIds && A.id_counts)) && n_all > kTilePix)
                     ? wave_brute_tile_ids(A, tile, s_ids[w])
                     : wave_sorted_tile_ids(seg, n_all, s_ids[w], reinterpret_cast<unsigned *>(s_buf[w]));
         if (kIdx && A.id_counts && w == 0) write_sorted_ids(A, tile, range.x, n, s_ids[0]);
@@ -1026,6 +1034,11 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
                    ? kModeBanded
                    : kModeSparse;
     if (knob(17) == 1 && mode == kModeSparse) mode = kModeSparsePrio;  // A/B knob 17
+    if (A.id_counts && !A.final_idx) {
+        // render over id slabs (A/B knob 24): the sparse kernel's id instance only
+        if (!kDiag) return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: id slabs need final_idx");
+        mode = kModeSparseIds;
+    }
     if (mode == kModeStamp && A.layout != kLayoutHWC)
         return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: stamp mode needs the HWC layout");
     if (A.frames > 1 && (mode == kModeStamp || mode == kModeSparseStamp))
@@ -1068,6 +1081,9 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
                 A.stamps = reinterpret_cast<long long *>(debug_ptr());
                 launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeSparseStamp, true> : raster_sum_fwd_kernel<kModeSparseStamp, false>, grid,
                            dim3(64), s, tev, A);
+                break;
+            case kModeSparseIds:
+                launch_fwd(raster_sum_fwd_kernel<kModeSparseIds, false>, grid, dim3(64), s, tev, A);
                 break;
             case kModeSparsePrio:
                 launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeSparsePrio, true>

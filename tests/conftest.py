@@ -39,6 +39,8 @@ def knobs(*pairs):
         return
     with _lib.diagnostic() as lib:
         olds = [(k, lib.gsvc_debug_set(k, v)) for k, v in pairs]
+        # an unknown key returns -1 and sets nothing: an A/B that would test nothing
+        assert all(o >= 0 for _, o in olds), f"knob key out of range: {pairs}"
         try:
             yield lib
         finally:

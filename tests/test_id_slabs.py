@@ -1,0 +1,46 @@
+"""GPU suite: the render over 4-byte id slabs (A/B knob 24 = 1, diagnostic
+library) against the product render over 48-byte slab
+records.  Same entries per tile, same id order, same blend: the images must
+be bit-identical, including tiles past 256 entries (their first 256 ids
+rebuilt from the bboxes), ragged image sizes and a frame with no
+intersections (rasterize_sum.py:121-127's background)."""
+import pytest
+import torch
+
+from conftest import knobs
+
+pytestmark = pytest.mark.gpu
+
+
+def _frame(n, seed, chol, dev, cluster=0.0):
+    g = torch.Generator().manual_seed(seed)
+    xyz = torch.atanh(2 * (torch.rand(n, 2, generator=g) - 0.5) * 0.999)
+    if cluster > 0:  # a share of the splats piled onto a few tiles
+        k = int(n * cluster)
+        xyz[:k] = torch.atanh(0.02 * (torch.rand(k, 2, generator=g) - 0.5))
+    chol = torch.rand(n, 3, generator=g) * chol
+    feat = torch.rand(n, 3, generator=g)
+    return xyz.to(dev), chol.to(dev), feat.to(dev)
+
+
+@pytest.mark.parametrize("n,H,W,chol,cluster", [
+    (10000, 1080, 1920, 1.0, 0.0),
+    (50000, 1080, 1920, 3.0, 0.0),
+    (20000, 360, 640, 1.0, 0.2),   # tiles past 256 entries
+    (3000, 250, 333, 1.0, 0.0),    # ragged edge tiles
+    (500, 128, 128, 0.0, 0.0),     # L = 0 (no bound): no intersections, the background
+])
+def test_id_slab_render_bit_identical(cuda, n, H, W, chol, cluster):
+    from gsvc_amd.render import render_frame_sum
+    xyz, c, f = _frame(n, 7 + n, chol, cuda, cluster)
+    bound = torch.tensor([0.5, 0.0, 0.5], device=cuda) if chol > 0 else None
+    bg = torch.tensor([0.3, 0.6, 0.9], device=cuda)
+    ref = [render_frame_sum(xyz, c, f, H, W, bg, cholesky_bound=bound) for _ in range(2)]
+    with knobs((24, 1)):
+        got = [render_frame_sum(xyz, c, f, H, W, bg, cholesky_bound=bound) for _ in range(3)]
+    torch.cuda.synchronize()
+    assert torch.equal(ref[0], ref[1])
+    for g in got:
+        assert torch.equal(g, ref[0])
+    if chol == 0:
+        assert torch.equal(ref[0][0], bg.view(3, 1, 1).expand(3, H, W))

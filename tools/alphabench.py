@@ -65,7 +65,8 @@ def main():
         lib = L.load()
         for kv in a.knob:
             k, v = kv.split("=")
-            lib.gsvc_debug_set(int(k), int(v))
+            if lib.gsvc_debug_set(int(k), int(v)) < 0:
+                raise ValueError("unknown A/B knob key (gsvc_debug_set returned -1)")
     for n in a.splats:
         fwd = run(n, a.calls, dev, False)
         both = run(n, a.calls, dev, True)

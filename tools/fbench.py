@@ -42,6 +42,9 @@ def main():
                     help="rasterizer modes (gsvc_debug_set(0)); 0 = automatic")
     ap.add_argument("--knob", type=int, nargs=2, action="append", default=[],
                     metavar=("KEY", "VALUE"), help="extra gsvc_debug_set for a second pass")
+    ap.add_argument("--set", type=int, nargs=2, action="append", default=[],
+                    metavar=("KEY", "VALUE"), help="gsvc_debug_set for every pass (e.g. to trace "
+                    "one variant alone)")
     ap.add_argument("--stamps", action="store_true",
                     help="also run the timestamped one-wave kernel (mode 7) and print phases")
     ap.add_argument("--stamps-out", default=None,
@@ -50,6 +53,9 @@ def main():
                     help="also stamp the projection kernel's waves (knob 5) and print phases")
     args = ap.parse_args()
     lib = L.load()
+    for k, v in args.set:
+        if lib.gsvc_debug_set(k, v) < 0:
+            raise ValueError("unknown A/B knob key (gsvc_debug_set returned -1)")
     dev = torch.device("cuda:0")
     for n in args.splats:
         g = torch.Generator().manual_seed(n)
@@ -80,7 +86,8 @@ def main():
         for mode, kv in passes:
             lib.gsvc_debug_set(0, mode)
             if kv:
-                lib.gsvc_debug_set(kv[0], kv[1])
+                if lib.gsvc_debug_set(kv[0], kv[1]) < 0:
+                    raise ValueError("unknown A/B knob key (gsvc_debug_set returned -1)")
 
             hint = [0]  # the density hint render.py passes: M of an earlier frame
 

@@ -65,7 +65,8 @@ def main():
     _lib.load().gsvc_debug_set(8, 1 if a.tile_kernel == "wg256" else 0)
     for kv in a.knob:
         k, v = kv.split("=")
-        _lib.load().gsvc_debug_set(int(k), int(v))
+        if _lib.load().gsvc_debug_set(int(k), int(v)) < 0:
+            raise ValueError("unknown A/B knob key (gsvc_debug_set returned -1)")
     dev = torch.device("cuda:0")
     H, W = 1080, 1920
     model = make_frame_model(H, W, a.splats, dev, seed=7,
@@ -76,7 +77,8 @@ def main():
     torch.cuda.synchronize()
     for kv in a.knob_after:
         k, v = kv.split("=")
-        _lib.load().gsvc_debug_set(int(k), int(v))
+        if _lib.load().gsvc_debug_set(int(k), int(v)) < 0:
+            raise ValueError("unknown A/B knob key (gsvc_debug_set returned -1)")
     if a.frozen:
         from gsvc_amd import ops
         from gsvc_amd.train import train_step_sum

@@ -30,7 +30,8 @@ def main():
     for f in a.frames:
         for kv in [None] + a.knob:
             if kv:
-                lib.gsvc_debug_set(kv[0], kv[1])
+                if lib.gsvc_debug_set(kv[0], kv[1]) < 0:
+                    raise ValueError("unknown A/B knob key (gsvc_debug_set returned -1)")
             r = bench.video_decode(dev, frames=f)
             if kv:
                 lib.gsvc_debug_set(kv[0], 0)
