@@ -5,9 +5,9 @@
 For each rasterizer mode (gsvc_debug_set(0)) captures ``iters`` back-to-back
 frame renders in a HIP graph, replays it and prints microseconds per frame.
 Every mode's image must equal the first one bit for bit.  (A frame inside a
-graph keeps its frame_index argument from capture time; the two M slots then
-alternate only between replays, so frames of one replay share a slot --
-harmless here since every frame renders the same splats.)
+graph keeps its frame_index argument from capture time, so a graph must hold
+an even number of frames for the two parity slots to keep alternating across
+replays; ``iters`` is rounded down to even.)
 """
 from __future__ import annotations
 
@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--proj-stamps", action="store_true",
                     help="also stamp the projection kernel's waves (knob 5) and print phases")
     args = ap.parse_args()
+    args.iters = max(2, args.iters - args.iters % 2)
     lib = L.load()
     for k, v in args.set:
         if lib.gsvc_debug_set(k, v) < 0:
@@ -84,6 +85,12 @@ def main():
         passes = [(mode, None) for mode in args.modes] + [(m, kv) for kv in args.knob
                                                           for m in args.modes]
         for mode, kv in passes:
+            # every pass from a zeroed workspace: the captured graph below freezes
+            # each frame's parity (see the module docstring), so the counts it
+            # leaves are stale, and a variant that reads the slab memory in
+            # another layout (knob 24: ids) must not inherit them
+            torch.cuda.synchronize()
+            ws.zero_()
             lib.gsvc_debug_set(0, mode)
             if kv:
                 if lib.gsvc_debug_set(kv[0], kv[1]) < 0:
@@ -115,21 +122,26 @@ def main():
                 b.record()
                 torch.cuda.synchronize()
                 best = min(best, a.elapsed_time(b) * 1e3 / args.iters)
-            # the same frame as a one-frame graph replayed per step (host
-            # submits one graph per frame, as a per-call graph launch would)
+            # the same frame as a small graph replayed per step (host submits
+            # one graph per frame, as a per-call graph launch would).  Two
+            # frames per graph: a frame's parity is frozen at capture, and a
+            # one-frame graph replayed would re-add to the same counts every
+            # time (duplicate entries, then every tile past 256: the bbox
+            # rebuild -- not a valid state of the workspace contract)
             g1 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1):
+                frame()
                 frame()
             g1.replay()
             torch.cuda.synchronize()
             a1 = torch.cuda.Event(enable_timing=True)
             b1 = torch.cuda.Event(enable_timing=True)
             a1.record()
-            for _ in range(args.iters):
+            for _ in range(args.iters // 2):
                 g1.replay()
             b1.record()
             torch.cuda.synchronize()
-            per_graph = a1.elapsed_time(b1) * 1e3 / args.iters
+            per_graph = a1.elapsed_time(b1) * 1e3 / (2 * (args.iters // 2))
             # and as plain launches (the library call per step, no graph)
             a1.record()
             for _ in range(args.iters):
