@@ -183,7 +183,8 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_ordered_kernel(
     unsigned *__restrict__ counts, float4 *__restrict__ slab, int *__restrict__ m_acc,
     int *__restrict__ m_clear, float4 *__restrict__ grad_zero, unsigned *__restrict__ key,
     int *__restrict__ key_id, unsigned key_invisible, long long *stamps,
-    int *__restrict__ carry_ids, uint2 *__restrict__ carry_box, uint2 *__restrict__ carry_hull) {
+    int *__restrict__ carry_ids, uint2 *__restrict__ carry_box, uint2 *__restrict__ carry_hull,
+    int *__restrict__ id_slab) {
     __shared__ int s_hits[kProjThreads / 64];
     __shared__ unsigned s_cnt[kAggWin];
     __shared__ int s_box[4][kProjThreads / 64];
@@ -217,8 +218,10 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_ordered_kernel(
         if (carry_ids) carry_box[i] = carry_hull[i] = pack_box(x0, y0, x1, y1);
     }
     if (kStamp && lane == 0) st[1] = proj_stamp();
+    // ids in place of records: the carried bins' candidate lists, or the
+    // render's id slabs (both 256 slots per tile)
     const int hits = slab_insert_window(S, x0, y0, x1, y1, tbx, tby, counts, slab, s_cnt, s_box, st,
-                                        carry_ids);
+                                        carry_ids ? carry_ids : id_slab);
     if (kStamp) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) st[2] = proj_stamp();
@@ -310,7 +313,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
                                ord->carry_ids ? ord->carry_counts : f.counts, w.slab, f.m_acc,
                                f.m_clear, grad_zero, ord->key, ord->key_id, strip_key_invisible(tbx, tby),
                                reinterpret_cast<long long *>(debug_ptr()), ord->carry_ids,
-                               ord->carry_box, ord->carry_hull);
+                               ord->carry_box, ord->carry_hull, id_slab);
             return check_launch("frame projection (ordered)");
         }
         hipEvent_t tev[2];
@@ -320,7 +323,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
                      tby, w.xys, w.radii, w.rec, ord->carry_ids ? ord->carry_counts : f.counts,
                      w.slab, f.m_acc, f.m_clear, grad_zero, ord->key, ord->key_id,
                      strip_key_invisible(tbx, tby), (long long *)nullptr, ord->carry_ids,
-                     ord->carry_box, ord->carry_hull);
+                     ord->carry_box, ord->carry_hull, id_slab);
         timing_end(s, tslot, kTimingProject);
         return check_launch("frame projection (ordered)");
     }
@@ -427,12 +430,14 @@ static int render_frames(int frames, const int *frame_off_host, const int *frame
         ord.key = w.okey;
         ord.key_id = w.okey_id;
     }
-    // A/B knob 24 = 1 (diagnostic library): id slabs -- the projection appends each
-    // splat's id (4 B) in place of its 48-byte record, the composite gathers the
-    // records by id from w.rec (the slab memory holds the T x 256 ids)
+    // A single sparse frame renders over id slabs: the projection appends each
+    // splat's id (4 B) in place of its 48-byte record and the composite gathers
+    // the records by id from w.rec (the slab memory holds the T x 256 ids).
+    // Batched frames and dense frames (the banded kernel) keep the records;
+    // A/B knob 24 = 1 (diagnostic library) too.
     int *id_slab = nullptr;
-    if constexpr (kDiag)
-        if (knob(24) == 1 && frames == 1 && !use_order && !refresh) id_slab = reinterpret_cast<int *>(w.slab);
+    if (frames == 1 && !sum_forward_dense(density_hint, ntiles, 1) && knob(24) != 1)
+        id_slab = reinterpret_cast<int *>(w.slab);
     int rc = frame_project_launch(num_points, xyz, xyz_tanh, cholesky, cholesky_bound, features,
                                   rgb_w, opacity, img_height, img_width, w, f, nullptr, s, frames,
                                   frame_off_dev, max_n, (use_order || refresh) ? &ord : nullptr,

@@ -72,5 +72,10 @@ struct SumFwdArgs {
 // ``density_hint`` (or the gsvc_debug_set(0) override).
 void sum_fwd_args_init(SumFwdArgs &A);
 int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s);
+// The launcher's sparse / banded choice from the caller's intersection count
+// (M of an earlier frame): true = banded (two waves per tile).  Render over
+// id slabs (A.id_counts without final_idx) is the sparse kernel only, so a
+// render takes id slabs exactly when this is false.
+bool sum_forward_dense(int density_hint, int ntiles, int frames);
 
 }  // namespace gsvc

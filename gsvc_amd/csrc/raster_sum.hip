@@ -75,8 +75,10 @@ constexpr int kSlice = 220;  // float4s of LDS per wave (3.4 KB; sum_fwd_sparse'
 enum { kModeAdaptive = 6, kModeSparse = 1, kModeBanded = 2, kModeStamp = 3, kModeNoBlend = 4,
        kModeNoStore = 5, kModeSparseStamp = 7, kModeSparsePrio = 8, kModeSparseIds = 9 };
 // kModeSparseIds: kModeSparse over 4-byte id slabs (A.id_counts / A.ids_rw, the
-// entries' records gathered by id from A.rec) for the render paths -- the
-// projection appends ids instead of 48-byte records (A/B knob 24 = 1)
+// entries' records gathered by id from A.rec): the single-frame render -- its
+// projection appends ids instead of 48-byte records (trained 1080p / 50k:
+// projection 14.9 -> 10.5 us, composite 20.7 -> 21.4, frame 25.8k -> 28.8k fps;
+// 10k equal; profiles/r04/id_slabs/).  A/B knob 24 = 1 restores the records.
 // kModeSparsePrio: kModeSparse with the wave priority raised over the staging
 // (s_setprio 3 until the blend; A/B knob 17 = 1 selects it for the sparse launches)
 // Banded (two waves per tile) only past this many entries per tile on average.
@@ -274,7 +276,7 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
                                                float4 *s_slice, float3 init, bool ids_in_lds,
                                                const int *s_ids, const float4 *seg_rec,
                                                const float4 *seg_head, float4 spec0, float4 spec1,
-                                               float4 spec2, int spec_slots) {
+                                               float4 spec2, int spec_slots, int spec_id) {
     // staged entries (slot kChunk: the grouped loop's no-op sentinel), their
     // blocks, and the lane groups' lists [64 iterations][16 groups]
     constexpr int kS = kChunk + 1, kS4 = (kS + 3) / 4;
@@ -311,7 +313,9 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
             // <= 64 slab records in fill order: staged at their rank by id
         float4 geo = spec0, col = spec1, bx = spec2;
         if (lane >= spec_slots && lane < cnt) {
-            const float4 *r = slot_rec(seg_head, seg_rec, lane);
+            // slab records at their slot, or (id slabs, no head) the record of
+            // the lane's id gathered from A.rec -- the same 48 bytes
+            const float4 *r = seg_head ? slot_rec(seg_head, seg_rec, lane) : A.rec + 3 * (size_t)spec_id;
             geo = r[0];
             col = r[1];
             bx = r[2];
@@ -693,6 +697,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
     int n_all;
     const float4 *seg_rec = nullptr;  // slab records, when the fast path applies
     float4 spec0 = make_float4(0.f, 0.f, 0.f, 0.f), spec1 = spec0, spec2 = spec0;
+    int spec_id = 0;  // id slabs (render): the lane's slot, loaded with the count
     if (A.slab) {
         // this frame's count, and the first kSpecSlots records loaded in the
         // same round trip (speculatively: most tiles have that few)
@@ -722,6 +727,9 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         // op path, unsorted id slabs (its autograd forward: kIdx instances
         // only): this call's count (M from the insertion)
         n_all = (int)__builtin_amdgcn_readfirstlane(A.id_counts[tile]);
+        // render over id slabs: slot `lane` in the same round trip as the count
+        // (all 256 slots of every tile exist; past the count it is not used)
+        if (kMode == kModeSparseIds) spec_id = A.ids_rw[(size_t)tile * kTilePix + (threadIdx.x & 63)];
         if (threadIdx.x == 0) {
             A.id_counts_clear[tile] = 0u;  // the next call's counts
             if (tile == 0) {
@@ -733,6 +741,9 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         seg.ids = A.ids_rw + (size_t)tile * kTilePix;
         seg.recs = nullptr;
         seg.head = nullptr;
+        // render, <= 64 entries: records gathered by id and ranked straight
+        // into the staging, as the slab records are (sum_fwd_sparse)
+        if (kMode == kModeSparseIds && n_all <= kChunk) seg_rec = A.rec;
     } else {
         range = A.bins[tile];
         n_all = range.y - range.x;
@@ -763,7 +774,8 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
                     : wave_sorted_tile_ids(seg, n_all, s_ids[0], reinterpret_cast<unsigned *>(s_buf[0]));
         if (kIdx && A.id_counts) write_sorted_ids(A, tile, range.x, n, s_ids[0]);
         sum_fwd_sparse<kMode, kIdx>(A, tile, range, n, s_buf[0], init, by_ids, s_ids[0], seg_rec,
-                                    seg.head, spec0, spec1, spec2, A.spec_slots);
+                                    seg.head, spec0, spec1, spec2, seg.head ? A.spec_slots : 0,
+                                    spec_id);
     } else {
         if (ty * kTile + w * 8 >= A.img_h) return;  // band below the image
         if (by_ids)
@@ -1000,6 +1012,11 @@ __global__ __launch_bounds__(kProjThreads) void tile_insert_ids_kernel(
     add_hits(hits, s_hits, m_acc);
 }
 
+bool sum_forward_dense(int density_hint, int ntiles, int frames) {
+    if (knob(0) != 0) return knob(0) != kModeSparse;  // a forced kernel mode (A/B): no id slabs
+    return (long long)density_hint > (long long)kDenseEntriesPerTile * ntiles * frames;
+}
+
 void sum_fwd_args_init(SumFwdArgs &A) {
     A = SumFwdArgs{};
     A.sparse_max = knob(3) > 0 ? knob(3) : 8;
@@ -1029,16 +1046,9 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
     A.store_policy = knob(7);  // kStoreNtSc1 unless an A/B run selects another (knob 7)
     const int ntiles = A.ntiles;
     int mode = knob(0);
-    if (mode == 0)
-        mode = ((long long)density_hint > (long long)kDenseEntriesPerTile * ntiles * A.frames)
-                   ? kModeBanded
-                   : kModeSparse;
+    if (mode == 0) mode = sum_forward_dense(density_hint, ntiles, A.frames) ? kModeBanded : kModeSparse;
     if (knob(17) == 1 && mode == kModeSparse) mode = kModeSparsePrio;  // A/B knob 17
-    if (A.id_counts && !A.final_idx) {
-        // render over id slabs (A/B knob 24): the sparse kernel's id instance only
-        if (!kDiag) return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: id slabs need final_idx");
-        mode = kModeSparseIds;
-    }
+    if (A.id_counts && !A.final_idx) mode = kModeSparseIds;  // render over id slabs: one instance
     if (mode == kModeStamp && A.layout != kLayoutHWC)
         return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: stamp mode needs the HWC layout");
     if (A.frames > 1 && (mode == kModeStamp || mode == kModeSparseStamp))
@@ -1054,6 +1064,8 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
         launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeBanded, true>
                                : raster_sum_fwd_kernel<kModeBanded, false>,
                    grid, dim3(128), s, tev, A);
+    } else if (mode == kModeSparseIds) {
+        launch_fwd(raster_sum_fwd_kernel<kModeSparseIds, false>, grid, dim3(64), s, tev, A);
     } else if constexpr (kDiag) {
         // diagnostic variants (libgsvc_amd_diag.so only)
         switch (mode) {
@@ -1081,9 +1093,6 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
                 A.stamps = reinterpret_cast<long long *>(debug_ptr());
                 launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeSparseStamp, true> : raster_sum_fwd_kernel<kModeSparseStamp, false>, grid,
                            dim3(64), s, tev, A);
-                break;
-            case kModeSparseIds:
-                launch_fwd(raster_sum_fwd_kernel<kModeSparseIds, false>, grid, dim3(64), s, tev, A);
                 break;
             case kModeSparsePrio:
                 launch_fwd(A.final_idx ? raster_sum_fwd_kernel<kModeSparsePrio, true>

@@ -1,9 +1,11 @@
-"""GPU suite: the render over 4-byte id slabs (A/B knob 24 = 1, diagnostic
-library) against the product render over 48-byte slab
-records.  Same entries per tile, same id order, same blend: the images must
-be bit-identical, including tiles past 256 entries (their first 256 ids
-rebuilt from the bboxes), ragged image sizes and a frame with no
-intersections (rasterize_sum.py:121-127's background)."""
+"""GPU suite: the single-frame render over 4-byte id slabs (the product
+default for sparse frames) against the render over 48-byte
+slab records (A/B knob 24 = 1, diagnostic library) and the banded kernel
+(knob 0 = 2, records).  Same entries per tile, same id order, same blend: the
+images must be bit-identical, including tiles past 256 entries (their first
+256 ids rebuilt from the bboxes), ragged image sizes and a frame with no
+intersections (rasterize_sum.py:121-127's background).  The calls go through
+render_frame_sum, i.e. the ordered projection after the first call."""
 import pytest
 import torch
 
@@ -36,8 +38,10 @@ def test_id_slab_render_bit_identical(cuda, n, H, W, chol, cluster):
     bound = torch.tensor([0.5, 0.0, 0.5], device=cuda) if chol > 0 else None
     bg = torch.tensor([0.3, 0.6, 0.9], device=cuda)
     ref = [render_frame_sum(xyz, c, f, H, W, bg, cholesky_bound=bound) for _ in range(2)]
-    with knobs((24, 1)):
-        got = [render_frame_sum(xyz, c, f, H, W, bg, cholesky_bound=bound) for _ in range(3)]
+    got = []
+    for pair in ((24, 1), (0, 2)):
+        with knobs(pair):
+            got += [render_frame_sum(xyz, c, f, H, W, bg, cholesky_bound=bound) for _ in range(3)]
     torch.cuda.synchronize()
     assert torch.equal(ref[0], ref[1])
     for g in got:
