@@ -114,6 +114,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
         end = frame_off[b + 1];
         counts += (size_t)b * counts_stride;
         slab += b * slab_stride;
+        if (ids) ids += 4 * b * slab_stride;  // id slabs in the frame's slab memory
         m_acc += (size_t)b * m_stride;
         m_clear += (size_t)b * m_stride;
     }
@@ -436,7 +437,8 @@ static int render_frames(int frames, const int *frame_off_host, const int *frame
     // Batched frames and dense frames (the banded kernel) keep the records;
     // A/B knob 24 = 1 (diagnostic library) too.
     int *id_slab = nullptr;
-    if (frames == 1 && !sum_forward_dense(density_hint, ntiles, 1) && knob(24) != 1)
+    if (!sum_forward_dense(density_hint, ntiles, frames) && knob(24) != 1 &&
+        (frames == 1 || knob(25) == 1))  // A/B knob 25 = 1: batched frames too
         id_slab = reinterpret_cast<int *>(w.slab);
     int rc = frame_project_launch(num_points, xyz, xyz_tanh, cholesky, cholesky_bound, features,
                                   rgb_w, opacity, img_height, img_width, w, f, nullptr, s, frames,

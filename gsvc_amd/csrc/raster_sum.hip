@@ -681,9 +681,16 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
     if (A.frames > 1) {  // batched frames: this block's frame and tile
         const int b = tile / A.ntiles;
         tile -= b * A.ntiles;
-        A.slab += b * A.slab_stride;
-        A.slab_counts += (size_t)b * A.counts_stride;
-        A.slab_counts_clear += (size_t)b * A.counts_stride;
+        if (A.slab) {  // (an offset null pointer would read as a slab)
+            A.slab += b * A.slab_stride;
+            A.slab_counts += (size_t)b * A.counts_stride;
+            A.slab_counts_clear += (size_t)b * A.counts_stride;
+        }
+        if (kMode == kModeSparseIds) {  // id slabs in each frame's slab memory
+            A.ids_rw += 4 * b * A.slab_stride;
+            A.id_counts += (size_t)b * A.counts_stride;
+            A.id_counts_clear += (size_t)b * A.counts_stride;
+        }
         A.m_dev += (size_t)b * A.m_stride;
         A.meta_out += (size_t)b * A.m_stride;
         A.out += b * A.out_stride;

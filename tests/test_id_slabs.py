@@ -48,3 +48,24 @@ def test_id_slab_render_bit_identical(cuda, n, H, W, chol, cluster):
         assert torch.equal(g, ref[0])
     if chol == 0:
         assert torch.equal(ref[0][0], bg.view(3, 1, 1).expand(3, H, W))
+
+
+def test_id_slab_batched_render_bit_identical(cuda):
+    """Batched frames (gsvc_render_frames_sum) over id slabs (A/B knob 25 = 1)
+    against the records: every frame's image bit-identical."""
+    from gsvc_amd.render import render_frames_sum
+    H, W = 270, 480
+    sizes = [3000, 0, 5000, 1200]
+    parts = [_frame(n, 100 + k, 1.0, cuda) for k, n in enumerate(sizes)]
+    xyz = torch.cat([p[0] for p in parts])
+    chol = torch.cat([p[1] for p in parts])
+    feat = torch.cat([p[2] for p in parts])
+    bound = torch.tensor([0.5, 0.0, 0.5], device=cuda)
+    bg = torch.ones(3, device=cuda)
+    ref = render_frames_sum(xyz, chol, feat, sizes, H, W, bg, cholesky_bound=bound)
+    with knobs((25, 1)):
+        got = [render_frames_sum(xyz, chol, feat, sizes, H, W, bg, cholesky_bound=bound)
+               for _ in range(3)]
+    torch.cuda.synchronize()
+    for g in got:
+        assert torch.equal(g, ref)
