@@ -135,7 +135,10 @@ __device__ __forceinline__ void blend_pair(float gx, float ha, float b, float bd
 // kSigmaCutBits -- the same pairs pass, sigma is never NaN there, and
 // alpha = exp(-sigma) <= 1 needs no min), and a failing pair adds colour * 0
 // instead of selecting (+-0: an accumulator starts at +0 and is never -0).
-// The same bits as blend_pair without the last-index tracking.
+// The same bits as blend_pair without the last-index tracking.  (An indexed
+// variant -- final_idx from the same threshold test -- measured slower in the
+// op path's composite: 28.3 vs 27.5 us at the trained 1080p / 50k frame, its
+// extra loop bodies spilled 17 VGPRs around the chunk loop.)
 __device__ __forceinline__ void blend_pair_cut(float gx, float ha, float bdy, float cq, float cr,
                                                float cg, float cb, v2f px, v2f &ar, v2f &ag,
                                                v2f &ab) {
@@ -736,7 +739,11 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         n_all = (int)__builtin_amdgcn_readfirstlane(A.id_counts[tile]);
         // render over id slabs: slot `lane` in the same round trip as the count
         // (all 256 slots of every tile exist; past the count it is not used)
-        if (kMode == kModeSparseIds) spec_id = A.ids_rw[(size_t)tile * kTilePix + (threadIdx.x & 63)];
+        // (measured for the op path's indexed instance too, its <= 64 ids ranked
+        // from these: slower, 44.3 vs 42.4 us per tools/slabbench.py call at
+        // the trained 1080p / 50k frame -- its ids stay read after the count)
+        if (kMode == kModeSparseIds)
+            spec_id = A.ids_rw[(size_t)tile * kTilePix + (threadIdx.x & 63)];
         if (threadIdx.x == 0) {
             A.id_counts_clear[tile] = 0u;  // the next call's counts
             if (tile == 0) {
