@@ -58,6 +58,9 @@ _SIGS = {
     "gsvc_rasterize_sum_slabs_workspace_bytes": [_I],
     "gsvc_rasterize_sum_forward_slabs": [_I, _P, _P, _P, _P, _P, _P, _U, _U, _I, _I, _P, _SZ, _P,
                                          _P, _P, _P, _P, _P, _P],
+    "gsvc_rasterize_sum_order_workspace_bytes": [_I],
+    "gsvc_rasterize_sum_forward_slabs_ordered": [_I, _P, _P, _P, _P, _P, _P, _U, _U, _I, _I, _P, _SZ,
+                                                 _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _I],
     "gsvc_rasterize_sum_backward_zeroed": [_U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "gsvc_rasterize_sum_backward_zeroed_strided": [_U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _LL,
                                                    _LL, _LL, _P, _P],
@@ -127,6 +130,7 @@ _RESTYPE = {
     "gsvc_bin_tiles_counted_workspace_bytes": _SZ,
     "gsvc_render_frame_workspace_bytes": _SZ,
     "gsvc_rasterize_sum_slabs_workspace_bytes": _SZ,
+    "gsvc_rasterize_sum_order_workspace_bytes": _SZ,
     "gsvc_render_frame_zeroed_bytes": _SZ,
     "gsvc_train_step_workspace_bytes": _SZ,
     "gsvc_train_step_det_workspace_bytes": _SZ,

@@ -1026,6 +1026,84 @@ __global__ __launch_bounds__(kProjThreads) void tile_insert_ids_kernel(
     add_hits(hits, s_hits, m_acc);
 }
 
+// The same insertion with a splat order (gsvc_rasterize_sum_forward_slabs_ordered):
+// lane t inserts splat order[t] (NULL: t), and the workgroup -- spatially
+// coherent once ``order`` sorts the splats by their centre's tile strip --
+// takes its slots window-wise (frame_dev.h slab_insert_window: one device
+// atomic per touched tile of the block's window instead of one per (splat,
+// tile)).  The slabs hold the same ids per tile either way; the composite
+// sorts them.  ``key`` (the refresh call): each splat's strip key and id for
+// the next order.
+__global__ __launch_bounds__(kProjThreads) void tile_insert_ids_ordered_kernel(
+    int n, const int *__restrict__ order, const float2 *__restrict__ xys,
+    const int *__restrict__ radii, int tbx, int tby, unsigned *__restrict__ counts,
+    int *__restrict__ ids, int *__restrict__ m_acc, int *__restrict__ m_clear,
+    float4 *__restrict__ rec_zero, unsigned *__restrict__ key, int *__restrict__ key_id,
+    unsigned key_invisible) {
+    __shared__ int s_hits[kProjThreads / 64];
+    __shared__ unsigned s_cnt[kAggWin];
+    __shared__ int s_box[4][kProjThreads / 64];
+    const int t = blockIdx.x * kProjThreads + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *m_clear = 0;  // the next call's M
+    const int i = t < n ? (order ? order[t] : t) : n;
+    SplatOut S;
+    S.P.xy = make_float2(0.f, 0.f);
+    S.P.rad = 0;
+    S.r0 = S.r1 = make_float4(0.f, 0.f, 0.f, 0.f);
+    S.r2 = make_float4(0.f, __int_as_float(i), 0.f, 0.f);  // the id (slab_insert_window's ids)
+    unsigned x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+    if (i < n) {
+        if (rec_zero) {
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rec_zero[4 * (size_t)i + q] = z;
+        }
+        const int r = radii[i];
+        const float2 c = xys[i];
+        S.P.xy = c;
+        S.P.rad = r;
+        if (r > 0) tile_bbox(c.x, c.y, (float)r, tbx, tby, x0, y0, x1, y1);
+        if (key) {
+            key[i] = strip_key(c.x, c.y, r, tbx, tby, key_invisible);
+            key_id[i] = i;
+        }
+    }
+    // every lane of the block (block-uniform control flow inside)
+    const int hits = slab_insert_window(S, x0, y0, x1, y1, tbx, tby, counts, nullptr, s_cnt, s_box,
+                                        nullptr, ids);
+    add_hits(hits, s_hits, m_acc);
+}
+
+// The op path's splat-order buffers (n-sized): strip keys and ids, the sorted
+// keys and the order, the sort's scratch and counters.
+struct OpOrderWs {
+    unsigned *okey, *skey, *kbuf;
+    int *okey_id, *order, *vbuf;
+    unsigned *sort_counts, *sort_offsets;
+    size_t bytes;
+};
+static OpOrderWs op_order_ws(char *base, int n) {
+    OpOrderWs w;
+    size_t off = 0;
+    const size_t nn = (size_t)(n > 0 ? n : 1);
+    auto take = [&](size_t b) {
+        char *p = base ? base + off : nullptr;
+        off += ws_align(b);
+        return p;
+    };
+    w.okey = (unsigned *)take(sizeof(unsigned) * nn);
+    w.skey = (unsigned *)take(sizeof(unsigned) * nn);
+    w.kbuf = (unsigned *)take(sizeof(unsigned) * nn);
+    w.okey_id = (int *)take(sizeof(int) * nn);
+    w.order = (int *)take(sizeof(int) * nn);
+    w.vbuf = (int *)take(sizeof(int) * nn);
+    const size_t cb = sort_u32_counts_bytes(n > 0 ? n : 1);
+    w.sort_counts = (unsigned *)take(cb);
+    w.sort_offsets = (unsigned *)take(cb);
+    w.bytes = off;
+    return w;
+}
+
 bool sum_forward_dense(int density_hint, int ntiles, int frames) {
     if (knob(0) != 0) return knob(0) != kModeSparse;  // a forced kernel mode (A/B): no id slabs
     return (long long)density_hint > (long long)kDenseEntriesPerTile * ntiles * frames;
@@ -1180,12 +1258,12 @@ extern "C" size_t gsvc_rasterize_sum_slabs_workspace_bytes(int num_tiles) {
     return sizeof(unsigned) * (2 * (size_t)(num_tiles > 0 ? num_tiles : 0) + 2);
 }
 
-extern "C" int gsvc_rasterize_sum_forward_slabs(
+static int forward_slabs_impl(
     int num_points, const float *xys, const int *radii, const float *conics, const float *colors,
     const float *opacities, const float *background, unsigned img_height, unsigned img_width,
     int call_index, int density_hint, void *workspace, size_t workspace_bytes,
     int *gaussian_ids, int *tile_bins, int *meta, float *grad_records_zero, float *out_img,
-    int *final_idx, void *stream) {
+    int *final_idx, void *stream, void *order_ws, size_t order_ws_bytes, int order_flags) {
     if (num_points < 0 || img_height == 0 || img_width == 0)
         return set_error(GSVC_ERR_ARG, "rasterize_sum_forward_slabs: bad sizes");
     const int tbx = ceil_div((int)img_width, kTile), tby = ceil_div((int)img_height, kTile);
@@ -1199,7 +1277,23 @@ extern "C" int gsvc_rasterize_sum_forward_slabs(
     const int par = call_index & 1;
     unsigned *counts = (unsigned *)workspace;
     int *m_slots = (int *)(counts + 2 * (size_t)ntiles);
-    if (num_points > 0) {
+    const bool ordered = order_ws && (order_flags & (GSVC_TRAIN_ORDER | GSVC_TRAIN_ORDER_REFRESH));
+    OpOrderWs ow{};
+    if (ordered) {
+        ow = op_order_ws((char *)order_ws, num_points);
+        if (order_ws_bytes < ow.bytes)
+            return set_error(GSVC_ERR_WORKSPACE, "rasterize_sum_forward_slabs_ordered: order workspace too small");
+    }
+    if (num_points > 0 && ordered) {
+        const bool refresh = (order_flags & GSVC_TRAIN_ORDER_REFRESH) != 0;
+        hipLaunchKernelGGL(tile_insert_ids_ordered_kernel, dim3(ceil_div(num_points, kProjThreads)),
+                           dim3(kProjThreads), 0, s, num_points,
+                           (order_flags & GSVC_TRAIN_ORDER) ? (const int *)ow.order : nullptr,
+                           (const float2 *)xys, radii, tbx, tby, counts + (size_t)par * ntiles,
+                           gaussian_ids, m_slots + par, m_slots + (par ^ 1),
+                           (float4 *)grad_records_zero, refresh ? ow.okey : nullptr,
+                           refresh ? ow.okey_id : nullptr, strip_key_invisible(tbx, tby));
+    } else if (num_points > 0) {
         hipLaunchKernelGGL(tile_insert_ids_kernel, dim3(ceil_div(num_points, kProjThreads)),
                            dim3(kProjThreads), 0, s, num_points, (const float2 *)xys, radii, tbx,
                            tby, counts + (size_t)par * ntiles, gaussian_ids, m_slots + par,
@@ -1231,7 +1325,45 @@ extern "C" int gsvc_rasterize_sum_forward_slabs(
     A.opac = opacities;
     A.out = out_img;
     A.final_idx = final_idx;
-    return sum_forward_launch(A, density_hint, s);
+    const int rc = sum_forward_launch(A, density_hint, s);
+    if (rc || !ordered || !(order_flags & GSVC_TRAIN_ORDER_REFRESH) || num_points <= 0) return rc;
+    // the next calls' order: splat ids by strip key (stable)
+    return sort_u32_pairs(num_points, ow.okey, ow.okey_id, ow.skey, ow.order, ow.kbuf, ow.vbuf,
+                          strip_key_bits(tbx, tby), ow.sort_counts, ow.sort_offsets, s);
+}
+
+extern "C" int gsvc_rasterize_sum_forward_slabs(
+    int num_points, const float *xys, const int *radii, const float *conics, const float *colors,
+    const float *opacities, const float *background, unsigned img_height, unsigned img_width,
+    int call_index, int density_hint, void *workspace, size_t workspace_bytes,
+    int *gaussian_ids, int *tile_bins, int *meta, float *grad_records_zero, float *out_img,
+    int *final_idx, void *stream) {
+    return forward_slabs_impl(num_points, xys, radii, conics, colors, opacities, background,
+                              img_height, img_width, call_index, density_hint, workspace,
+                              workspace_bytes, gaussian_ids, tile_bins, meta, grad_records_zero,
+                              out_img, final_idx, stream, nullptr, 0, 0);
+}
+
+extern "C" size_t gsvc_rasterize_sum_order_workspace_bytes(int num_points) {
+    return op_order_ws(nullptr, num_points).bytes;
+}
+
+extern "C" int gsvc_rasterize_sum_forward_slabs_ordered(
+    int num_points, const float *xys, const int *radii, const float *conics, const float *colors,
+    const float *opacities, const float *background, unsigned img_height, unsigned img_width,
+    int call_index, int density_hint, void *workspace, size_t workspace_bytes,
+    int *gaussian_ids, int *tile_bins, int *meta, float *grad_records_zero, float *out_img,
+    int *final_idx, void *stream, void *order_workspace, size_t order_workspace_bytes,
+    int order_flags) {
+    if (order_flags & ~(GSVC_TRAIN_ORDER | GSVC_TRAIN_ORDER_REFRESH))
+        return set_error(GSVC_ERR_ARG, "rasterize_sum_forward_slabs_ordered: unknown flags");
+    if (order_flags && !order_workspace)
+        return set_error(GSVC_ERR_WORKSPACE, "rasterize_sum_forward_slabs_ordered: no order workspace");
+    return forward_slabs_impl(num_points, xys, radii, conics, colors, opacities, background,
+                              img_height, img_width, call_index, density_hint, workspace,
+                              workspace_bytes, gaussian_ids, tile_bins, meta, grad_records_zero,
+                              out_img, final_idx, stream, order_workspace, order_workspace_bytes,
+                              order_flags);
 }
 
 extern "C" int gsvc_rasterize_sum_backward_zeroed_strided(

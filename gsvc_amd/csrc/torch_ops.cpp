@@ -27,6 +27,7 @@
 #include <torch/extension.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -171,7 +172,42 @@ struct SlabWs {
     Tensor buf;
     int tiles = -1;
     int calls = 0;
+    // the splat order of the id insertion (speed only): sorted by a refresh
+    // call for order_n splats, re-sorted every kOrderRefresh calls
+    Tensor order;
+    int order_n = -1, order_age = 0;
 };
+constexpr int kOrderRefresh = 64;  // as the training path's ORDER_REFRESH_EVERY
+
+// GSVC_OP_ORDER=0 turns the op path's splat order off (A/B)
+bool op_order_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("GSVC_OP_ORDER");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// GSVC_TRAIN_ORDER when ws holds an order for n splats, GSVC_TRAIN_ORDER_REFRESH
+// when it has none or it is kOrderRefresh calls old (train.py order_flags).
+int order_flags(SlabWs &ws, int n, const Tensor &like) {
+    if (!op_order_enabled() || n <= 0) return 0;
+    int flags = 0;
+    if (ws.order_n == n) {
+        flags |= GSVC_TRAIN_ORDER;
+        ++ws.order_age;
+    }
+    if (ws.order_n != n || ws.order_age >= kOrderRefresh) {
+        flags |= GSVC_TRAIN_ORDER_REFRESH;
+        if (ws.order_n != n) {
+            const size_t bytes = gsvc_rasterize_sum_order_workspace_bytes(n);
+            ws.order = at::empty({(int64_t)bytes}, like.options().dtype(at::kByte));
+        }
+        ws.order_n = n;
+        ws.order_age = 0;
+    }
+    return flags;
+}
 std::mutex g_ws_lock;
 std::vector<std::pair<std::pair<int, void *>, SlabWs>> g_ws;
 
@@ -220,12 +256,14 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
         Tensor meta = at::empty({2}, i), out = at::empty({H, W, 3}, f), idx = at::empty({H, W}, i);
         Tensor rec = need_grad ? at::empty({n, 16}, f) : Tensor();
         const int hint = hint_value(xys.device().index());  // M of an earlier call
-        check(gsvc_rasterize_sum_forward_slabs(
+        const int oflags = order_flags(ws, (int)n, xys);
+        check(gsvc_rasterize_sum_forward_slabs_ordered(
                   (int)n, fp(xys), ip(radii), fp(conics), fp(colors), fp(opacity), fp(background),
                   (unsigned)H, (unsigned)W, ws.calls++, hint, ws.buf.data_ptr(),
                   4 * (size_t)ws.buf.numel(), ip(gids), ip(bins), ip(meta), fp(rec), fp(out),
-                  ip(idx), st),
-              "gsvc_rasterize_sum_forward_slabs");
+                  ip(idx), st, oflags ? ws.order.data_ptr() : nullptr,
+                  oflags ? (size_t)ws.order.numel() : 0, oflags),
+              "gsvc_rasterize_sum_forward_slabs_ordered");
         hint_refresh(meta, st);
         Tensor m_dev = meta.narrow(0, 0, 1);
         ctx->save_for_backward({gids, bins, xys, conics, colors, opacity, idx});

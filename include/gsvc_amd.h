@@ -297,6 +297,21 @@ int gsvc_rasterize_sum_forward_slabs(
     unsigned img_height, unsigned img_width, int call_index, int density_hint,
     void *workspace, size_t workspace_bytes, int *gaussian_ids, int *tile_bins,
     int *meta, float *grad_records_zero, float *out_img, int *final_idx, void *stream);
+/* The same with a splat order for the id insertion (speed only; the same
+ * results): order_flags GSVC_TRAIN_ORDER inserts the splats in the order an
+ * earlier GSVC_TRAIN_ORDER_REFRESH call with this order_workspace and
+ * num_points sorted (by the tile strip of their centres), so a workgroup's
+ * slot atomics aggregate per tile; GSVC_TRAIN_ORDER_REFRESH sorts a new one
+ * from this call's xys.  order_workspace: gsvc_rasterize_sum_order_workspace_bytes
+ * (num_points) bytes, no initial contents.  Not part of the reference. */
+size_t gsvc_rasterize_sum_order_workspace_bytes(int num_points);
+int gsvc_rasterize_sum_forward_slabs_ordered(
+    int num_points, const float *xys, const int *radii, const float *conics,
+    const float *colors, const float *opacities, const float *background,
+    unsigned img_height, unsigned img_width, int call_index, int density_hint,
+    void *workspace, size_t workspace_bytes, int *gaussian_ids, int *tile_bins,
+    int *meta, float *grad_records_zero, float *out_img, int *final_idx, void *stream,
+    void *order_workspace, size_t order_workspace_bytes, int order_flags);
 /* gsvc_rasterize_sum_backward (backward.cu:696-862) into grad_records that
  * the caller has zeroed (gsvc_rasterize_sum_forward_slabs did): no memset. */
 int gsvc_rasterize_sum_backward_zeroed(
