@@ -210,3 +210,21 @@ def test_train_step_ahead_flag_errors_without_launch():
     a.adan_flags, a.grads_out = base | T.TRAIN_TILES_NEXT, dummy
     assert lib.gsvc_train_step_sum_args(ctypes.byref(a)) == 1
     assert b"Adan update" in lib.gsvc_last_error()
+
+
+def test_slabs_ordered_argument_errors_without_launch():
+    """gsvc_rasterize_sum_forward_slabs_ordered checks its order flags and
+    workspaces before any HIP call; the order workspace grows with the splat
+    count and has room for the sort's counters."""
+    from gsvc_amd import _lib
+    lib = _lib.load()
+    assert lib.gsvc_rasterize_sum_order_workspace_bytes(50000) >= 6 * 4 * 50000
+    assert lib.gsvc_rasterize_sum_order_workspace_bytes(1) > 0
+    args = [10, None, None, None, None, None, None, 64, 64, 0, 0, None, 0, None, None, None, None,
+            None, None, None]
+    assert lib.gsvc_rasterize_sum_forward_slabs_ordered(*args, None, 0, 0x1) == 1
+    assert b"unknown flags" in lib.gsvc_last_error()
+    assert lib.gsvc_rasterize_sum_forward_slabs_ordered(*args, None, 0, 0x200) == 2
+    assert b"order workspace" in lib.gsvc_last_error()
+    w = ctypes.c_void_p(16)  # never dereferenced: the slab workspace check fails first
+    assert lib.gsvc_rasterize_sum_forward_slabs_ordered(*args, w, 16, 0x200) == 2
