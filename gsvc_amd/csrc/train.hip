@@ -77,9 +77,14 @@ struct TrainTileArgs {
     // step to step (train_splat_kernel) -- and an entry is a candidate whose
     // current tile box cbox[id] holds the tile; records come from rec by id.
     // m_clear: the next frame's M slot (zeroed here; the splat kernel fills it)
-    const int *cids;
+    // csorted[tile]: how many leading cids are in id order (a rebuild zeroes it,
+    // the splat kernel's appends leave it behind the count); a tile of <= 64
+    // whose cids are all sorted ranks its entries by one ballot, and one that
+    // is not sorts them, writes them back and sets it
+    int *cids;
     const uint2 *cbox;
     int *m_clear;
+    unsigned *csorted;
 };
 
 __device__ __forceinline__ float clamp_unit(float x) {
@@ -737,6 +742,8 @@ struct BandLds {
     int misc[4];   // the waves' error sums
     int nsel;      // carried bins: the tile's entries among its candidates
 };
+// the order phase reads part row 0 as int4s (ids at [0, 64), candidates at [64, 128))
+static_assert(offsetof(BandLds, part) % 16 == 0, "BandLds.part must be 16-byte aligned");
 
 // kDet: GSVC_TRAIN_DETERMINISTIC's slot stores in place of the atomics (its
 // own instantiation: the slot arithmetic in the flush would cost the atomic
@@ -773,9 +780,10 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     constexpr bool carry = kCarry;
     const int m_frame = *A.m_dev;
     const unsigned cnt_raw = A.counts[tile];
+    const unsigned srt_raw = kCarry && A.csorted ? A.csorted[tile] : 0u;
     float4 r0, r1, r2;
     int cid = 0;  // carried bins: the lane's candidate id
-    const int *tcids = carry ? A.cids + (size_t)tile * kTilePix : nullptr;
+    int *tcids = carry ? A.cids + (size_t)tile * kTilePix : nullptr;
     if (carry) {
         cid = tcids[tid < spec_of(A) ? tid : 0];
     } else {
@@ -835,7 +843,11 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             }
             const int id = mem ? cid : 0x7fffffff;
             int rank = 0;
-            if (kDiag && (A.diag & 128)) {
+            const bool sorted = A.csorted && (int)__builtin_amdgcn_readfirstlane(srt_raw) == n;
+            if (sorted) {
+                // candidates in id order: a member's rank is the members below it
+                rank = __popcll(__ballot(mem) & ((1ull << lane) - 1ull));
+            } else if (kDiag && (A.diag & 128)) {
                 rank = rank_below(id, n);
             } else {
                 // rank by id with the ids through LDS (part row 0, free during the
@@ -848,6 +860,22 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                     const int4 q = *reinterpret_cast<const int4 *>(s_rid + k);
                     rank += (q.x < id ? 1 : 0) + (q.y < id ? 1 : 0) + (q.z < id ? 1 : 0) +
                             (q.w < id ? 1 : 0);
+                }
+                if (A.csorted) {
+                    // every candidate's place in id order (part row 0 past s_rid
+                    // as the scratch; the ids are unique), written back for later steps
+                    int *s_cid = reinterpret_cast<int *>(&S.part[0][0]) + 64;  // 16-byte aligned
+                    const int cv = lane < n ? cid : 0x7fffffff;
+                    s_cid[lane] = cv;
+                    wave_lds_sync();
+                    int place = 0;
+                    for (int k = 0; k < n; k += 4) {
+                        const int4 q = *reinterpret_cast<const int4 *>(s_cid + k);
+                        place += (q.x < cv ? 1 : 0) + (q.y < cv ? 1 : 0) + (q.z < cv ? 1 : 0) +
+                                 (q.w < cv ? 1 : 0);
+                    }
+                    if (lane < n) tcids[place] = cid;
+                    if (lane == 0) A.csorted[tile] = (unsigned)n;
                 }
             }
             if (mem) {
@@ -1656,7 +1684,7 @@ struct TrainWs {
     // GSVC_TRAIN_CARRY: per tile its candidate ids and their count, per splat
     // its current tile box and the hull of the boxes it is binned under
     int *cids;
-    unsigned *ccount;
+    unsigned *ccount, *csorted;  // csorted: TrainTileArgs.csorted, right after ccount
     uint2 *cbox, *chull;
     size_t bytes;
 };
@@ -1674,7 +1702,8 @@ static TrainWs train_ws(char *base, int n, int ntiles) {
     w.grad = (float4 *)take(sizeof(float4) * 4 * nn);
     w.err = (float2 *)take(sizeof(float2) * nt);
     w.cids = (int *)take(sizeof(int) * kTilePix * nt);
-    w.ccount = (unsigned *)take(sizeof(unsigned) * nt);
+    w.ccount = (unsigned *)take(sizeof(unsigned) * 2 * nt);  // ccount[T], csorted[T]
+    w.csorted = w.ccount ? w.ccount + nt : nullptr;
     w.cbox = (uint2 *)take(sizeof(uint2) * nn);
     w.chull = (uint2 *)take(sizeof(uint2) * nn);
     w.bytes = off;
@@ -1804,7 +1833,7 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
         if (carry) {
             // a new set of carried bins: counts and this frame's M from zero (a
             // previous step's splat kernel may have carried into them)
-            if (hipMemsetAsync(w.ccount, 0, sizeof(unsigned) * (size_t)ntiles, s) != hipSuccess ||
+            if (hipMemsetAsync(w.ccount, 0, sizeof(unsigned) * 2 * (size_t)ntiles, s) != hipSuccess ||
                 hipMemsetAsync(f.m_acc, 0, sizeof(int), s) != hipSuccess)
                 return set_error(GSVC_ERR_HIP, "train_step_sum: memset failed");
         }
@@ -1865,6 +1894,9 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     if (carry) {
         T.cids = w.cids;
         T.cbox = w.cbox;
+        // (zeroed with ccount whenever the bins are rebuilt; A/B knob 28 = 1: no
+        // sorted lists -- every step ranks, nothing is written back)
+        T.csorted = knob(28) == 1 ? nullptr : w.csorted;
     }
     // the tile kernel of the frame whose slots are fs
     auto launch_tiles = [&](const FrameSlots &fs) {
@@ -1995,7 +2027,7 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
             // the splat kernel's carry is superseded: counts and M from zero,
             // then the projection bins frame_index + 1 afresh (and re-zeroes the
             // gradient records)
-            if (hipMemsetAsync(w.ccount, 0, sizeof(unsigned) * (size_t)ntiles, s) != hipSuccess ||
+            if (hipMemsetAsync(w.ccount, 0, sizeof(unsigned) * 2 * (size_t)ntiles, s) != hipSuccess ||
                 hipMemsetAsync(fn.m_acc, 0, sizeof(int), s) != hipSuccess)
                 return set_error(GSVC_ERR_HIP, "train_step_sum: memset failed");
             rc = frame_project_launch(num_points, xyz, 1, cholesky, cholesky_bound, features, rgb_w,
