@@ -309,6 +309,105 @@ def cpu_baseline(n_splats, reps=5, warm=2):
                       "over tiles, numpy clamp/L2/Adan)"}
 
 
+def _cpu_cores():
+    """This process's CPU share: the affinity mask, capped by OMP_NUM_THREADS
+    (the GPU box grants 16 CPUs per GPU while its mask shows the machine)."""
+    cores = len(os.sched_getaffinity(0))
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        cores = min(cores, max(1, int(os.environ["OMP_NUM_THREADS"])))
+    return cores
+
+
+def _median_s(fn, reps, warm):
+    ts = []
+    for _ in range(warm + reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    ts = sorted(ts[warm:])
+    return ts[len(ts) // 2]
+
+
+def cpu_render_baseline(means, L, colors, H_, W_, label, reps=5, warm=2, backward=False):
+    """The CPU baselines of one frame render (BASELINE.md §4 protocol, SURVEY
+    §8d; the FPS loop of train_video_Represent.py:101-106): the oracle
+    restatement (oracle/oracle.py render_sum: C project / bin / sum-raster,
+    numpy glue; kind "port") and this package's own CPU dispatch of the two
+    operators (gsplat.project_gaussians_2d + rasterize_gaussians_sum on CPU
+    tensors, libgsvc_amd_cpu.so: the reference's "PyTorch-CPU fallback"
+    config), each at k = 1 and k = all cores, median of ``reps`` frames after
+    ``warm`` warm-ups.  Inputs: activated means2d [N,2], L [N,3], colours
+    [N,3] (CPU float32).  ``backward``: also forward + backward of the CPU
+    dispatch (v_out = ones)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    from gsvc_amd import cpu as C
+    from gsplat.project_gaussians_2d import project_gaussians_2d
+    from gsplat.rasterize_sum import rasterize_gaussians_sum
+    n = means.shape[0]
+    mn, Ln, cn = (np.ascontiguousarray(t.numpy(), dtype=np.float32) for t in (means, L, colors))
+    on = np.ones((n, 1), np.float32)
+    tb = ((W_ + 15) // 16, (H_ + 15) // 16, 1)
+    ones = torch.ones(n, 1)
+    bg = torch.ones(3)
+
+    def product_fwd():
+        xys, depths, radii, conics, nth = project_gaussians_2d(means, L, H_, W_, tb)
+        rasterize_gaussians_sum(xys, depths, radii, conics, nth, colors, ones, H_, W_, 16, 16,
+                                background=bg)
+
+    def product_fwd_bwd():
+        m, l, c = (t.clone().requires_grad_(True) for t in (means, L, colors))
+        xys, depths, radii, conics, nth = project_gaussians_2d(m, l, H_, W_, tb)
+        out = rasterize_gaussians_sum(xys, depths, radii, conics, nth, c, ones, H_, W_, 16, 16,
+                                      background=bg)
+        out.sum().backward()
+
+    cores = _cpu_cores()
+    per = {"oracle": {}, "product_cpu": {}}
+    if backward:
+        per["product_cpu_fwd_bwd"] = {}
+    torch_threads = torch.get_num_threads()
+    for k in sorted({1, cores}):
+        O.set_threads(k)
+        C.set_threads(k)
+        torch.set_num_threads(k)
+        per["oracle"][str(k)] = round(1.0 / _median_s(lambda: O.render_sum(mn, Ln, cn, on, H_, W_),
+                                                      reps, warm), 3)
+        with torch.no_grad():
+            per["product_cpu"][str(k)] = round(1.0 / _median_s(product_fwd, reps, warm), 3)
+        if backward:
+            per["product_cpu_fwd_bwd"][str(k)] = round(1.0 / _median_s(product_fwd_bwd, reps, warm), 3)
+    O.set_threads(1)
+    C.set_threads(cores)
+    torch.set_num_threads(torch_threads)
+    best_k = max(per["oracle"], key=per["oracle"].get)
+    return {"value": per["oracle"][best_k], "unit": "frames/s", "cores": int(best_k), "kind": "port",
+            "cpu_model": _cpu_model(), "per_path_per_cores": per,
+            "sample": f"median of {reps} renders after {warm} warm-ups per path and core count, "
+                      f"{label}: {W_}x{H_}, {n} splats; value = the oracle restatement "
+                      "(oracle/oracle.py render_sum: C project/bin/sum-raster, numpy glue); "
+                      "product_cpu = gsplat ops on CPU tensors (libgsvc_amd_cpu.so, OpenMP)"}
+
+
+def config0_cpu(reps=5, warm=2):
+    """BASELINE configs[0]: a single 256x256 synthetic frame, 1k splats, on the
+    CPU (the reference's PyTorch-CPU rasterize case): forward and forward +
+    backward through the operators' CPU dispatch, and the oracle."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    means, L, colors, _ = O.synthetic_frame(1000, 0)
+    r = cpu_render_baseline(torch.from_numpy(np.ascontiguousarray(means, np.float32)),
+                            torch.from_numpy(np.ascontiguousarray(L, np.float32)),
+                            torch.from_numpy(np.ascontiguousarray(colors, np.float32)),
+                            256, 256, "BASELINE configs[0] (synthetic frame, seed 0)", reps, warm,
+                            backward=True)
+    r["workload"] = "BASELINE configs[0]: one 256x256 frame, 1k splats, CPU only"
+    return r
+
+
 def psnr_vs_ref(device):
     """Run the reference trajectory's iterations (same seed, init, target) on
     the fused path and compare per-iteration PSNR with the reference's CPU run."""
@@ -375,11 +474,16 @@ def render_block(model, steps, warmup):
             "project_avg_us": round(_avg(times["project"]) * 1e3, 2), "shape": shape}
 
 
-def render_10k(device, steps=200, warmup=20):
-    """configs[1]: render one 1920x1080 frame of 10k splats."""
+def render10k_model(device):
     from gsvc_amd.frame import make_frame_model
     model = make_frame_model(H, W, 10000, device, seed=1000)
     model.eval()
+    return model
+
+
+def render_10k(device, steps=200, warmup=20):
+    """configs[1]: render one 1920x1080 frame of 10k splats."""
+    model = render10k_model(device)
     r = render_block(model, steps, warmup)
     r["workload"] = r["workload"].replace("(configs[2] render)", "(configs[1])")
     return r
@@ -429,13 +533,13 @@ def op_path_block(model, gt, device, steps=200, warmup=20):
     bench's trained frame (fresh optimizer state, as a P-frame starts).
     ``train_iters_per_s`` uses gsvc_amd.adan.Adan (one fused update kernel);
     ``train_iters_per_s_foreach_adan`` the reference optimizer's own foreach
-    sequence (tests/adan_checker.py, op for op optimizer.py:296-362), i.e.
+    sequence (tools/foreach_adan.py, op for op optimizer.py:296-362), i.e.
     GSVC's files with nothing changed but the gsplat package."""
     import math
     import torch.nn.functional as F
     from gsvc_amd.frame import make_frame_model
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    from adan_checker import ForeachAdan
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from foreach_adan import ForeachAdan
     n = model._xyz.shape[0]
     op = make_frame_model(H, W, n, device, seed=0, fused_train=False, fused_render=False)
     with torch.no_grad():
@@ -653,6 +757,18 @@ def main():
         line["op_path"] = op_path_block(model, gt, device)
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args.splats)
+        if "render" in line:  # configs[2] render and configs[1]: the same frames on the CPU
+            with torch.no_grad():
+                line["render"]["cpu_baseline"] = cpu_render_baseline(
+                    model.get_xyz.detach().cpu(), model.get_cholesky_elements.detach().cpu(),
+                    model.get_features.detach().cpu().contiguous(), H, W,
+                    "the bench's trained configs[2] frame")
+                m10 = render10k_model(device)
+                line["render_10k"]["cpu_baseline"] = cpu_render_baseline(
+                    m10.get_xyz.detach().cpu(), m10.get_cholesky_elements.detach().cpu(),
+                    m10.get_features.detach().cpu().contiguous(), H, W,
+                    "configs[1]'s frame (random init, seed 1000)")
+        line["config0_cpu"] = config0_cpu()
     print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -141,7 +141,7 @@ _RESTYPE = {
     "gsvc_ssim_backward_scratch_bytes": _SZ,
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _libs = {}       # path -> loaded CDLL
 _active = None   # the library ops call (load())

@@ -28,6 +28,7 @@ TILE_KEEP = 256
 _P, _I, _U = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint
 _SIGS = {
     "gsvc_cpu_abi_version": ([], _I),
+    "gsvc_cpu_set_threads": ([_I], _I),
     "gsvc_cpu_project_gaussians_2d_forward": ([_I, _P, _P, _U, _U, _I, _I, _P, _P, _P, _P, _P],
                                               ctypes.c_longlong),
     "gsvc_cpu_project_gaussians_2d_backward": ([_I, _P, _U, _U, _P, _P, _P, _P, _P, _P, _P], None),
@@ -54,6 +55,11 @@ def lib():
                     fn.restype = res
                 _lib = h
     return _lib
+
+
+def set_threads(n: int) -> int:
+    """OpenMP threads of the CPU dispatch (results do not depend on it)."""
+    return int(lib().gsvc_cpu_set_threads(int(n)))
 
 
 def _p(t):

@@ -31,6 +31,9 @@ constexpr unsigned kSigmaCutBits = 0x40b15208u;  // sigma 5.5412636 (gfx950 v_ex
 // Host-side error plumbing -------------------------------------------------
 int set_error(int code, const char *fmt, ...);
 int check_launch(const char *what);
+// GSVC_ERR_CAPTURE when stream s is capturing a graph (entries with host-indexed
+// workspace parity; include/gsvc_amd.h conventions), else GSVC_OK
+int refuse_capture(hipStream_t s, const char *what);
 // A/B knobs and diagnostic kernel variants exist only in the diagnostic
 // library (built with -DGSVC_DIAG: libgsvc_amd_diag.so, include/gsvc_amd_diag.h,
 // for tools/ and the variant-comparison tests).  In the product library every
@@ -51,7 +54,8 @@ constexpr void *debug_ptr() { return nullptr; }
 // timing.hip: slot, or -1 when not recording; dispatch_ev[2] = the events the
 // launch must carry itself (hipExtLaunchKernel), both null otherwise
 constexpr int kTimingComposite = 0, kTimingTrainTile = 1, kTimingProject = 2,
-              kTimingTrainSplat = 3, kTimingChannels = 4;
+              kTimingTrainSplat = 3, kTimingSumBwd = 4, kTimingAlphaFwd = 5, kTimingAlphaBwd = 6,
+              kTimingChannels = 7;
 int timing_begin(hipStream_t s, hipEvent_t *dispatch_ev, int channel = kTimingComposite);
 void timing_end(hipStream_t s, int slot, int channel = kTimingComposite);
 

@@ -18,6 +18,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <omp.h>
+
 #include <algorithm>
 #include <vector>
 
@@ -58,6 +60,13 @@ float sigma_of(float ha, float b, float hc, float dx, float dy) {
 extern "C" {
 
 int gsvc_cpu_abi_version(void) { return 1; }
+
+// OpenMP threads of this library's loops (results do not depend on it; the
+// bench's k = 1 / all-cores CPU baselines).  Returns the count in effect.
+int gsvc_cpu_set_threads(int n) {
+    omp_set_num_threads(n > 0 ? n : 1);
+    return omp_get_max_threads();
+}
 
 // foward2d.cu:12-69 for every splat; returns M = the sum of num_tiles_hit.
 long long gsvc_cpu_project_gaussians_2d_forward(int n, const float *means2d, const float *L,

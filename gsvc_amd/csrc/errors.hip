@@ -27,6 +27,15 @@ int check_launch(const char *what) {
     return GSVC_OK;
 }
 
+int refuse_capture(hipStream_t s, const char *what) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    // (a failing query -- e.g. no device -- is left to the launches to report)
+    if (hipStreamIsCapturing(s, &st) != hipSuccess || st == hipStreamCaptureStatusNone) return GSVC_OK;
+    return set_error(GSVC_ERR_CAPTURE,
+                     "%s cannot be captured in a graph: its workspace alternates parity slots indexed "
+                     "by the host's call counter, which a replay would not advance", what);
+}
+
 #ifdef GSVC_DIAG
 int g_knobs[kKnobs] = {};
 void *g_debug_ptr = nullptr;
@@ -34,7 +43,7 @@ void *g_debug_ptr = nullptr;
 
 }  // namespace gsvc
 
-extern "C" int gsvc_abi_version(void) { return 1; }
+extern "C" int gsvc_abi_version(void) { return GSVC_ABI_VERSION; }
 
 #ifdef GSVC_DIAG
 // include/gsvc_amd_diag.h: the diagnostic library only

@@ -195,7 +195,9 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_ordered_kernel(
     if (kStamp && lane == 0) st[0] = proj_stamp();
     if (blockIdx.x == 0 && tid == 0) *m_clear = 0;  // the next frame's slot
     const int i = t < n ? (order ? order[t] : t) : n;  // order NULL: identity
-    const bool have = i < n;
+    // unsigned: an order entry outside [0, n) (a buffer never sorted) projects
+    // nothing instead of indexing before the arrays (round-4 fault)
+    const bool have = (unsigned)i < (unsigned)n;
     SplatOut S;
     S.P.rad = 0;
     unsigned x0 = 0, y0 = 0, x1 = 0, y1 = 0;
@@ -396,6 +398,8 @@ using namespace gsvc;
 
 namespace gsvc {
 
+constexpr int kPlainProjMaxPerTile = 8;
+
 // The one-call render of ``frames`` frames (frame b: splats [frame_off[b],
 // frame_off[b + 1]), image out + b * 3HW); frames == 1: splats [0, n).
 static int render_frames(int frames, const int *frame_off_host, const int *frame_off_dev,
@@ -411,6 +415,7 @@ static int render_frames(int frames, const int *frame_off_host, const int *frame
     if (!workspace || workspace_bytes < w.bytes)
         return set_error(GSVC_ERR_WORKSPACE, "render_frame_sum: workspace too small (%zu < %zu)",
                          workspace_bytes, w.bytes);
+    if (const int rc = refuse_capture(s, frames > 1 ? "render_frames_sum" : "render_frame_sum")) return rc;
     int max_n = num_points;
     if (frames > 1) {
         max_n = 0;
@@ -440,10 +445,20 @@ static int render_frames(int frames, const int *frame_off_host, const int *frame
     if (!sum_forward_dense(density_hint, ntiles, frames) && knob(24) != 1 &&
         (frames == 1 || knob(25) == 1))  // A/B knob 25 = 1: batched frames too
         id_slab = reinterpret_cast<int *>(w.slab);
+    // A sparse single frame (<= kPlainProjMaxPerTile entries per tile by the
+    // hint) projects in id order with plain paired atomics: the windowed
+    // atomics pay only where tiles are dense (fbench at 1080p / 10k: 6.7 vs
+    // 7.9-8.4 us).  A refresh call still takes the ordered kernel, which writes
+    // the strip keys its sort reads -- a refresh whose projection skipped them
+    // sorted uninitialised keys and ids into the order, and the next ordered
+    // call gathered splats through it (the round-4 fault).  Knob 27
+    // = 1 keeps the order at any density (A/B).
+    const bool plain = use_order && !refresh && knob(27) != 1 &&
+                       (long long)density_hint <= (long long)kPlainProjMaxPerTile * ntiles;
     int rc = frame_project_launch(num_points, xyz, xyz_tanh, cholesky, cholesky_bound, features,
                                   rgb_w, opacity, img_height, img_width, w, f, nullptr, s, frames,
-                                  frame_off_dev, max_n, (use_order || refresh) ? &ord : nullptr,
-                                  id_slab);
+                                  frame_off_dev, max_n,
+                                  ((use_order && !plain) || refresh) ? &ord : nullptr, id_slab);
     if (rc) return rc;
     SumFwdArgs A;
     sum_fwd_args_init(A);

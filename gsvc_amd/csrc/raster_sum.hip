@@ -45,6 +45,7 @@
 #include "frame.h"
 #include "frame_dev.h"
 #include "raster_sum.h"
+#include "rows.h"
 #include "tile_ids.h"
 
 namespace gsvc {
@@ -674,7 +675,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
     // id slabs: the op path's autograd forward (kIdx) and the render A/B mode
     constexpr bool kIds = kIdx || kMode == kModeSparseIds;
     __shared__ float4 s_buf[kOneWave ? 1 : 2][kSlice];
-    __shared__ int s_ids[kOneWave ? 1 : 2][kTilePix];
+    __shared__ int s_ids[1][kTilePix];  // the tile's sorted ids (one copy per tile)
     // raised wave priority over the staging (loads, ranking, lists): the
     // arbiter favours older waves, so a young wave would otherwise wait behind
     // its elders' blending to issue its round trips (train.hip, same reason)
@@ -791,13 +792,24 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
                                     seg.head, spec0, spec1, spec2, seg.head ? A.spec_slots : 0,
                                     spec_id);
     } else {
+        if (by_ids) {
+            // ONE sort per tile, by wave 0, shared by both waves through LDS:
+            // with id slabs wave 0 writes the sorted ids back over the very
+            // slots a second sorting wave would still be reading
+            __shared__ int s_n;
+            if (w == 0) {
+                const int ns = ((A.slab || (kIds && A.id_counts)) && n_all > kTilePix)
+                                   ? wave_brute_tile_ids(A, tile, s_ids[0])
+                                   : wave_sorted_tile_ids(seg, n_all, s_ids[0],
+                                                          reinterpret_cast<unsigned *>(s_buf[0]));
+                if ((threadIdx.x & 63) == 0) s_n = ns;
+            }
+            __syncthreads();
+            n = s_n;
+            if (kIdx && A.id_counts && w == 0) write_sorted_ids(A, tile, range.x, n, s_ids[0]);
+        }
         if (ty * kTile + w * 8 >= A.img_h) return;  // band below the image
-        if (by_ids)
-            n = ((A.slab || (kIds && A.id_counts)) && n_all > kTilePix)
-                    ? wave_brute_tile_ids(A, tile, s_ids[w])
-                    : wave_sorted_tile_ids(seg, n_all, s_ids[w], reinterpret_cast<unsigned *>(s_buf[w]));
-        if (kIdx && A.id_counts && w == 0) write_sorted_ids(A, tile, range.x, n, s_ids[0]);
-        sum_fwd_band<kMode, kIdx>(A, tile, w, range, n, s_buf[w], init, by_ids, s_ids[w], seg_rec,
+        sum_fwd_band<kMode, kIdx>(A, tile, w, range, n, s_buf[w], init, by_ids, s_ids[0], seg_rec,
                                   seg.head, spec0, spec1, spec2);
     }
     if (kMode == kModeStamp && (threadIdx.x & 63) == 0) {
@@ -823,7 +835,245 @@ __host__ __device__ inline VStrides hwc_strides(unsigned img_w) {
 // det_off (deterministic backward, det.h): each (splat, tile) sum goes to
 // det_part[9 * slot ...] instead of the record's atomics (slots past det_cap:
 // atomics); det_radii: the splats' radii for the slot's bbox.
-__global__ __launch_bounds__(256) void raster_sum_bwd_kernel(
+//
+// Backward (backward.cu:696-862), round 5: a 128-thread workgroup (two waves)
+// per tile, each wave over the rectangle rows of its own 8-row band -- the
+// training tile kernel's per-row work items (rows.h).  Per chunk of 64 of the
+// tile's first <= 256 sorted entries: the entries' records gathered by id
+// with their alpha >= 1/255 rectangle of tile pixels (ellipse_rect: a pair
+// outside contributes nothing in the reference either); work items = one
+// rectangle row of an entry in the band, laid out longest first; each lane
+// walks its item's pixels accumulating the row sums S_k = sum v_sigma dx^k
+// (k = 0, 1, 2: v_xy and v_conic factor by the row's constant dy), the colour
+// sums alpha * v_out and v_opacity = sum vis * v_alpha; a DPP segmented scan
+// adds an entry's items in a fixed tree order and the run's last lane adds the
+// run into the entry's LDS sums (fixed order, no LDS atomics); the two bands'
+// sums go to the splat's record with one 9-lane atomic request per (splat,
+// tile).  final_idx bounds no sum: an entry past a pixel's final_idx fails the
+// alpha test there in the forward's own op sequence (that is what final_idx
+// records), so the reference's k > final_idx skip is implied; entries past the
+// tile's 256th are skipped as there (final_idx < range.x + 256).
+// Round 4's entry-per-thread kernel (each thread looping over E pixels with
+// the skip, 9 block reductions per entry) is raster_sum_bwd_kernel_r4 below,
+// in the diagnostic library only (A/B knob 29 = 1).
+constexpr int kSBChunk = 64;
+constexpr int kSBThreads = 128;
+struct SumBwdLds {
+    float v[3][kTile * kVRow];          // v_out planes (rows padded to kVRow words)
+    float4 geo[kSBChunk];               // x, y, a/2, b
+    float4 col[kSBChunk];               // c/2, opacity, r, g
+    float blu[kSBChunk];                // b
+    unsigned short ro[kSBChunk];        // alpha >= 1/255 rectangle (ellipse_rect)
+    int gid[kSBChunk];                  // splat id
+    float part[2][9][kSBChunk];         // per wave: the entries' 9 sums of its band
+    signed char own[kSBThreads];        // per wave: the entry of the round's first items
+    signed char perm[kSBThreads];       // per wave: the chunk's entries by item length
+};
+
+__global__ __launch_bounds__(kSBThreads, 8) void raster_sum_bwd_kernel(
+    int tbx, int img_w, int img_h, int ntiles, const int *__restrict__ ids,
+    const int2 *__restrict__ bins, const float2 *__restrict__ xys, const float *__restrict__ conics,
+    const float *__restrict__ colors, const float *__restrict__ opac,
+    const int *__restrict__ final_idx, const float *__restrict__ v_out, VStrides vs,
+    float *__restrict__ grad, const int *__restrict__ det_off, const int *__restrict__ det_radii,
+    float *__restrict__ det_part, long long det_cap) {
+    (void)final_idx;
+    __shared__ SumBwdLds S;
+    const int tile = xcd_remap(blockIdx.x, ntiles);
+    const int ty = tile / tbx, tx = tile - ty * tbx;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
+    const int2 range = bins[tile];
+    const int n = min(max(range.y - range.x, 0), kTilePix);
+    // the lane's pixel pair of its band: v_out into the planes (0 outside the
+    // image, where no item reaches)
+    {
+        const int prow = 8 * w + (lane >> 3), pcol = (lane & 7) << 1;
+        const int pi = ty * kTile + prow, pj = tx * kTile + pcol;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            float a = 0.f, b = 0.f, c = 0.f;
+            if (n > 0 && pi < img_h && pj + q < img_w) {
+                const float *v = v_out + (long long)pi * vs.h + (long long)(pj + q) * vs.w;
+                a = v[0];
+                b = v[vs.c];
+                c = v[2 * vs.c];
+            }
+            S.v[0][prow * kVRow + pcol + q] = a;
+            S.v[1][prow * kVRow + pcol + q] = b;
+            S.v[2][prow * kVRow + pcol + q] = c;
+        }
+    }
+    if (n == 0) return;  // (block-uniform)
+    const int y_lo = 8 * w, y_hi = 8 * w + 7;
+    float *eacc = &S.part[w][0][0];
+    signed char *wown = S.own + w * 64;
+    signed char *wperm = S.perm + w * 64;
+    const int tby = (img_h + kTile - 1) / kTile;
+    for (int c0 = 0; c0 < n; c0 += kSBChunk) {
+        const int gn = min(kSBChunk, n - c0);
+        __syncthreads();  // the previous chunk's flush has read the staging
+        if (tid < gn) {
+            const int g = ids[range.x + c0 + tid];
+            const float2 xy = xys[g];
+            const float a = conics[3 * g], b = conics[3 * g + 1], c = conics[3 * g + 2];
+            const float o = opac[g];
+            S.geo[tid] = make_float4(xy.x, xy.y, 0.5f * a, b);
+            S.col[tid] = make_float4(0.5f * c, o, colors[3 * g], colors[3 * g + 1]);
+            S.blu[tid] = colors[3 * g + 2];
+            S.gid[tid] = g;
+            S.ro[tid] = (unsigned short)ellipse_rect(xy.x, xy.y, a, b, c, o, tx0, ty0);
+        }
+        __syncthreads();
+        // work items of entry `lane` in this band: one per rectangle row
+        int items = 0, ilen = 0;
+        unsigned rc = kNoRect;
+        if (lane < gn) {
+            rc = S.ro[lane];
+            if (rc != kNoRect) {
+                const int ry0 = max((int)((rc >> 8) & 15u), y_lo), ry1 = min((int)((rc >> 12) & 15u), y_hi);
+                if (ry0 <= ry1) {
+                    items = ry1 - ry0 + 1;
+                    ilen = (int)((rc >> 4) & 15u) - (int)(rc & 15u) + 1;
+                }
+            }
+        }
+        // the entries' items laid out longest first (four length classes, entry
+        // order within a class): a round's 64 items have similar pixel loops;
+        // each entry's items stay together, in row order
+        {
+            const unsigned long long below = (1ull << lane) - 1ull;
+            int rank = 0, seen = 0;
+            unsigned long long left = __ballot(true);
+            const int cls = ilen >= 9 ? 3 : (ilen >= 7 ? 2 : (ilen >= 5 ? 1 : 0));
+            for (int L = 3; L >= 0 && left; --L) {
+                const unsigned long long m = __ballot(cls == L);
+                if (cls == L) rank = seen + __popcll(m & below);
+                seen += __popcll(m);
+                left &= ~m;
+            }
+            wperm[rank] = (signed char)lane;
+        }
+        __builtin_amdgcn_wave_barrier();
+        // unit opacity and bounded geometry for the whole chunk (GSVC's frames):
+        // the alpha cut as the sigma threshold (common.h kSigmaCutBits)
+        bool ok = true;
+        if (lane < gn) {
+            const float4 G = S.geo[lane], C = S.col[lane];
+            ok = C.y == 1.0f && geo_bounded(G.x, G.y, G.z, G.w, C.x);
+        }
+        const bool bcut = __ballot(!ok) == 0ull;
+        const int ent = wperm[lane];  // the entry in sorted slot `lane`
+        const int sitems = __shfl(items, ent, 64);
+        const int incl = wave_scan_dpp<false>(sitems, 0);
+        const int off = incl - sitems;  // sorted slot `lane`'s first item
+        const int total = __builtin_amdgcn_readlane(incl, 63);
+#pragma unroll
+        for (int c = 0; c < 9; ++c) eacc[c * kSBChunk + lane] = 0.0f;
+        for (int base = 0; base < total; base += 64) {
+            // the entry of item base + lane: the last entry whose first item is <= it
+            wown[lane] = -1;
+            __builtin_amdgcn_wave_barrier();
+            if (sitems > 0 && off >= base && off < base + 64) wown[off - base] = (signed char)lane;
+            const int straddle = __popcll(__ballot(lane < gn && off <= base)) - 1;
+            __builtin_amdgcn_wave_barrier();
+            int slot = max((int)wown[lane], straddle);
+            slot = wave_scan_dpp<true>(slot, -2147483647 - 1);  // sorted slot of item base + lane
+            const int item = base + lane;
+            const int own = __shfl(ent, slot, 64);
+            const int eoff = __shfl(off, slot, 64);
+            const unsigned ro = (unsigned)__shfl((int)rc, own, 64);
+            float g[9];
+#pragma unroll
+            for (int c = 0; c < 9; ++c) g[c] = 0.0f;
+            if (item < total) {
+                const float4 G = S.geo[own], C = S.col[own];
+                const float bl = S.blu[own];
+                const int row = max((int)((ro >> 8) & 15u), y_lo) + (item - eoff);
+                const int cs = (int)(ro & 15u);
+                const int ce = min((int)((ro >> 4) & 15u), img_w - 1 - (int)tx0);
+                const float pyf = ty0 + (float)row;
+                if ((int)pyf < img_h) {
+                    const float dy = G.y - pyf;
+                    const float cq = (C.x * dy) * dy;  // splat_sigma_h's row terms
+                    const float bdy = G.w * dy;
+                    // dy is constant along the row, so the per-pixel sums of
+                    // backward.cu:822-848 factor: v_conic = 1/2 (S2, dy S1, dy^2 S0),
+                    // v_xy = (a S1 + b dy S0, b S1 + c dy S0), S_k = sum v_sigma dx^k
+                    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+                    const float *vp = &S.v[0][0] + row * kVRow + cs;
+                    const float *const ve = &S.v[0][0] + row * kVRow + ce;
+                    float px = tx0 + (float)cs;
+                    auto walk = [&](auto kcut) {
+                        for (; vp <= ve; ++vp, px += 1.0f) {
+                            const float Px = vp[0], Py = vp[kTile * kVRow], Pz = vp[2 * kTile * kVRow];
+                            const float dx = G.x - px;  // the forward's own dx
+                            const float sgm = fmaf(fmaf(G.z, dx, bdy), dx, cq);
+                            const float vis = exp_neg(sgm);
+                            float al;
+                            if constexpr (decltype(kcut)::value) {
+                                if (__float_as_uint(sgm) > kSigmaCutBits) continue;
+                                al = vis;  // opacity 1
+                            } else {
+                                al = fminf(1.0f, C.y * vis);
+                                if (sgm < 0.0f || al < kAlphaMin) continue;
+                            }
+                            const float v_alpha = fmaf(bl, Pz, fmaf(C.w, Py, C.z * Px));
+                            const float v_sigma = (-C.y * vis) * v_alpha;
+                            g[5] = fmaf(al, Px, g[5]);
+                            g[6] = fmaf(al, Py, g[6]);
+                            g[7] = fmaf(al, Pz, g[7]);
+                            g[8] = fmaf(vis, v_alpha, g[8]);
+                            s0 += v_sigma;
+                            const float vdx = v_sigma * dx;
+                            s1 += vdx;
+                            s2 = fmaf(vdx, dx, s2);
+                        }
+                    };
+                    if (bcut)
+                        walk(std::true_type{});
+                    else
+                        walk(std::false_type{});
+                    const float hdy = 0.5f * dy;
+                    g[0] = fmaf(2.0f * G.z, s1, bdy * s0);
+                    g[1] = fmaf(G.w, s1, ((2.0f * C.x) * dy) * s0);
+                    g[2] = 0.5f * s2;
+                    g[3] = hdy * s1;
+                    g[4] = (hdy * dy) * s0;
+                }
+            }
+            // an entry has at most 8 rows in a band: runs of <= 8 lanes
+            wave_seg_sums<9, false>(g, own);
+            const int own_next = __shfl_down(own, 1, 64);
+            if (item < total && (lane == 63 || item + 1 == total || own_next != own)) {
+#pragma unroll
+                for (int c = 0; c < 9; ++c) eacc[c * kSBChunk + own] += g[c];
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        __syncthreads();
+        // 16 lanes per entry, 9 of them add band 0 + band 1 of one sum into the
+        // splat's 64-byte record: one memory request per (splat, tile)
+        for (int q = tid; q < gn * 16; q += kSBThreads) {
+            const int e = q >> 4, c = q & 15;
+            if (c >= 9) continue;
+            const float v = S.part[0][c][e] + S.part[1][c][e];
+            if (det_off) {
+                const long long slot = det_slot(det_off, xys, det_radii, S.gid[e], tx, ty, tbx, tby);
+                if (slot < det_cap) {
+                    det_part[9 * slot + c] = v;
+                    continue;
+                }
+            }
+            unsafeAtomicAdd(grad + (size_t)S.gid[e] * 16 + c, v);
+        }
+    }
+}
+
+#ifdef GSVC_DIAG
+// Round 4's op-path backward (diagnostic library, A/B knob 29 = 1): one
+// 256-thread workgroup per tile, entry-parallel (below).
+__global__ __launch_bounds__(256) void raster_sum_bwd_kernel_r4(
     int tbx, int img_w, int img_h, int ntiles, const int *__restrict__ ids,
     const int2 *__restrict__ bins, const float2 *__restrict__ xys, const float *__restrict__ conics,
     const float *__restrict__ colors, const float *__restrict__ opac,
@@ -963,6 +1213,8 @@ __global__ __launch_bounds__(256) void raster_sum_bwd_kernel(
     }
 }
 
+#endif
+
 // Deterministic backward: splat i's record = its slots summed in bbox order +
 // the atomics of slots past det_cap (zero unless the capacity was short).
 __global__ __launch_bounds__(256) void det_gather_kernel(int n, const int *__restrict__ off,
@@ -1046,13 +1298,14 @@ __global__ __launch_bounds__(kProjThreads) void tile_insert_ids_ordered_kernel(
     const int t = blockIdx.x * kProjThreads + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x == 0) *m_clear = 0;  // the next call's M
     const int i = t < n ? (order ? order[t] : t) : n;
+    const bool have = (unsigned)i < (unsigned)n;  // (an unsorted order buffer: nothing)
     SplatOut S;
     S.P.xy = make_float2(0.f, 0.f);
     S.P.rad = 0;
     S.r0 = S.r1 = make_float4(0.f, 0.f, 0.f, 0.f);
     S.r2 = make_float4(0.f, __int_as_float(i), 0.f, 0.f);  // the id (slab_insert_window's ids)
     unsigned x0 = 0, y0 = 0, x1 = 0, y1 = 0;
-    if (i < n) {
+    if (have) {
         if (rec_zero) {
             const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -1274,6 +1527,7 @@ static int forward_slabs_impl(
         (num_points > 0 && (!xys || !radii || !conics || !colors || !opacities)))
         return set_error(GSVC_ERR_ARG, "rasterize_sum_forward_slabs: missing input");
     hipStream_t s = (hipStream_t)stream;
+    if (const int rc = refuse_capture(s, "rasterize_sum_forward_slabs")) return rc;
     const int par = call_index & 1;
     unsigned *counts = (unsigned *)workspace;
     int *m_slots = (int *)(counts + 2 * (size_t)ntiles);
@@ -1366,6 +1620,31 @@ extern "C" int gsvc_rasterize_sum_forward_slabs_ordered(
                               order_flags);
 }
 
+// The op-path backward's launch (every backward entry point): the row-item
+// kernel, timed on channel kTimingSumBwd; the diagnostic library's knob 29 = 1
+// launches round 4's kernel instead (A/B).
+static void sum_bwd_launch(hipStream_t s, int tbx, int img_w, int img_h, int ntiles,
+                           const int *ids, const int2 *bins, const float2 *xys, const float *conics,
+                           const float *colors, const float *opac, const int *final_idx,
+                           const float *v_out, VStrides vs, float *grad, const int *det_off,
+                           const int *det_radii, float *det_part, long long det_cap) {
+    hipEvent_t tev[2];
+    const int tslot = timing_begin(s, tev, kTimingSumBwd);
+#ifdef GSVC_DIAG
+    if (knob(29) == 1) {
+        launch_timed(raster_sum_bwd_kernel_r4, dim3(ntiles), dim3(256), 0, s, tev, tbx, img_w, img_h,
+                     ntiles, ids, bins, xys, conics, colors, opac, final_idx, v_out, vs, grad, det_off,
+                     det_radii, det_part, det_cap);
+        timing_end(s, tslot, kTimingSumBwd);
+        return;
+    }
+#endif
+    launch_timed(raster_sum_bwd_kernel, dim3(ntiles), dim3(kSBThreads), 0, s, tev, tbx, img_w, img_h,
+                 ntiles, ids, bins, xys, conics, colors, opac, final_idx, v_out, vs, grad, det_off,
+                 det_radii, det_part, det_cap);
+    timing_end(s, tslot, kTimingSumBwd);
+}
+
 extern "C" int gsvc_rasterize_sum_backward_zeroed_strided(
     unsigned img_height, unsigned img_width, int num_points, const int *gaussian_ids_sorted,
     const int *tile_bins, const float *xys, const float *conics, const float *colors,
@@ -1377,10 +1656,9 @@ extern "C" int gsvc_rasterize_sum_backward_zeroed_strided(
         return set_error(GSVC_ERR_ARG, "rasterize_sum_backward_zeroed_strided: bad num_points");
     const int ntiles = tbx * tby;
     if (ntiles == 0 || num_points == 0) return GSVC_OK;
-    hipLaunchKernelGGL(raster_sum_bwd_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, tbx,
-                       (int)img_width, (int)img_height, ntiles, gaussian_ids_sorted,
-                       (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacities,
-                       final_idx, v_output, vs, grad_records, nullptr, nullptr, nullptr, 0ll);
+    sum_bwd_launch((hipStream_t)stream, tbx, (int)img_width, (int)img_height, ntiles,
+                   gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys, conics, colors,
+                   opacities, final_idx, v_output, vs, grad_records, nullptr, nullptr, nullptr, 0ll);
     return check_launch("rasterize_sum_backward_zeroed_strided");
 }
 
@@ -1415,10 +1693,9 @@ extern "C" int gsvc_rasterize_sum_backward(unsigned img_height, unsigned img_wid
         return set_error(GSVC_ERR_HIP, "rasterize_sum_backward: memset failed");
     const int ntiles = tbx * tby;
     if (ntiles == 0 || num_points == 0) return GSVC_OK;
-    hipLaunchKernelGGL(raster_sum_bwd_kernel, dim3(ntiles), dim3(256), 0, s, tbx, (int)img_width,
-                       (int)img_height, ntiles, gaussian_ids_sorted, (const int2 *)tile_bins,
-                       (const float2 *)xys, conics, colors, opacities, final_idx, v_output,
-                       hwc_strides(img_width), grad_records, nullptr, nullptr, nullptr, 0ll);
+    sum_bwd_launch(s, tbx, (int)img_width, (int)img_height, ntiles, gaussian_ids_sorted,
+                   (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacities, final_idx,
+                   v_output, hwc_strides(img_width), grad_records, nullptr, nullptr, nullptr, 0ll);
     return check_launch("rasterize_sum_backward");
 }
 
@@ -1458,10 +1735,9 @@ extern "C" int gsvc_rasterize_sum_backward_det(
     if (det_capacity > 0 &&
         hipMemsetAsync(part, 0, sizeof(float) * 9 * (size_t)det_capacity, s) != hipSuccess)
         return set_error(GSVC_ERR_HIP, "rasterize_sum_backward_det: memset failed");
-    hipLaunchKernelGGL(raster_sum_bwd_kernel, dim3(ntiles), dim3(256), 0, s, tbx, (int)img_width,
-                       (int)img_height, ntiles, gaussian_ids_sorted, (const int2 *)tile_bins,
-                       (const float2 *)xys, conics, colors, opacities, final_idx, v_output,
-                       hwc_strides(img_width), grad_records, off, radii, part, det_capacity);
+    sum_bwd_launch(s, tbx, (int)img_width, (int)img_height, ntiles, gaussian_ids_sorted,
+                   (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacities, final_idx,
+                   v_output, hwc_strides(img_width), grad_records, off, radii, part, det_capacity);
     hipLaunchKernelGGL(det_gather_kernel, dim3(ceil_div(num_points, 256)), dim3(256), 0, s,
                        num_points, off, part, det_capacity, grad_records);
     if (pairs_out &&

@@ -47,6 +47,9 @@ __device__ __forceinline__ int rank_below(int v, int n) {
 __device__ inline int wave_sorted_tile_ids(SegIds ids, int n_all, int *s_ids, unsigned *bm) {
     const int lane = threadIdx.x & 63;
     if (n_all <= 0) return 0;
+    // a segment holds at most 256 slots (the slabs' size; a longer tile takes
+    // the bbox rebuild): never read past them, whatever the count says
+    n_all = min(n_all, kTilePix);
     if (n_all <= 64) {
         const int v = lane < n_all ? ids[lane] : 0x7fffffff;
         const int rank = rank_below(v, n_all);

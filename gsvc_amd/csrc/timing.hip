@@ -5,6 +5,8 @@
 //   1  train_tile_kernel   (the fused training step's per-tile kernel)
 //   2  frame_project_kernel (render and training projection + slab insertion)
 //   3  train_splat_kernel  (projection VJP + Adan)
+//   4  raster_sum_bwd_kernel (the op path's sum backward)
+//   5  raster_alpha_fwd_kernel, 6 raster_alpha_bwd_kernel (the alpha path)
 // Two ways (gsvc_timing_enable's ``how``):
 //   0  marker events recorded before and after the launch (hipEventRecord):
 //      includes the marker packets' latency and the kernel's dispatch, ~3 us

@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -76,6 +77,13 @@ struct LazyCount {
 };
 LazyCount g_counts[64];
 std::mutex g_count_lock;
+
+// The last value read, without polling the event (graph capture).
+int hint_cached(int d) {
+    if (d < 0 || d >= 64) return 0;
+    std::lock_guard<std::mutex> g(g_count_lock);
+    return g_counts[d].value;
+}
 
 int hint_value(int d) {
     if (d < 0 || d >= 64) return 0;
@@ -167,10 +175,14 @@ struct ProjectFn : public torch::autograd::Function<ProjectFn> {
 constexpr int kTileKeep = 256;  // entries per tile the sum rasterizer blends (config.h BLOCK_SIZE)
 
 // The id-slab counters of gsvc_rasterize_sum_forward_slabs, per device and
-// stream (zeroed once; each call leaves them ready for the next).
+// stream (zeroed once; each call leaves them ready for the next).  A call
+// holds the workspace's lock from its flags to its launches; the workspaces
+// live behind unique_ptrs, so registering another (device, stream) never
+// moves one a call is using.
 struct SlabWs {
+    std::mutex lock;
     Tensor buf;
-    int tiles = -1;
+    int tiles = -1;  // -1: (re)zero before use -- new, or a failed call left it dirty
     int calls = 0;
     // the splat order of the id insertion (speed only): sorted by a refresh
     // call for order_n splats, re-sorted every kOrderRefresh calls
@@ -190,44 +202,60 @@ bool op_order_enabled() {
 
 // GSVC_TRAIN_ORDER when ws holds an order for n splats, GSVC_TRAIN_ORDER_REFRESH
 // when it has none or it is kOrderRefresh calls old (train.py order_flags).
+// Nothing is recorded here: order_commit() does that once the call has
+// succeeded, so a failed call never leaves an order marked valid that was not
+// written (an unsorted order buffer is what faulted in round 4).
 int order_flags(SlabWs &ws, int n, const Tensor &like) {
     if (!op_order_enabled() || n <= 0) return 0;
     int flags = 0;
-    if (ws.order_n == n) {
-        flags |= GSVC_TRAIN_ORDER;
-        ++ws.order_age;
-    }
-    if (ws.order_n != n || ws.order_age >= kOrderRefresh) {
+    if (ws.order_n == n) flags |= GSVC_TRAIN_ORDER;
+    if (ws.order_n != n || ws.order_age + 1 >= kOrderRefresh) {
         flags |= GSVC_TRAIN_ORDER_REFRESH;
-        if (ws.order_n != n) {
-            const size_t bytes = gsvc_rasterize_sum_order_workspace_bytes(n);
+        const size_t bytes = gsvc_rasterize_sum_order_workspace_bytes(n);
+        if (!ws.order.defined() || (size_t)ws.order.numel() < bytes)
             ws.order = at::empty({(int64_t)bytes}, like.options().dtype(at::kByte));
-        }
-        ws.order_n = n;
-        ws.order_age = 0;
     }
     return flags;
 }
-std::mutex g_ws_lock;
-std::vector<std::pair<std::pair<int, void *>, SlabWs>> g_ws;
 
-SlabWs &slab_ws(const Tensor &like, void *stream, int ntiles) {
+void order_commit(SlabWs &ws, int n, int flags) {
+    if (flags & GSVC_TRAIN_ORDER_REFRESH) {
+        ws.order_n = n;
+        ws.order_age = 0;
+    } else if (flags & GSVC_TRAIN_ORDER) {
+        ++ws.order_age;
+    }
+}
+
+std::mutex g_ws_lock;
+std::vector<std::pair<std::pair<int, void *>, std::unique_ptr<SlabWs>>> g_ws;
+
+// The (device, stream) workspace, created on first use (stable address).
+SlabWs &slab_ws(const Tensor &like, void *stream) {
     std::lock_guard<std::mutex> g(g_ws_lock);
     const std::pair<int, void *> key(like.device().index(), stream);
-    SlabWs *w = nullptr;
     for (auto &kv : g_ws)
-        if (kv.first == key) w = &kv.second;
-    if (!w) {
-        g_ws.emplace_back(key, SlabWs());
-        w = &g_ws.back().second;
-    }
-    if (w->tiles != ntiles) {
+        if (kv.first == key) return *kv.second;
+    g_ws.emplace_back(key, std::make_unique<SlabWs>());
+    return *g_ws.back().second;
+}
+
+// Counters for ntiles tiles, zeroed when the workspace is new, resized or dirty
+// (caller holds ws.lock).
+void slab_ws_ready(SlabWs &w, const Tensor &like, int ntiles) {
+    if (w.tiles != ntiles) {
         const size_t bytes = gsvc_rasterize_sum_slabs_workspace_bytes(ntiles);
-        w->buf = at::zeros({(int64_t)((bytes + 3) / 4)}, like.options().dtype(at::kInt));
-        w->tiles = ntiles;
-        w->calls = 0;
+        w.buf = at::zeros({(int64_t)((bytes + 3) / 4)}, like.options().dtype(at::kInt));
+        w.tiles = ntiles;
+        w.calls = 0;
+        w.order_n = -1;
     }
-    return *w;
+}
+
+bool capturing(void *stream) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing((hipStream_t)stream, &cs) == hipSuccess &&
+           cs != hipStreamCaptureStatusNone;
 }
 
 // rasterize_sum.py:89-254 with the binning of gsvc_rasterize_sum_forward_slabs
@@ -251,20 +279,50 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
         const auto f = xys.options();
         const auto i = f.dtype(at::kInt);
         void *st = stream_of(xys);
-        SlabWs &ws = slab_ws(xys, st, nt);
         Tensor gids = at::empty({(int64_t)nt * kTileKeep}, i), bins = at::empty({nt, 2}, i);
         Tensor meta = at::empty({2}, i), out = at::empty({H, W, 3}, f), idx = at::empty({H, W}, i);
-        Tensor rec = need_grad ? at::empty({n, 16}, f) : Tensor();
-        const int hint = hint_value(xys.device().index());  // M of an earlier call
-        const int oflags = order_flags(ws, (int)n, xys);
-        check(gsvc_rasterize_sum_forward_slabs_ordered(
-                  (int)n, fp(xys), ip(radii), fp(conics), fp(colors), fp(opacity), fp(background),
-                  (unsigned)H, (unsigned)W, ws.calls++, hint, ws.buf.data_ptr(),
-                  4 * (size_t)ws.buf.numel(), ip(gids), ip(bins), ip(meta), fp(rec), fp(out),
-                  ip(idx), st, oflags ? ws.order.data_ptr() : nullptr,
-                  oflags ? (size_t)ws.order.numel() : 0, oflags),
-              "gsvc_rasterize_sum_forward_slabs_ordered");
-        hint_refresh(meta, st);
+        Tensor rec;
+        if (capturing(st)) {
+            // Graph capture: the slab workspace's parity is host state a replay
+            // would freeze, so the capturable route -- the counted binning (its
+            // scratch allocated per call, from the graph's pool) and the
+            // composite over its bins; the same ids, order and bits.  The
+            // backward adds into records zeroed here (the insertion zeroes them
+            // on the slab route).
+            rec = need_grad ? at::zeros({n, 16}, f) : Tensor();
+            const int64_t cap = (int64_t)nt * std::min<int64_t>(n, kTileKeep);
+            Tensor scratch = at::empty({std::max<int64_t>(cap, 1)}, i);
+            Tensor cws = at::empty(
+                {(int64_t)(gsvc_bin_tiles_counted_workspace_bytes(nt) / 4 + 1)}, i);
+            check(gsvc_bin_tiles_counted((int)n, fp(xys), ip(radii), tbx, tby, cap, kTileKeep,
+                                         ip(scratch), ip(gids), ip(bins), ip(meta), cws.data_ptr(),
+                                         4 * (size_t)cws.numel(), st),
+                  "gsvc_bin_tiles_counted");
+            check(gsvc_rasterize_sum_forward_ex(tbx, tby, 1, 16, 16, 1, (unsigned)W, (unsigned)H, 1,
+                                                ip(gids), ip(bins), fp(xys), fp(conics), fp(colors),
+                                                fp(opacity), fp(background), ip(meta),
+                                                hint_cached(xys.device().index()), 0, fp(out),
+                                                nullptr, ip(idx), st),
+                  "gsvc_rasterize_sum_forward_ex");
+        } else {
+            rec = need_grad ? at::empty({n, 16}, f) : Tensor();
+            SlabWs &ws = slab_ws(xys, st);
+            std::lock_guard<std::mutex> wl(ws.lock);
+            slab_ws_ready(ws, xys, nt);
+            const int hint = hint_value(xys.device().index());  // M of an earlier call
+            const int oflags = order_flags(ws, (int)n, xys);
+            const int rc = gsvc_rasterize_sum_forward_slabs_ordered(
+                (int)n, fp(xys), ip(radii), fp(conics), fp(colors), fp(opacity), fp(background),
+                (unsigned)H, (unsigned)W, ws.calls, hint, ws.buf.data_ptr(),
+                4 * (size_t)ws.buf.numel(), ip(gids), ip(bins), ip(meta), fp(rec), fp(out), ip(idx),
+                st, oflags ? ws.order.data_ptr() : nullptr, oflags ? (size_t)ws.order.numel() : 0,
+                oflags);
+            if (rc != 0) ws.tiles = -1;  // counters and order in an unknown state: rebuild
+            check(rc, "gsvc_rasterize_sum_forward_slabs_ordered");
+            ++ws.calls;
+            order_commit(ws, (int)n, oflags);
+            hint_refresh(meta, st);
+        }
         Tensor m_dev = meta.narrow(0, 0, 1);
         ctx->save_for_backward({gids, bins, xys, conics, colors, opacity, idx});
         ctx->set_materialize_grads(false);  // M's gradient (always undefined): no fill

@@ -33,6 +33,7 @@
 #include "frame.h"
 #include "frame_dev.h"
 #include "det.h"
+#include "rows.h"
 #include "tile_ids.h"
 
 namespace gsvc {
@@ -90,36 +91,6 @@ struct TrainTileArgs {
 __device__ __forceinline__ float clamp_unit(float x) {
     // torch.clamp(x, 0, 1): NaN stays NaN
     return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x);
-}
-
-// The pixels of the 16x16 tile at (tx0, ty0) at whose centres splat (x, y,
-// conic a b c, opacity o) can reach alpha >= 1/255, as a rectangle of tile
-// coordinates packed {x0, x1, y0, y1} (4 bits each, inclusive); kNoRect
-// when provably none.  alpha >= 1/255 needs sigma <= ln(255 o), i.e.
-// d^T C d <= 2 ln(255 o), an ellipse with half-extents sqrt(2 ln(255 o) c / det)
-// and sqrt(2 ln(255 o) a / det); the margins (0.1 % + 0.01 px) dwarf fp32
-// rounding (the banded forward's test, raster_sum.hip ellipse_hits_rect).  A
-// culled (entry, pixel) pair contributes nothing in the reference either.
-constexpr unsigned kNoRect = 0x000fu;  // x0 = 15 > x1 = 0: empty (fits the 16-bit LDS slot)
-constexpr unsigned kFullRect = 0xf0f0u;  // x 0..15, y 0..15
-
-__device__ __forceinline__ unsigned ellipse_rect(float x, float y, float a, float b, float c,
-                                                 float o, float tx0, float ty0) {
-    if (!(o > 0.0f)) return (o <= 0.0f) ? kNoRect : kFullRect;  // o <= 0: never valid; NaN: keep
-    const float det = a * c - b * b;
-    if (!(a > 0.0f) || !(det > 0.0f) || !(o < 3.0e38f) || !(fabsf(x) < 1e30f) || !(fabsf(y) < 1e30f))
-        return kFullRect;  // not positive definite / non-finite: no culling
-    const float lg = __logf(255.0f * o);
-    if (lg < -0.01f) return kNoRect;  // o < e^-0.01 / 255: alpha < 1/255 everywhere
-    const float S2 = 2.0f * (lg * 1.001f + 0.01f);
-    // hardware rcp / sqrt (~1 ulp): the 0.1 % + 0.01 px margins dwarf their error
-    const float inv_det = __builtin_amdgcn_rcpf(det);
-    const float ex = __builtin_amdgcn_sqrtf(S2 * c * inv_det) * 1.001f + 0.01f;
-    const float ey = __builtin_amdgcn_sqrtf(S2 * a * inv_det) * 1.001f + 0.01f;
-    const float x0 = fmaxf(ceilf(x - ex - tx0), 0.0f), x1 = fminf(floorf(x + ex - tx0), 15.0f);
-    const float y0 = fmaxf(ceilf(y - ey - ty0), 0.0f), y1 = fminf(floorf(y + ey - ty0), 15.0f);
-    if (!(x0 <= x1) || !(y0 <= y1)) return kNoRect;
-    return (unsigned)x0 | ((unsigned)x1 << 4) | ((unsigned)y0 << 8) | ((unsigned)y1 << 12);
 }
 
 // The first <= 256 ids (ascending) of the splats whose bbox covers tile
@@ -548,101 +519,6 @@ __device__ __forceinline__ void blend2_cut(float gx, float ha, float bdy, float 
     ab = __builtin_elementwise_fma((v2f)cb, av, ab);
 }
 
-// An entry's geometry (x, y, a/2, b; c/2) is bounded (cull.h geo_bounded):
-// its sigma is then never NaN, and the sigma-threshold alpha cut applies.
-__device__ __forceinline__ bool geo_cut_ok(const float4 &G, float hc) {
-    return geo_bounded(G.x, G.y, G.z, G.w, hc);
-}
-
-// Inclusive scans over one wave's 64 lanes with DPP (no LDS traffic):
-// row_shr 1, 2, 4, 8 inside each 16-lane row, then row_bcast 15 / 31 carry a
-// row's last lane into the rows above; ``id`` is the operation's identity.
-template <bool kMax>
-__device__ __forceinline__ int wave_scan_dpp(int v, int id) {
-    auto step = [&](int t) { v = kMax ? max(v, t) : v + t; };
-    step(__builtin_amdgcn_update_dpp(id, v, 0x111, 0xf, 0xf, false));  // row_shr:1
-    step(__builtin_amdgcn_update_dpp(id, v, 0x112, 0xf, 0xf, false));  // row_shr:2
-    step(__builtin_amdgcn_update_dpp(id, v, 0x114, 0xf, 0xf, false));  // row_shr:4
-    step(__builtin_amdgcn_update_dpp(id, v, 0x118, 0xf, 0xf, false));  // row_shr:8
-    step(__builtin_amdgcn_update_dpp(id, v, 0x142, 0xa, 0xf, false));  // row_bcast:15 -> rows 1, 3
-    step(__builtin_amdgcn_update_dpp(id, v, 0x143, 0xc, 0xf, false));  // row_bcast:31 -> rows 2, 3
-    return v;
-}
-
-// One step of a segmented inclusive sum: lanes whose DPP source lane carries
-// the same key add its 8 sums (sources outside the row / masked rows: key -1,
-// and the lane is not written).  ``g += m * g[src]`` with m = 1 or 0 as ONE
-// v_fmac_f32_dpp per sum (the compiler does not fold the DPP move into an fma);
-// exact while the sums are finite (x * 0 = 0), so a wave with a non-finite sum
-// takes the select form (seg_step8_sel).
-#define GSVC_FMAC_DPP8(CTRL)                                                               \
-    asm volatile("s_nop 1\n\t"                                                             \
-                 "v_fmac_f32_dpp %0, %0, %8 " CTRL "\n\t"                                  \
-                 "v_fmac_f32_dpp %1, %1, %8 " CTRL "\n\t"                                  \
-                 "v_fmac_f32_dpp %2, %2, %8 " CTRL "\n\t"                                  \
-                 "v_fmac_f32_dpp %3, %3, %8 " CTRL "\n\t"                                  \
-                 "v_fmac_f32_dpp %4, %4, %8 " CTRL "\n\t"                                  \
-                 "v_fmac_f32_dpp %5, %5, %8 " CTRL "\n\t"                                  \
-                 "v_fmac_f32_dpp %6, %6, %8 " CTRL "\n\t"                                  \
-                 "v_fmac_f32_dpp %7, %7, %8 " CTRL "\n\t"                                  \
-                 "s_nop 1"                                                                 \
-                 : "+v"(g[0]), "+v"(g[1]), "+v"(g[2]), "+v"(g[3]), "+v"(g[4]), "+v"(g[5]), \
-                   "+v"(g[6]), "+v"(g[7])                                                  \
-                 : "v"(m))
-
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ float seg_mask(int key) {
-    const int ks = __builtin_amdgcn_update_dpp(-1, key, kCtrl, kRowMask, 0xf, false);
-    return ks == key ? 1.0f : 0.0f;
-}
-
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ void seg_step8_sel(float (&g)[8], int key) {
-    const int ks = __builtin_amdgcn_update_dpp(-1, key, kCtrl, kRowMask, 0xf, false);
-    const bool same = ks == key;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const float t = __int_as_float(
-            __builtin_amdgcn_update_dpp(0, __float_as_int(g[c]), kCtrl, kRowMask, 0xf, false));
-        g[c] = same ? g[c] + t : g[c];
-    }
-}
-
-// Segmented inclusive sums over one wave's 64 lanes, segments = runs of equal
-// key >= 0 (contiguous): lane i ends with the sum of its run's lanes <= i.
-// The wave_scan_dpp steps; a source lane is added only inside the run, so
-// each lane's sum covers exactly [max(run start, ...), i].
-template <bool kLong>
-__device__ __forceinline__ void wave_seg_sums(float (&g)[8], int key) {
-    // finite unless some sum is inf / NaN (or the total overflows: then the
-    // exact select form runs, which is still right)
-    const float tot = ((g[0] + g[1]) + (g[2] + g[3])) + ((g[4] + g[5]) + (g[6] + g[7]));
-    if (__ballot(!__builtin_isfinite(tot)) == 0ull) {
-        float m;
-        m = seg_mask<0x111, 0xf>(key);
-        GSVC_FMAC_DPP8("row_shr:1 row_mask:0xf bank_mask:0xf");
-        m = seg_mask<0x112, 0xf>(key);
-        GSVC_FMAC_DPP8("row_shr:2 row_mask:0xf bank_mask:0xf");
-        m = seg_mask<0x114, 0xf>(key);
-        GSVC_FMAC_DPP8("row_shr:4 row_mask:0xf bank_mask:0xf");
-        if (kLong) {  // runs longer than 8 lanes
-            m = seg_mask<0x118, 0xf>(key);
-            GSVC_FMAC_DPP8("row_shr:8 row_mask:0xf bank_mask:0xf");
-        }
-        m = seg_mask<0x142, 0xa>(key);
-        GSVC_FMAC_DPP8("row_bcast:15 row_mask:0xa bank_mask:0xf");
-        m = seg_mask<0x143, 0xc>(key);
-        GSVC_FMAC_DPP8("row_bcast:31 row_mask:0xc bank_mask:0xf");
-    } else {
-        seg_step8_sel<0x111, 0xf>(g, key);  // row_shr:1
-        seg_step8_sel<0x112, 0xf>(g, key);  // row_shr:2
-        seg_step8_sel<0x114, 0xf>(g, key);  // row_shr:4
-        if (kLong) seg_step8_sel<0x118, 0xf>(g, key);  // row_shr:8
-        seg_step8_sel<0x142, 0xa>(g, key);  // row_bcast:15 -> rows 1, 3
-        seg_step8_sel<0x143, 0xc>(g, key);  // row_bcast:31 -> rows 2, 3
-    }
-}
-#undef GSVC_FMAC_DPP8
 
 // The loss workgroup's loads per round: 16 tile pairs per thread in flight, so
 // a 1080p frame (4080 pairs) is one round trip.
@@ -725,10 +601,6 @@ __device__ __forceinline__ void publish_loss(const float2 *err, int ntiles, doub
     }
 }
 
-// v_out rows padded to 17 words: the backward's lanes read pixels of
-// different rows of one column, which with 16-word rows share a bank every 4
-// rows (measured: LDS bank conflicts ~ the VALU time at trained density).
-constexpr int kVRow = kTile + 1;
 
 struct BandLds {
     float v[3][kTile * kVRow];     // v_out planes, rows padded to kVRow words
@@ -1322,9 +1194,9 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             // crossing a 16-lane row still takes the row broadcast)
             if (!(kDiag && (A.diag & 16))) {  // diag 16: no run sums (wrong)
                 if (brun_of(A) < 16)
-                    wave_seg_sums<true>(g, own);
+                    wave_seg_sums<8, true>(g, own);
                 else
-                    wave_seg_sums<false>(g, own);
+                    wave_seg_sums<8, false>(g, own);
             }
             const int own_next = __shfl_down(own, 1, 64);
             if (item < total && (lane == 63 || item + 1 == total || own_next != own)) {
@@ -1757,6 +1629,7 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
         return set_error(GSVC_ERR_WORKSPACE, "train_step_sum: workspace too small (%zu < %zu)",
                          workspace_bytes, w.bytes);
     hipStream_t s = (hipStream_t)stream;
+    if (const int rc = refuse_capture(s, "train_step_sum")) return rc;
     const FrameSlots f = frame_slots(w.f, ntiles, frame_index);
     // GSVC_TRAIN_ORDER: project in the workspace's splat order (windowed slot
     // atomics); GSVC_TRAIN_ORDER_REFRESH: write keys and sort a new order

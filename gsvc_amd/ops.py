@@ -64,7 +64,8 @@ def composite_times_ms(max_launches: int = 4096):
     return list(buf[: cnt.value])
 
 
-TIMING_CHANNELS = {"composite": 0, "train_tile": 1, "project": 2, "train_splat": 3}
+TIMING_CHANNELS = {"composite": 0, "train_tile": 1, "project": 2, "train_splat": 3,
+                   "sum_bwd": 4, "alpha_fwd": 5, "alpha_bwd": 6}
 
 
 def channel_timing(channel: str, on: bool, max_launches: int = 4096, every: int = 1,

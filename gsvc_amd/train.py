@@ -411,7 +411,13 @@ class BoundStep:
                 if torch.is_deterministic_algorithms_warn_only_enabled():
                     warnings.warn(msg)
                 else:
-                    raise RuntimeError(msg)
+                    # the step has run (its Adan update is applied: the short
+                    # capacity is only known from the step's own pair count);
+                    # the work it enqueued for the next step used the same short
+                    # capacity, so it is discarded and the next call rebuilds
+                    ws.pending = None
+                    ws.dirty = True
+                    raise RuntimeError(msg + "; this step's parameter update has been applied")
         return self.host_f[0], self.host_f[1]
 
 

@@ -49,6 +49,8 @@ class _LazyCount:
         self.calls += 1
         if self.calls % self.period != 1 and self.period != 1:
             return self.value
+        if torch.cuda.is_current_stream_capturing():
+            return self.value  # no event query or copy inside a graph capture
         if self.event is not None and self.event.query():
             self.value = int(self.buf[0])
             self.event = None

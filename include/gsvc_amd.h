@@ -15,7 +15,14 @@
  *   - All pointers are device (HBM) pointers unless stated otherwise.
  *   - ``stream`` is a hipStream_t (NULL = legacy default stream); every entry
  *     point is asynchronous on it and never synchronises the device, so calls
- *     can be captured in a hipGraph.
+ *     can be captured in a hipGraph -- except the entries whose workspace
+ *     alternates host-indexed parity slots (call_index / frame_index: the
+ *     slab renders, gsvc_rasterize_sum_forward_slabs*, the fused training
+ *     step): a replay would re-add into the slots capture froze, so they
+ *     refuse a capturing stream with GSVC_ERR_CAPTURE before any launch (the
+ *     reference's own forward cannot be captured either: its .item(),
+ *     utils.py:117).  The counted binning + rasterize_sum entries are the
+ *     capturable route.
  *   - Return value: 0 on success, otherwise a gsvc_status code; the message of
  *     the last failure on the calling thread is gsvc_last_error().  Bad
  *     arguments are rejected before any launch (the reference raised
@@ -40,8 +47,13 @@ enum gsvc_status {
     GSVC_OK = 0,
     GSVC_ERR_ARG = 1,       /* invalid argument (shape, size, tile size) */
     GSVC_ERR_WORKSPACE = 2, /* workspace too small */
-    GSVC_ERR_HIP = 3        /* HIP runtime / launch error */
+    GSVC_ERR_HIP = 3,       /* HIP runtime / launch error */
+    GSVC_ERR_CAPTURE = 4    /* the stream is capturing a graph and the entry keeps host-indexed state */
 };
+
+/* ABI version 2: gsvc_debug_set / gsvc_debug_set_ptr moved to the diagnostic
+ * library (gsvc_amd_diag.h); GSVC_ERR_CAPTURE added. */
+#define GSVC_ABI_VERSION 2
 
 /* Library identity and error reporting. */
 int gsvc_abi_version(void);
@@ -88,7 +100,8 @@ int gsvc_timing_enable(int max_launches, int every, int how);
 int gsvc_timing_collect(float *ms, int max_out, int *count);
 /* The same for one kernel channel: 0 the composite (as above), 1 the fused
  * training step's tile kernel, 2 the frame projection (render and training),
- * 3 the training step's per-splat kernel (projection VJP + Adan). */
+ * 3 the training step's per-splat kernel (projection VJP + Adan), 4 the sum
+ * rasterizer's backward, 5 / 6 the alpha rasterizer's forward / backward. */
 int gsvc_timing_enable_channel(int channel, int max_launches, int every, int how);
 int gsvc_timing_collect_channel(int channel, float *ms, int max_out, int *count);
 

@@ -8,7 +8,7 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(REPO, "tests", "golden")
-for p in (REPO, os.path.join(REPO, "oracle")):
+for p in (REPO, os.path.join(REPO, "oracle"), os.path.join(REPO, "tools")):
     if p not in sys.path:
         sys.path.insert(0, p)
 

@@ -1,5 +1,5 @@
 """Fused Adan (gsvc_amd.adan.Adan over gsvc_adan_step) against the foreach
-restatement of optimizer.py:296-362 (tests/adan_checker.py) on the GPU,
+restatement of optimizer.py:296-362 (tools/foreach_adan.py) on the GPU,
 several steps, with and without weight decay and no_prox, and against the
 reference's own first step (fixture).  fp32 bar: rtol 2e-6 / atol 1e-7 per
 step on params and state (rounding only).  Gradient clipping: the step's clip
@@ -21,7 +21,7 @@ def _params(n, seed, dev):
 
 @pytest.mark.parametrize("wd,no_prox", [(0.0, False), (0.02, False), (0.02, True)])
 def test_fused_matches_foreach(cuda, wd, no_prox):
-    from adan_checker import ForeachAdan
+    from foreach_adan import ForeachAdan
     from gsvc_amd.adan import Adan
     a = _params(5003, 1, cuda)
     b = [torch.nn.Parameter(p.detach().clone()) for p in a]
@@ -57,7 +57,7 @@ def test_fused_first_step_matches_reference_fixture(cuda):
 def test_clipping_scales_grads_like_reference(cuda):
     """max_grad_norm > 0: the update uses clip = min(1, max / (||g|| + eps))
     and p.grad is left scaled by it (optimizer.py:129-147, 319)."""
-    from adan_checker import foreach_adan
+    from foreach_adan import foreach_adan
     from gsvc_amd.adan import Adan
     a = _params(777, 4, cuda)
     grads = [torch.randn(p.shape, generator=torch.Generator().manual_seed(9)).to(cuda) * 3.0

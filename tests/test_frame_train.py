@@ -26,10 +26,10 @@ def _load_init(model, z, prefix="init_"):
 
 
 def test_adan_step_matches_reference_cpu():
-    """The foreach Adan checker (tests/adan_checker.py, what the fused kernel
+    """The foreach Adan checker (tools/foreach_adan.py, what the fused kernel
     is held to) vs the reference's first Adan step, on CPU: same init, same
     gradients."""
-    from adan_checker import ForeachAdan
+    from foreach_adan import ForeachAdan
     z = load_golden(FIX)
     names = ["_xyz", "_cholesky", "_features_dc"]
     params = [torch.nn.Parameter(torch.from_numpy(z["init_" + k].copy())) for k in names]

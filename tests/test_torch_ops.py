@@ -211,3 +211,28 @@ def test_cpp_functions_splat_order_bit_identical(cuda):
                 xys, depths, radii, conics, nth = project_gaussians_2d(means, L, H, W, tb)
                 rasterize_gaussians_sum(xys, depths, radii, conics, nth, col, o, H, W, 16, 16,
                                         background=torch.ones(3, device=cuda))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,chol", [(9000, 0.4), (24000, 0.4)])
+def test_cpp_function_banded_id_slabs(cuda, n, chol):
+    """A dense frame (> 96 entries per tile on average): once the lazy M hint
+    has seen it, the C++ Function's composite takes the banded kernel over the
+    id slabs -- two waves per tile, ONE id sort per tile shared through LDS
+    and written back for the backward (both waves used to sort from
+    the slots wave 0 rewrites).  Every call (the first sparse, the rest
+    banded) equals the Python Function (counted binning) bit for bit in the
+    image, and its gradients within the atomics' order; 24k splats on 64 tiles
+    also pass 256 entries per tile (the bbox rebuild)."""
+    H = W = 128
+    means, L, col = _inputs(n, H, W, 77 + n, cuda, chol)
+    v_out = torch.randn(H, W, 3, generator=torch.Generator().manual_seed(5)).to(cuda)
+    ref, gr = _run(means, L, col, H, W, True, v_out)
+    m = int(ref[4].sum())  # num_tiles_hit: M
+    assert m > 96 * 64
+    for _ in range(6):
+        fast, gf = _run(means, L, col, H, W, False, v_out)
+        for a, b in zip(fast, ref):
+            assert torch.equal(a, b)
+        for a, b in zip(gf, gr):
+            assert float((a - b).abs().max()) <= 1e-5 * max(float(b.abs().max()), 1e-30)

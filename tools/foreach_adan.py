@@ -1,8 +1,10 @@
-"""TEST INFRASTRUCTURE: the foreach Adan update of GSVC's optimizer
-(reference optimizer.py:296-362 ``_multi_tensor_adan``, bias corrections
-:171-173,211, first-step neg_pre_grad :187-189) as torch foreach ops, op for
-op.  The product optimizer (gsvc_amd/adan.py) runs the fused kernel; the tests
-hold it to this sequence.  Never imported by the product path."""
+"""The foreach Adan update of GSVC's optimizer (reference optimizer.py:296-362
+``_multi_tensor_adan``, bias corrections :171-173,211, first-step neg_pre_grad
+:187-189) as torch foreach ops, op for op.  Two users: the tests hold the
+product optimizer (gsvc_amd/adan.py, one fused kernel) to this sequence, and
+bench.py's op_path times GSVC's files with the reference optimizer's own
+sequence (train_iters_per_s_foreach_adan).  Never imported by the product
+path."""
 import math
 
 import torch
