@@ -36,7 +36,11 @@ Reported beside the primary value:
   render_10k    configs[1] (render only, 10k splats) and ``video_decode``.
   op_path       the unchanged-caller path (GSVC's own files over the gsplat
                 drop-in: autograd op by op): forward, forward + backward, render
-                fps and train-iters/s at the same trained frame.
+                fps and train-iters/s at the same trained frame, with the
+                composite's and the backward kernel's rooflines.
+  alpha         the alpha-compositing operators (rasterize_gaussians) at
+                1080p / 50k: forward, forward + backward, kernel rooflines.
+  config0_cpu   BASELINE configs[0] (256x256, 1k splats) on the CPU.
 """
 from __future__ import annotations
 
@@ -162,6 +166,32 @@ def composite_bytes(shape):
     """SURVEY §8d B_fwd for the render (inference) forward: 36 N_vis + 4 M_eff +
     8 T + 12 P (the [3,H,W] clamped image written once, no final_idx)."""
     return 36 * shape["N_vis"] + 4 * shape["M_eff"] + 8 * shape["T"] + 12 * shape["P"]
+
+
+def op_composite_bytes(shape):
+    """SURVEY §8d B_fwd of the autograd forward (op path): the render's bytes
+    plus final_idx 4 P."""
+    return composite_bytes(shape) + 4 * shape["P"]
+
+
+def sum_bwd_bytes(shape, n):
+    """SURVEY §8d B_bwd: v_out 12 P + final_idx 4 P + the visible splats 36 N_vis
+    + the tile id lists 4 M_eff + bins 8 T (read) + the gradients 36 N (written)."""
+    return 16 * shape["P"] + 36 * shape["N_vis"] + 4 * shape["M_eff"] + 8 * shape["T"] + 36 * n
+
+
+def alpha_fwd_bytes(shape):
+    """The alpha forward (forward.cu:252-374): the visible splats 36 N_vis, every
+    entry of the tile lists 4 M (no 256 cap) and bins 8 T (read); out 12 P,
+    final_Ts 4 P, final_idx 4 P (written)."""
+    return 36 * shape["N_vis"] + 4 * shape["M"] + 8 * shape["T"] + 20 * shape["P"]
+
+
+def alpha_bwd_bytes(shape, n):
+    """The alpha backward (backward.cu:138-315): v_out 12 P, v_out_alpha 4 P,
+    final_Ts 4 P, final_idx 4 P, 36 N_vis + 4 M + 8 T (read); the gradients
+    36 N (written)."""
+    return 24 * shape["P"] + 36 * shape["N_vis"] + 4 * shape["M"] + 8 * shape["T"] + 36 * n
 
 
 def train_tile_bytes(shape, n):
@@ -594,13 +624,79 @@ def op_path_block(model, gt, device, steps=200, warmup=20):
     t_train = timed(train, steps, warmup)
     t_train_fe = timed(train_foreach, steps, warmup)
     assert op.fused_steps == 0
+    # the drop-in's own kernels in forward + backward calls, HIP events on
+    # their dispatches (outside the timed loops)
+    kt = time_channels(["composite", "sum_bwd"], fwd_bwd, 100)
+    shape = frame_shape(op.get_xyz.detach(), op.get_cholesky_elements.detach(), op.tile_bounds)
+    prof = load_profile("op_path")
     return {"workload": f"unchanged-caller op path at 1920x1080 / {n} splats (the bench's trained "
                         "frame): autograd through gsplat.* + clamp + NCHW",
             "fwd_us": round(t_fwd * 1e6, 1), "fwd_bwd_us": round(t_fb * 1e6, 1),
             "render_fps": round(1.0 / t_render, 1),
             "train_iters_per_s": round(1.0 / t_train, 1),
             "train_iters_per_s_foreach_adan": round(1.0 / t_train_fe, 1),
-            "timing": f"wall clock over {steps} calls after {warmup} warm-ups, synchronized"}
+            "timing": f"wall clock over {steps} calls after {warmup} warm-ups, synchronized",
+            "kernels": {
+                "raster_sum_fwd": roofline("raster_sum_fwd_kernel (op path: final_idx, id slabs)",
+                                           op_composite_bytes(shape), kt["composite"], prof,
+                                           "rasterize_sum_forward"),
+                "raster_sum_bwd": roofline("raster_sum_bwd_kernel", sum_bwd_bytes(shape, n),
+                                           kt["sum_bwd"], prof, "rasterize_sum_backward")}}
+
+
+def alpha_block(device, n=50000, steps=100, warmup=10):
+    """The alpha-compositing path north_star names (rasterize.py:14-253,
+    forward.cu:252-374, backward.cu:138-315) through the drop-in operators at
+    1920x1080: random-init splats with opacity U(0.1, 1) (tools/alphabench.py's
+    workload), project_gaussians_2d + rasterize_gaussians per call, forward and
+    forward + backward; each kernel's roofline from HIP events on its own
+    dispatches."""
+    from gsplat.project_gaussians_2d import project_gaussians_2d
+    from gsplat.rasterize import rasterize_gaussians
+    g = torch.Generator().manual_seed(n)
+    means = torch.tanh(torch.atanh(2 * (torch.rand(n, 2, generator=g) - 0.5))).to(device)
+    L = (torch.rand(n, 3, generator=g) + torch.tensor([0.5, 0, 0.5])).to(device)
+    col = torch.rand(n, 3, generator=g).to(device)
+    opac = (0.1 + 0.9 * torch.rand(n, 1, generator=g)).to(device)
+    bg = torch.ones(3, device=device)
+    tb = ((W + 15) // 16, (H + 15) // 16, 1)
+    params = [t.clone().requires_grad_(True) for t in (means, L, col, opac)]
+
+    def fwd():
+        with torch.no_grad():
+            xys, depths, radii, conics, nth = project_gaussians_2d(means, L, H, W, tb)
+            rasterize_gaussians(xys, depths, radii, conics, nth, col, opac, H, W, 16, 16, background=bg)
+
+    def fwd_bwd():
+        m, l, c, o = params
+        xys, depths, radii, conics, nth = project_gaussians_2d(m, l, H, W, tb)
+        out = rasterize_gaussians(xys, depths, radii, conics, nth, c, o, H, W, 16, 16, background=bg)
+        torch.autograd.grad(out.sum(), params)
+
+    def timed(fn):
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps
+
+    t_f = timed(fwd)
+    t_fb = timed(fwd_bwd)
+    kt = time_channels(["alpha_fwd", "alpha_bwd"], fwd_bwd, 100)
+    shape = frame_shape(means, L, tb)
+    prof = load_profile("alpha_50000")
+    return {"workload": f"rasterize_gaussians (alpha compositing) at 1920x1080 / {n} splats, random "
+                        "init, opacity U(0.1, 1): project_gaussians_2d + rasterize_gaussians per call",
+            "fwd_us": round(t_f * 1e6, 1), "fwd_bwd_us": round(t_fb * 1e6, 1),
+            "kernels": {
+                "raster_alpha_fwd": roofline("raster_alpha_fwd_kernel", alpha_fwd_bytes(shape),
+                                             kt["alpha_fwd"], prof, "alpha_forward"),
+                "raster_alpha_bwd": roofline("raster_alpha_bwd_kernel", alpha_bwd_bytes(shape, n),
+                                             kt["alpha_bwd"], prof, "alpha_backward")},
+            "shape": shape}
 
 
 def dry_run(args, world, rank):
@@ -755,6 +851,7 @@ def main():
         line["render_10k"] = render_10k(device)
         line["video_decode"] = video_decode(device)
         line["op_path"] = op_path_block(model, gt, device)
+        line["alpha"] = alpha_block(device)
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args.splats)
         if "render" in line:  # configs[2] render and configs[1]: the same frames on the CPU

@@ -563,8 +563,8 @@ static int radix_sort(int n, const K *kin, const int *vin, K *kout, int *vout, K
         ++npass;
     }
     if (npass == 0) {
-        if (hipMemcpyAsync(kout, kin, sizeof(K) * (size_t)n, hipMemcpyDeviceToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(vout, vin, sizeof(int) * (size_t)n, hipMemcpyDeviceToDevice, s) != hipSuccess)
+        if (dev_copy(kout, kin, sizeof(K) * (size_t)n, s) != GSVC_OK ||
+            dev_copy(vout, vin, sizeof(int) * (size_t)n, s) != GSVC_OK)
             return set_error(GSVC_ERR_HIP, "radix_sort: copy failed");
         return GSVC_OK;
     }
@@ -641,7 +641,7 @@ extern "C" int gsvc_compute_cumulative_intersects(int num_points, const int *num
                                                   void *stream) {
     hipStream_t s = (hipStream_t)stream;
     if (num_points <= 0) {
-        if (hipMemsetAsync(meta, 0, 4 * sizeof(int), s) != hipSuccess)
+        if (dev_zero(meta, 4 * sizeof(int), s) != GSVC_OK)
             return set_error(GSVC_ERR_HIP, "compute_cumulative_intersects: memset failed");
         return GSVC_OK;
     }
@@ -670,8 +670,8 @@ extern "C" int gsvc_map_gaussian_to_intersects(int num_points, int num_intersect
         return set_error(GSVC_ERR_ARG, "map_gaussian_to_intersects: bad sizes");
     hipStream_t s = (hipStream_t)stream;
     if (num_intersects > 0) {
-        if (hipMemsetAsync(isect_ids, 0, sizeof(int64_t) * (size_t)num_intersects, s) != hipSuccess ||
-            hipMemsetAsync(gaussian_ids, 0, sizeof(int) * (size_t)num_intersects, s) != hipSuccess)
+        if (dev_zero(isect_ids, sizeof(int64_t) * (size_t)num_intersects, s) != GSVC_OK ||
+            dev_zero(gaussian_ids, sizeof(int) * (size_t)num_intersects, s) != GSVC_OK)
             return set_error(GSVC_ERR_HIP, "map_gaussian_to_intersects: memset failed");
     }
     if (num_points == 0) return GSVC_OK;
@@ -714,7 +714,7 @@ extern "C" int gsvc_get_tile_bin_edges(int num_intersects, const int64_t *isect_
                                        int *tile_bins, int rows, void *stream) {
     if (num_intersects < 0 || rows < 0) return set_error(GSVC_ERR_ARG, "get_tile_bin_edges: bad sizes");
     hipStream_t s = (hipStream_t)stream;
-    if (rows > 0 && hipMemsetAsync(tile_bins, 0, sizeof(int) * 2 * (size_t)rows, s) != hipSuccess)
+    if (rows > 0 && dev_zero(tile_bins, sizeof(int) * 2 * (size_t)rows, s) != GSVC_OK)
         return set_error(GSVC_ERR_HIP, "get_tile_bin_edges: memset failed");
     if (num_intersects == 0) return GSVC_OK;
     hipLaunchKernelGGL(bins_i64_kernel, dim3(ceil_div(num_intersects, 256)), dim3(256), 0, s,
@@ -742,7 +742,7 @@ extern "C" int gsvc_bin_and_sort_tiles(int num_points, int num_intersects, const
         return set_error(GSVC_ERR_ARG, "bin_and_sort_tiles: bad sizes (rows %d < tiles %d?)",
                          tile_bins_rows, num_tiles);
     hipStream_t s = (hipStream_t)stream;
-    if (hipMemsetAsync(tile_bins, 0, sizeof(int) * 2 * (size_t)tile_bins_rows, s) != hipSuccess)
+    if (dev_zero(tile_bins, sizeof(int) * 2 * (size_t)tile_bins_rows, s) != GSVC_OK)
         return set_error(GSVC_ERR_HIP, "bin_and_sort_tiles: memset failed");
     const int m = num_intersects;
     if (m == 0 || num_points == 0) return GSVC_OK;
@@ -802,7 +802,7 @@ extern "C" int gsvc_bin_tiles_counted(int num_points, const float *xys, const in
     hipStream_t s = (hipStream_t)stream;
     unsigned *counts = (unsigned *)workspace;
     unsigned *cursor = (unsigned *)((char *)workspace + align_up(sizeof(unsigned) * (size_t)ntiles));
-    if (hipMemsetAsync(counts, 0, sizeof(unsigned) * (size_t)ntiles, s) != hipSuccess)
+    if (dev_zero(counts, sizeof(unsigned) * (size_t)ntiles, s) != GSVC_OK)
         return set_error(GSVC_ERR_HIP, "bin_tiles_counted: memset failed");
     if (num_points > 0)
         hipLaunchKernelGGL(tile_count_kernel, dim3(ceil_div(num_points, 256)), dim3(256), 0, s,

@@ -34,6 +34,13 @@ int check_launch(const char *what);
 // GSVC_ERR_CAPTURE when stream s is capturing a graph (entries with host-indexed
 // workspace parity; include/gsvc_amd.h conventions), else GSVC_OK
 int refuse_capture(hipStream_t s, const char *what);
+// hipMemsetAsync(p, 0, bytes, s) / a device-to-device hipMemcpyAsync as one
+// kernel of this library (errors.hip): the HIP runtime torch loads (ROCm 7.0)
+// replays graph-captured memset nodes wrongly once other work has run on the
+// stream (tools/capture_debug.py), so the library's own zeroing and copies are
+// kernels, which capture and replay like the rest.  Returns a gsvc status.
+int dev_zero(void *p, size_t bytes, hipStream_t s);
+int dev_copy(void *dst, const void *src, size_t bytes, hipStream_t s);
 // A/B knobs and diagnostic kernel variants exist only in the diagnostic
 // library (built with -DGSVC_DIAG: libgsvc_amd_diag.so, include/gsvc_amd_diag.h,
 // for tools/ and the variant-comparison tests).  In the product library every

@@ -28,12 +28,45 @@ int check_launch(const char *what) {
 }
 
 int refuse_capture(hipStream_t s, const char *what) {
+    // the legacy default stream cannot capture; asking HIP about it costs a
+    // device-wide wait (measured: op-path forward 77 -> 113 us)
+    if (s == nullptr) return GSVC_OK;
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     // (a failing query -- e.g. no device -- is left to the launches to report)
     if (hipStreamIsCapturing(s, &st) != hipSuccess || st == hipStreamCaptureStatusNone) return GSVC_OK;
     return set_error(GSVC_ERR_CAPTURE,
                      "%s cannot be captured in a graph: its workspace alternates parity slots indexed "
                      "by the host's call counter, which a replay would not advance", what);
+}
+
+namespace {
+// 16-byte chunks where both ends allow it, bytes otherwise (grid-stride)
+__global__ __launch_bounds__(256) void fill_kernel(unsigned char *__restrict__ dst,
+                                                   const unsigned char *__restrict__ src,
+                                                   size_t bytes) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool v16 = (((uintptr_t)dst | (uintptr_t)src) & 15u) == 0;
+    const size_t n16 = v16 ? bytes / 16 : 0;
+    for (size_t i = t0; i < n16; i += stride)
+        reinterpret_cast<uint4 *>(dst)[i] =
+            src ? reinterpret_cast<const uint4 *>(src)[i] : make_uint4(0u, 0u, 0u, 0u);
+    for (size_t i = 16 * n16 + t0; i < bytes; i += stride) dst[i] = src ? src[i] : (unsigned char)0;
+}
+
+int fill_launch(void *dst, const void *src, size_t bytes, hipStream_t s, const char *what) {
+    if (bytes == 0) return GSVC_OK;
+    const size_t chunks = (bytes + 15) / 16;
+    const unsigned grid = (unsigned)(chunks / 256 + 1 < 4096 ? chunks / 256 + 1 : 4096);
+    hipLaunchKernelGGL(fill_kernel, dim3(grid), dim3(256), 0, s, (unsigned char *)dst,
+                       (const unsigned char *)src, bytes);
+    return check_launch(what);
+}
+}  // namespace
+
+int dev_zero(void *p, size_t bytes, hipStream_t s) { return fill_launch(p, nullptr, bytes, s, "zero fill"); }
+int dev_copy(void *dst, const void *src, size_t bytes, hipStream_t s) {
+    return fill_launch(dst, src, bytes, s, "device copy");
 }
 
 #ifdef GSVC_DIAG

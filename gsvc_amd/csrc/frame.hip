@@ -346,8 +346,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
     const int per = frames > 1 ? max_frame_n : n;
     if (frames > 1 && per <= 0) {
         // no splats anywhere: only the M slots (memset of the whole [F][2] block)
-        if (hipMemsetAsync(f.m_acc < f.m_clear ? f.m_acc : f.m_clear, 0,
-                           sizeof(int) * 2 * (size_t)frames, s) != hipSuccess)
+        if (dev_zero(f.m_acc < f.m_clear ? f.m_acc : f.m_clear, sizeof(int) * 2 * (size_t)frames, s) != GSVC_OK)
             return set_error(GSVC_ERR_HIP, "frame projection: memset failed");
         return check_launch("frame projection");
     }
@@ -387,7 +386,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
             GSVC_FRAME_PROJECT(1);
         }
 #undef GSVC_FRAME_PROJECT
-    } else if (hipMemsetAsync(f.m_acc, 0, sizeof(int), s) != hipSuccess)
+    } else if (dev_zero(f.m_acc, sizeof(int), s) != GSVC_OK)
         return set_error(GSVC_ERR_HIP, "frame projection: memset failed");
     return check_launch("frame projection");
 }

@@ -255,8 +255,8 @@ extern "C" int gsvc_prune_lowest(int num_points, int remove_count, const float *
     const int chunks = ceil_div(num_points, kPruneChunk);
     hipStream_t s = (hipStream_t)stream;
     // (T, r) = (0, 0) removes nothing; the passes' tickets and histograms start at 0
-    if (hipMemsetAsync(workspace, 0, kPruneHeaderBytes, s) != hipSuccess)
-        return set_error(GSVC_ERR_HIP, "prune_lowest: hipMemsetAsync failed");
+    if (dev_zero(workspace, kPruneHeaderBytes, s) != GSVC_OK)
+        return set_error(GSVC_ERR_HIP, "prune_lowest: zero fill failed");
     if (remove_count > 0) {
         const int grid = std::min(ceil_div(num_points, 1024), 256);
         for (int d = 3; d >= 0; --d)

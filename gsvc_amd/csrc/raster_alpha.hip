@@ -325,12 +325,16 @@ extern "C" int gsvc_rasterize_forward(int tbx, int tby, int tbz, int block_x, in
         return set_error(GSVC_ERR_ARG, "rasterize_forward: tile_bounds do not match the image");
     const int ntiles = tbx * tby;
     if (ntiles == 0) return GSVC_OK;
-    hipLaunchKernelGGL(raster_alpha_fwd_kernel, dim3(ntiles), dim3(64), 0, (hipStream_t)stream, tbx,
-                       (int)img_width, (int)img_height, ntiles, gaussian_ids_sorted,
-                       (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacities,
-                       background, out_img, final_Ts, final_idx,
-                       // A/B knob 18 = v > 0: list threshold v - 1
-                       knob(18) > 0 ? knob(18) - 1 : kAGroupMin);
+    hipStream_t s = (hipStream_t)stream;
+    hipEvent_t tev[2];
+    const int tslot = timing_begin(s, tev, kTimingAlphaFwd);
+    launch_timed(raster_alpha_fwd_kernel, dim3(ntiles), dim3(64), 0, s, tev, tbx, (int)img_width,
+                 (int)img_height, ntiles, gaussian_ids_sorted, (const int2 *)tile_bins,
+                 (const float2 *)xys, conics, colors, opacities, background, out_img, final_Ts,
+                 final_idx,
+                 // A/B knob 18 = v > 0: list threshold v - 1
+                 knob(18) > 0 ? knob(18) - 1 : kAGroupMin);
+    timing_end(s, tslot, kTimingAlphaFwd);
     return check_launch("rasterize_forward");
 }
 
@@ -347,7 +351,7 @@ extern "C" int gsvc_rasterize_backward(unsigned img_height, unsigned img_width, 
     if (num_points < 0) return set_error(GSVC_ERR_ARG, "rasterize_backward: bad num_points");
     hipStream_t s = (hipStream_t)stream;
     if (num_points > 0 &&
-        hipMemsetAsync(grad_records, 0, sizeof(float) * 16 * (size_t)num_points, s) != hipSuccess)
+        dev_zero(grad_records, sizeof(float) * 16 * (size_t)num_points, s) != GSVC_OK)
         return set_error(GSVC_ERR_HIP, "rasterize_backward: memset failed");
     const int tbx = ceil_div((int)img_width, kTile), tby = ceil_div((int)img_height, kTile);
     const int ntiles = tbx * tby;
@@ -355,10 +359,12 @@ extern "C" int gsvc_rasterize_backward(unsigned img_height, unsigned img_width, 
     auto bwd = raster_alpha_bwd_kernel<true>;  // per-row DPP sums
     if constexpr (kDiag)
         if (knob(9) == 1) bwd = raster_alpha_bwd_kernel<false>;  // A/B: the shuffle butterflies
-    hipLaunchKernelGGL(bwd,
-                       dim3(ntiles), dim3(256), 0, s, tbx, (int)img_width,
-                       (int)img_height, ntiles, gaussian_ids_sorted, (const int2 *)tile_bins,
-                       (const float2 *)xys, conics, colors, opacities, background, final_Ts,
-                       final_idx, v_output, v_output_alpha, grad_records);
+    hipEvent_t tev[2];
+    const int tslot = timing_begin(s, tev, kTimingAlphaBwd);
+    launch_timed(bwd, dim3(ntiles), dim3(256), 0, s, tev, tbx, (int)img_width, (int)img_height,
+                 ntiles, gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys, conics,
+                 colors, opacities, background, final_Ts, final_idx, v_output, v_output_alpha,
+                 grad_records);
+    timing_end(s, tslot, kTimingAlphaBwd);
     return check_launch("rasterize_backward");
 }

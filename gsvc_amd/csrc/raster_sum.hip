@@ -1552,7 +1552,7 @@ static int forward_slabs_impl(
                            dim3(kProjThreads), 0, s, num_points, (const float2 *)xys, radii, tbx,
                            tby, counts + (size_t)par * ntiles, gaussian_ids, m_slots + par,
                            m_slots + (par ^ 1), (float4 *)grad_records_zero);
-    } else if (hipMemsetAsync(m_slots, 0, 2 * sizeof(int), s) != hipSuccess) {
+    } else if (dev_zero(m_slots, 2 * sizeof(int), s) != GSVC_OK) {
         return set_error(GSVC_ERR_HIP, "rasterize_sum_forward_slabs: memset failed");
     }
     SumFwdArgs A;
@@ -1689,7 +1689,7 @@ extern "C" int gsvc_rasterize_sum_backward(unsigned img_height, unsigned img_wid
     if (num_points < 0) return set_error(GSVC_ERR_ARG, "rasterize_sum_backward: bad num_points");
     hipStream_t s = (hipStream_t)stream;
     if (num_points > 0 &&
-        hipMemsetAsync(grad_records, 0, sizeof(float) * 16 * (size_t)num_points, s) != hipSuccess)
+        dev_zero(grad_records, sizeof(float) * 16 * (size_t)num_points, s) != GSVC_OK)
         return set_error(GSVC_ERR_HIP, "rasterize_sum_backward: memset failed");
     const int ntiles = tbx * tby;
     if (ntiles == 0 || num_points == 0) return GSVC_OK;
@@ -1723,7 +1723,7 @@ extern "C" int gsvc_rasterize_sum_backward_det(
         return set_error(GSVC_ERR_WORKSPACE, "rasterize_sum_backward_det: missing radii or workspace");
     hipStream_t s = (hipStream_t)stream;
     if (num_points > 0 &&
-        hipMemsetAsync(grad_records, 0, sizeof(float) * 16 * (size_t)num_points, s) != hipSuccess)
+        dev_zero(grad_records, sizeof(float) * 16 * (size_t)num_points, s) != GSVC_OK)
         return set_error(GSVC_ERR_HIP, "rasterize_sum_backward_det: memset failed");
     const int ntiles = tbx * tby;
     if (ntiles == 0 || num_points == 0) return GSVC_OK;
@@ -1733,7 +1733,7 @@ extern "C" int gsvc_rasterize_sum_backward_det(
     det_offsets_launch(num_points, (const float2 *)xys, radii, tbx, tby, off, (int *)part,
                        9 * (size_t)det_capacity, s);
     if (det_capacity > 0 &&
-        hipMemsetAsync(part, 0, sizeof(float) * 9 * (size_t)det_capacity, s) != hipSuccess)
+        dev_zero(part, sizeof(float) * 9 * (size_t)det_capacity, s) != GSVC_OK)
         return set_error(GSVC_ERR_HIP, "rasterize_sum_backward_det: memset failed");
     sum_bwd_launch(s, tbx, (int)img_width, (int)img_height, ntiles, gaussian_ids_sorted,
                    (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacities, final_idx,
@@ -1741,7 +1741,7 @@ extern "C" int gsvc_rasterize_sum_backward_det(
     hipLaunchKernelGGL(det_gather_kernel, dim3(ceil_div(num_points, 256)), dim3(256), 0, s,
                        num_points, off, part, det_capacity, grad_records);
     if (pairs_out &&
-        hipMemcpyAsync(pairs_out, off + num_points, sizeof(int), hipMemcpyDeviceToDevice, s) != hipSuccess)
+        dev_copy(pairs_out, off + num_points, sizeof(int), s) != GSVC_OK)
         return set_error(GSVC_ERR_HIP, "rasterize_sum_backward_det: copy failed");
     return check_launch("rasterize_sum_backward_det");
 }

@@ -253,6 +253,7 @@ void slab_ws_ready(SlabWs &w, const Tensor &like, int ntiles) {
 }
 
 bool capturing(void *stream) {
+    if (stream == nullptr) return false;  // the legacy default stream never captures (errors.hip)
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     return hipStreamIsCapturing((hipStream_t)stream, &cs) == hipSuccess &&
            cs != hipStreamCaptureStatusNone;

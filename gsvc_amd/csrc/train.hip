@@ -1706,8 +1706,8 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
         if (carry) {
             // a new set of carried bins: counts and this frame's M from zero (a
             // previous step's splat kernel may have carried into them)
-            if (hipMemsetAsync(w.ccount, 0, sizeof(unsigned) * 2 * (size_t)ntiles, s) != hipSuccess ||
-                hipMemsetAsync(f.m_acc, 0, sizeof(int), s) != hipSuccess)
+            if (dev_zero(w.ccount, sizeof(unsigned) * 2 * (size_t)ntiles, s) != GSVC_OK ||
+                dev_zero(f.m_acc, sizeof(int), s) != GSVC_OK)
                 return set_error(GSVC_ERR_HIP, "train_step_sum: memset failed");
         }
         // a refreshing projection's sort runs after the step (off the loss's path)
@@ -1724,7 +1724,7 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
         det_offsets_launch(num_points, (const float2 *)w.f.xys, w.f.radii, tbx, tby, det_off,
                            (int *)det_part, det_capacity > 0 ? 8 * (size_t)det_capacity : 0, s);
         if (det_capacity > 0 &&
-            hipMemsetAsync(det_part, 0, sizeof(float4) * 2 * (size_t)det_capacity, s) != hipSuccess)
+            dev_zero(det_part, sizeof(float4) * 2 * (size_t)det_capacity, s) != GSVC_OK)
             return set_error(GSVC_ERR_HIP, "train_step_sum: memset failed");
         return check_launch("train_step_sum: det offsets");
     };
@@ -1900,8 +1900,8 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
             // the splat kernel's carry is superseded: counts and M from zero,
             // then the projection bins frame_index + 1 afresh (and re-zeroes the
             // gradient records)
-            if (hipMemsetAsync(w.ccount, 0, sizeof(unsigned) * 2 * (size_t)ntiles, s) != hipSuccess ||
-                hipMemsetAsync(fn.m_acc, 0, sizeof(int), s) != hipSuccess)
+            if (dev_zero(w.ccount, sizeof(unsigned) * 2 * (size_t)ntiles, s) != GSVC_OK ||
+                dev_zero(fn.m_acc, sizeof(int), s) != GSVC_OK)
                 return set_error(GSVC_ERR_HIP, "train_step_sum: memset failed");
             rc = frame_project_launch(num_points, xyz, 1, cholesky, cholesky_bound, features, rgb_w,
                                       nullptr, img_height, img_width, w.f, fn, w.grad, s, 1, nullptr, 0,

@@ -1,15 +1,13 @@
-"""Graph-capture probe of the counted binning (tests/test_capture.py debugging):
-capture gsvc_bin_tiles_counted on a torch graph in three variants, replay,
-and compare the bins with the eager call.
-  V1 workspace allocated inside the capture (ops.bin_tiles_counted)
-  V2 workspace allocated before the capture (static)
-  V3 V2 plus a captured torch zero_() of the workspace before the call"""
+"""Graph-capture probe of the counted binning (tests/test_capture.py debugging).
+E1: replays back to back (no eager launch between them), checked after.
+E2: a torch-only graph replayed with eager ops in between.
+E3: the binning graph, replay -> an eager torch op -> replay.
+E4: the binning graph, replay -> an eager call of our library -> replay."""
 import sys
 
 import torch
 
 sys.path.insert(0, ".")
-from gsvc_amd import _lib as L  # noqa: E402
 from gsvc_amd import ops  # noqa: E402
 
 dev = torch.device("cuda:0")
@@ -24,28 +22,11 @@ xys, depths, radii, conics, nth = ops.project_gaussians_2d_forward(n, means, Lc,
 torch.cuda.synchronize()
 e_gids, e_bins, e_meta = ops.bin_tiles_counted(n, xys, radii, tb, cap, 256)
 torch.cuda.synchronize()
-print("eager M", int(e_meta[0]), flush=True)
-
-ws_static = torch.empty((L.size("gsvc_bin_tiles_counted_workspace_bytes", nt) // 4 + 1,),
-                        dtype=torch.int32, device=dev)
-sc_static = torch.empty((cap,), dtype=torch.int32, device=dev)
+M = int(e_meta[0])
+print("eager M", M, flush=True)
 
 
-def v2(zero):
-    gids = torch.empty((cap,), dtype=torch.int32, device=dev)
-    bins = torch.empty((nt, 2), dtype=torch.int32, device=dev)
-    meta = torch.empty((2,), dtype=torch.int32, device=dev)
-    if zero:
-        ws_static.zero_()
-    L.call("gsvc_bin_tiles_counted", n, L.ptr(xys), L.ptr(radii), tb[0], tb[1], cap, 256,
-           L.ptr(sc_static), L.ptr(gids), L.ptr(bins), L.ptr(meta), L.ptr(ws_static),
-           4 * ws_static.numel(), L.stream(dev))
-    return gids, bins, meta
-
-
-variants = {"V1": lambda: ops.bin_tiles_counted(n, xys, radii, tb, cap, 256),
-            "V2": lambda: v2(False), "V3": lambda: v2(True)}
-for name, fn in variants.items():
+def capture(fn):
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
@@ -53,11 +34,59 @@ for name, fn in variants.items():
     torch.cuda.current_stream().wait_stream(side)
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
-        g_gids, g_bins, g_meta = fn()
-    res = []
-    for r in range(3):
-        graph.replay()
-        torch.cuda.synchronize()
-        res.append((int(g_meta[0]), torch.equal(g_bins, e_bins)))
-    print(name, res, flush=True)
-    del graph
+        out = fn()
+    return graph, out
+
+
+binfn = lambda: ops.bin_tiles_counted(n, xys, radii, tb, cap, 256)  # noqa: E731
+# E1
+graph, (gg, gb, gm) = capture(binfn)
+for _ in range(3):
+    graph.replay()
+torch.cuda.synchronize()
+print("E1 back-to-back x3:", int(gm[0]), torch.equal(gb, e_bins), flush=True)
+graph.replay()
+torch.cuda.synchronize()
+print("E1 4th:", int(gm[0]), torch.equal(gb, e_bins), flush=True)
+del graph
+# E2
+x = torch.arange(1000, device=dev, dtype=torch.float32)
+tg, y = capture(lambda: x * 2 + 1)
+res = []
+for _ in range(3):
+    tg.replay()
+    torch.cuda.synchronize()
+    res.append(bool(torch.equal(y, x * 2 + 1)))
+    _ = (x + 3).sum().item()
+print("E2 torch graph with eager ops between:", res, flush=True)
+# E3
+graph, (gg, gb, gm) = capture(binfn)
+res = []
+for _ in range(3):
+    graph.replay()
+    torch.cuda.synchronize()
+    res.append((int(gm[0]), bool(torch.equal(gb, e_bins))))
+    _ = (x + 3).sum().item()
+print("E3 eager torch op between:", res, flush=True)
+del graph
+# E4
+graph, (gg, gb, gm) = capture(binfn)
+res = []
+for _ in range(3):
+    graph.replay()
+    torch.cuda.synchronize()
+    res.append((int(gm[0]), bool(torch.equal(gb, e_bins))))
+    ops.bin_tiles_counted(n, xys, radii, tb, cap, 256)
+    torch.cuda.synchronize()
+print("E4 eager library call between:", res, flush=True)
+# E0: host cost of hipStreamIsCapturing through torch's HIP runtime, on the
+# default stream (handle 0) and on a created stream
+import ctypes  # noqa: E402
+import time  # noqa: E402
+hip = ctypes.CDLL(torch.__file__.rsplit("/", 1)[0] + "/lib/libamdhip64.so")
+st = ctypes.c_int(0)
+for name, h in (("default", torch.cuda.current_stream().cuda_stream), ("side", torch.cuda.Stream().cuda_stream)):
+    t0 = time.perf_counter()
+    for _ in range(2000):
+        hip.hipStreamIsCapturing(ctypes.c_void_p(h), ctypes.byref(st))
+    print(f"E0 hipStreamIsCapturing({name}, handle {h}): {(time.perf_counter() - t0) / 2000 * 1e6:.2f} us", flush=True)

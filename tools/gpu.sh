@@ -62,7 +62,7 @@ steps)
 tests)
   run tests 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread "$@" ;;
 bench_pmc)
-  for wl in train50k render10k decode8; do
+  for wl in train50k render10k decode8 oppath alpha50k; do
     run "$wl.trace" 200 rocprofv3 --kernel-trace --stats -d "$OUT/$wl/trace" -o t --output-format csv -- python3 tools/pmc_workloads.py $wl
     pmc "$wl/fetch" FETCH_SIZE -- python3 tools/pmc_workloads.py $wl
     pmc "$wl/write" WRITE_SIZE -- python3 tools/pmc_workloads.py $wl
@@ -72,6 +72,8 @@ bench_pmc)
   done
   python3 tools/prof_summary.py --trace $OUT/render10k/trace --fetch $OUT/render10k/fetch --write $OUT/render10k/write --last 50 --out $OUT/pmc_traffic.json --key render_10000 > $OUT/render_10000.txt
   python3 tools/prof_summary.py --trace $OUT/decode8/trace --fetch $OUT/decode8/fetch --write $OUT/decode8/write --last 50 --out $OUT/pmc_traffic.json --key video_decode > $OUT/video_decode.txt
+  python3 tools/prof_summary.py --trace $OUT/oppath/trace --fetch $OUT/oppath/fetch --write $OUT/oppath/write --last 50 --out $OUT/pmc_traffic.json --key op_path > $OUT/op_path.txt
+  python3 tools/prof_summary.py --trace $OUT/alpha50k/trace --fetch $OUT/alpha50k/fetch --write $OUT/alpha50k/write --last 50 --out $OUT/pmc_traffic.json --key alpha_50000 > $OUT/alpha_50000.txt
   cat $OUT/pmc_traffic.json ;;
 pmc_valu)
   pmc valu SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAVES -- python3 tools/pmc_workloads.py train50k

@@ -6,7 +6,11 @@
              --iters renders of the trained model (configs[2] render);
   render10k  --iters renders of a random-init 10k-splat frame (configs[1]);
   decode8    --iters batched renders of a GOP of 8 distinct 10k-splat frame
-             models (bench.py ``video_decode``: one gsvc_render_frames_sum call).
+             models (bench.py ``video_decode``: one gsvc_render_frames_sum call);
+  oppath     train50k's trained state, then --iters forward + backward calls of
+             the unchanged-caller op path (bench.py ``op_path``);
+  alpha50k   --iters forward + backward calls of the alpha operators at 1080p /
+             50k, opacity U(0.1, 1) (bench.py ``alpha``).
 
 Summaries take each kernel's last --iters dispatches (tools/prof_summary.py
 --last), i.e. the trained state.
@@ -23,7 +27,7 @@ import torch  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["train50k", "render10k", "decode8"])
+    ap.add_argument("mode", choices=["train50k", "render10k", "decode8", "oppath", "alpha50k"])
     ap.add_argument("--settle", type=int, default=2000)
     ap.add_argument("--iters", type=int, default=50)
     a = ap.parse_args()
@@ -44,12 +48,43 @@ def main():
         torch.cuda.synchronize()
         print("done", a.mode, flush=True)
         return
-    if a.mode == "train50k":
+    if a.mode == "alpha50k":
+        from gsplat.project_gaussians_2d import project_gaussians_2d
+        from gsplat.rasterize import rasterize_gaussians
+        n = 50000
+        g = torch.Generator().manual_seed(n)  # bench.py alpha_block's inputs
+        ps = [torch.tanh(torch.atanh(2 * (torch.rand(n, 2, generator=g) - 0.5))),
+              torch.rand(n, 3, generator=g) + torch.tensor([0.5, 0, 0.5]),
+              torch.rand(n, 3, generator=g), 0.1 + 0.9 * torch.rand(n, 1, generator=g)]
+        ps = [p.to(dev).requires_grad_(True) for p in ps]
+        bg = torch.ones(3, device=dev)
+        tb = ((W + 15) // 16, (H + 15) // 16, 1)
+        for _ in range(a.iters + 5):
+            xys, depths, radii, conics, nth = project_gaussians_2d(ps[0], ps[1], H, W, tb)
+            out = rasterize_gaussians(xys, depths, radii, conics, nth, ps[2], ps[3], H, W, 16, 16,
+                                      background=bg)
+            torch.autograd.grad(out.sum(), ps)
+        torch.cuda.synchronize()
+        print("done", a.mode, flush=True)
+        return
+    if a.mode in ("train50k", "oppath"):
         model = make_frame_model(H, W, 50000, dev, seed=1000)
         gt = synthetic_gt(H, W, 8, "cpu").to(dev)
         for it in range(1, a.settle + a.iters + 1):
             model.train_iter(gt, it)
         model.eval()
+        if a.mode == "oppath":  # GSVC's own op sequence over the drop-in, on the trained frame
+            import torch.nn.functional as F
+            op = make_frame_model(H, W, 50000, dev, seed=0, fused_train=False, fused_render=False)
+            with torch.no_grad():
+                for k in ("_xyz", "_cholesky", "_features_dc"):
+                    getattr(op, k).copy_(getattr(model, k))
+            for _ in range(a.iters + 5):
+                img = op.forward()["render"]
+                F.mse_loss(img.squeeze(0), gt.squeeze(0)).backward()
+            torch.cuda.synchronize()
+            print("done", a.mode, flush=True)
+            return
     else:
         model = make_frame_model(H, W, 10000, dev, seed=1000)
         model.eval()

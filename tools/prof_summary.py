@@ -29,7 +29,9 @@ KERNELS = {"raster_sum_fwd_kernel": "rasterize_sum_forward",
            "raster_sum_bwd_kernel": "rasterize_sum_backward",
            "train_tile_kernel": "train_tile",
            "train_splat_kernel": "train_splat",
-           "frame_project_kernel": "frame_project"}
+           "frame_project_kernel": "frame_project",
+           "raster_alpha_fwd_kernel": "alpha_forward",
+           "raster_alpha_bwd_kernel": "alpha_backward"}
 
 
 def _short(name):
