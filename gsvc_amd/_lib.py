@@ -26,7 +26,8 @@ import torch  # noqa: F401  (loads torch's libamdhip64 first; the library reuses
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libgsvc_amd.so")
-DIAG_LIB_PATH = os.path.join(_HERE, "lib", "libgsvc_amd_diag.so")
+# GSVC_DIAG_LIB: another build of the diagnostic library (tools' A/B of two builds)
+DIAG_LIB_PATH = os.environ.get("GSVC_DIAG_LIB") or os.path.join(_HERE, "lib", "libgsvc_amd_diag.so")
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int

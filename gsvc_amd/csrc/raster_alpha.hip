@@ -15,13 +15,11 @@
 // wave leaves the tile when every lane's 4 pixels are done; chunks of more
 // than 24 entries are walked through lane-group lists (cull.h).
 // Backward: the transmittance recursion runs per pixel from the back, so it
-// is PIXEL-parallel: 256 threads = 256 pixels; per entry each wave sums its 9
-// partial gradients per 16-lane row with DPP adds (4 VALU each, no LDS
-// permutes), the rows' last lanes add them to an LDS record with LDS float
-// atomics (16 rows), and once per 256-entry chunk the tile's records go to HBM
-// as one 64-byte atomic request per (splat, tile).
+// is pixel-parallel: one wave per tile, 4 pixels per lane, per entry the
+// pixels' terms reduced as row sums by DPP into one lane (see the kernel).
 #include "common.h"
 #include "cull.h"
+#include "rows.h"
 
 namespace gsvc {
 
@@ -168,15 +166,213 @@ __device__ __forceinline__ float row_sum16(float v) {
     v = dpp_add<0x141>(v);  // row_half_mirror
     return dpp_add<0x140>(v);  // row_mirror
 }
-
-__device__ __forceinline__ float wave_sum_shfl(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+__device__ __forceinline__ float quad_sum(float v) { return dpp_add<0x4e>(dpp_add<0xb1>(v)); }
+// every 16-lane row holding its total in each lane: lane 63 ends with the sum
+// of the four rows (row_bcast:15 into rows 1 and 3, row_bcast:31 into 2 and 3)
+__device__ __forceinline__ float rows_to_last(float v) {
+    v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xa, 0xf, false));
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xc, 0xf, false));
 }
 
-template <bool kDpp>
-__global__ __launch_bounds__(256) void raster_alpha_bwd_kernel(
+// Backward (backward.cu:138-315), round 5: ONE wave per tile, 4 pixels of one
+// row per lane (the forward's layout), each pixel's back-to-front recursion
+// (T = T_final rolled back through every valid entry's 1 / (1 - alpha), the
+// colour buffer, v_alpha) kept in the lane.  Per entry the lane sums its 4
+// pixels' terms as 7 row sums -- S_k = sum v_sigma dx^k (k = 0, 1, 2: v_xy and
+// v_conic factor by the row's constant dy), alpha T v_out (3), vis v_alpha --
+// the 4 lanes of a tile row (a DPP quad) add them, the row's 9 gradient terms
+// are formed, and the 16 rows are added by DPP (half-row / row mirrors, row
+// broadcasts) into lane 63, which keeps the entry's 9 sums in LDS; once per
+// 64-entry chunk they go to the splat's record, one 64-byte atomic request per
+// (splat, tile).  An entry no pixel of the tile takes costs no sums.
+// Round 4's kernel (256 threads = 256 pixels, per entry and wave 9 DPP row
+// sums and LDS float atomics: 111 us at 1080p / 50k) stays in the diagnostic
+// library as raster_alpha_bwd_kernel_r4 (A/B knob 9 = 1).
+// kAbl (diagnostic library, A/B knob 30, wrong results): bit 0 no per-entry
+// sums, bit 1 no pixel work
+template <int kAbl = 0>
+__global__ __launch_bounds__(64, 5) void raster_alpha_bwd_kernel(
+    int tbx, int img_w, int img_h, int ntiles, const int *__restrict__ ids,
+    const int2 *__restrict__ bins, const float2 *__restrict__ xys, const float *__restrict__ conics,
+    const float *__restrict__ colors, const float *__restrict__ opac, const float *__restrict__ bg,
+    const float *__restrict__ final_Ts, const int *__restrict__ final_idx,
+    const float *__restrict__ v_out, const float *__restrict__ v_out_alpha,
+    float *__restrict__ grad) {
+    __shared__ float4 s_geo[kAChunk];  // x, y, a, b
+    __shared__ float4 s_col[kAChunk];  // c, opacity, r, g
+    __shared__ float s_blu[kAChunk];
+    __shared__ int s_gid[kAChunk];
+    __shared__ unsigned short s_ro[kAChunk];
+    __shared__ float s_row[8][kTile][8];  // a group's 8 entries: per tile row its 7 sums
+    __shared__ float s_acc[9][8];         // the group's entry sums
+    const int tile = xcd_remap(blockIdx.x, ntiles);
+    const int ty = tile / tbx, tx = tile - ty * tbx;
+    const int lane = threadIdx.x;
+    const int pi = ty * kTile + (lane >> 2);
+    const int pj = tx * kTile + ((lane & 3) << 2);
+    const float py = (float)pi;
+    const float ox = (float)(tx * kTile), oy = (float)(ty * kTile);
+    const unsigned lrow = (unsigned)(lane >> 2), lc0 = (unsigned)((lane & 3) << 2);
+    // per pixel: T (rolled back), v_out, BV = buffer . v_out (the colour
+    // buffer only ever enters v_alpha through this dot product, so the buffer
+    // is kept as it: BV += fac (c . v_out)), TK = T_final (v_out_alpha - bg .
+    // v_out) -- backward.cu:248-266's v_alpha regrouped as
+    // T (c . v_out) + (TK - BV) / (1 - alpha)
+    const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
+    float T[4], BV[4], TK[4];
+    float3 vo3[4];
+    int bf[4];
+    int fmax = -2147483647 - 1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const bool in = pi < img_h && pj + q < img_w;
+        const size_t p = in ? (size_t)pi * (size_t)img_w + (size_t)(pj + q) : 0;
+        const float tf = in ? final_Ts[p] : 1.0f;
+        bf[q] = in ? final_idx[p] : (-2147483647 - 1);  // outside the image: never valid
+        const float3 v = in ? make_float3(v_out[3 * p], v_out[3 * p + 1], v_out[3 * p + 2])
+                            : make_float3(0.f, 0.f, 0.f);
+        const float va = in ? v_out_alpha[p] : 0.f;
+        vo3[q] = v;
+        T[q] = tf;
+        BV[q] = 0.f;
+        TK[q] = tf * (va - fmaf(bg2, v.z, fmaf(bg1, v.y, bg0 * v.x)));
+        fmax = max(fmax, bf[q]);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) fmax = max(fmax, __shfl_xor(fmax, off, 64));
+    const int2 range = bins[tile];
+    // entries past every pixel's final index are never valid (backward.cu:226-230)
+    const int kend = min(range.y, fmax == (-2147483647 - 1) ? fmax : fmax + 1);
+
+    // chunks of <= 64 entries, back to front; within a chunk, groups of 8
+    for (int ce = kend; ce > range.x; ce -= kAChunk) {
+        const int cs = max(range.x, ce - kAChunk);
+        const int n = ce - cs;
+        if (lane < n) {
+            const int g = ids[cs + lane];
+            s_gid[lane] = g;
+            const float2 xy = xys[g];
+            s_geo[lane] = make_float4(xy.x, xy.y, conics[3 * g], conics[3 * g + 1]);
+            s_col[lane] = make_float4(conics[3 * g + 2], opac[g], colors[3 * g], colors[3 * g + 1]);
+            s_blu[lane] = colors[3 * g + 2];
+            // the pixels where alpha >= 1/255 is reachable (a pair outside
+            // is never valid in the reference either)
+            s_ro[lane] = (unsigned short)ellipse_rect(xy.x, xy.y, conics[3 * g], conics[3 * g + 1],
+                                                      conics[3 * g + 2], opac[g], ox, oy);
+        }
+        __syncthreads();
+        for (int g0 = ((n - 1) >> 3) << 3; g0 >= 0; g0 -= 8) {
+            const int g1 = min(g0 + 8, n);  // this group: entries [g0, g1), walked back to front
+            for (int t = g1 - 1; t >= g0; --t) {
+                const unsigned rc = s_ro[t];
+                // the lane's 4 pixels against the rectangle: none -> no pixel work
+                const bool lin = rc != kNoRect && lrow >= ((rc >> 8) & 15u) &&
+                                 lrow <= ((rc >> 12) & 15u) && lc0 + 3u >= (rc & 15u) &&
+                                 lc0 <= ((rc >> 4) & 15u);
+                const int k = lin ? cs + t : 0x7fffffff;
+                const float4 G = s_geo[t], C = s_col[t];
+                const float blu = s_blu[t];
+                const float dy = G.y - py;
+                const float ha = 0.5f * G.z, hc = 0.5f * C.x;
+                float sr = 0.f, sg = 0.f, sb = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f, so = 0.f;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (kAbl & 2) continue;
+                    if (k > bf[q]) continue;
+                    const float dx = G.x - (float)(pj + q);
+                    const float sgm = splat_sigma_h(ha, G.w, hc, dx, dy);
+                    const float vis = exp_neg(sgm);
+                    const float al = fminf(0.99f, C.y * vis);
+                    if (sgm < 0.0f || al < kAlphaMin) continue;
+                    // the reference's 1.f / (1.f - alpha) under --use_fast_math is the
+                    // hardware reciprocal (rcp.approx), as here (v_rcp_f32, ~1 ulp)
+                    const float ra = __builtin_amdgcn_rcpf(1.0f - al);
+                    const float3 vo = vo3[q];
+                    T[q] = T[q] * ra;
+                    const float fac = al * T[q];
+                    const float cvo = fmaf(blu, vo.z, fmaf(C.w, vo.y, C.z * vo.x));  // c . v_out
+                    const float v_alpha = fmaf(T[q], cvo, ra * (TK[q] - BV[q]));
+                    BV[q] = fmaf(fac, cvo, BV[q]);
+                    const float v_sigma = (-C.y * vis) * v_alpha;
+                    sr = fmaf(fac, vo.x, sr);
+                    sg = fmaf(fac, vo.y, sg);
+                    sb = fmaf(fac, vo.z, sb);
+                    s0 += v_sigma;
+                    const float vdx = v_sigma * dx;
+                    s1 += vdx;
+                    s2 = fmaf(vdx, dx, s2);
+                    so = fmaf(vis, v_alpha, so);
+                }
+                if (kAbl & 1) continue;
+                // a quad is one tile row: its 7 sums into the row's slot
+                s0 = quad_sum(s0);
+                s1 = quad_sum(s1);
+                s2 = quad_sum(s2);
+                sr = quad_sum(sr);
+                sg = quad_sum(sg);
+                sb = quad_sum(sb);
+                so = quad_sum(so);
+                if ((lane & 3) == 0) {
+                    float *r = &s_row[t & 7][lrow][0];
+                    *reinterpret_cast<float4 *>(r) = make_float4(s0, s1, s2, so);
+                    *reinterpret_cast<float4 *>(r + 4) = make_float4(sr, sg, sb, 0.f);
+                }
+            }
+            __syncthreads();
+            // the group's sums over the tile's 16 rows: lane = (entry te, rows
+            // 2 rr, 2 rr + 1); the row's 9 terms (dy constant along it), then
+            // the entry's 8 lanes by DPP into lane 8 te
+            {
+                const int te = lane >> 3, rr = (lane & 7) << 1;
+                const int t = g0 + te;
+                float gs[9];
+#pragma unroll
+                for (int c = 0; c < 9; ++c) gs[c] = 0.f;
+                if (t < g1) {
+                    const float4 G = s_geo[t], C = s_col[t];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const float *r = &s_row[t & 7][rr + h][0];
+                        const float4 a = *reinterpret_cast<const float4 *>(r);
+                        const float4 b = *reinterpret_cast<const float4 *>(r + 4);
+                        const float dy = G.y - (oy + (float)(rr + h));
+                        gs[0] += fmaf(G.z, a.y, (G.w * dy) * a.x);  // v_xy.x: sum v_sigma (a dx + b dy)
+                        gs[1] += fmaf(G.w, a.y, (C.x * dy) * a.x);  // v_xy.y: sum v_sigma (b dx + c dy)
+                        gs[2] += 0.5f * a.z;                       // v_conic: 1/2 sum v_sigma (dx^2, dx dy, dy^2)
+                        gs[3] += (0.5f * dy) * a.y;
+                        gs[4] += ((0.5f * dy) * dy) * a.x;
+                        gs[5] += b.x;
+                        gs[6] += b.y;
+                        gs[7] += b.z;
+                        gs[8] += a.w;
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < 9; ++c) gs[c] = dpp_add<0x141>(quad_sum(gs[c]));  // 8 lanes
+                if ((lane & 7) == 0 && t < g1) {
+#pragma unroll
+                    for (int c = 0; c < 9; ++c) s_acc[c][te] = gs[c];
+                }
+            }
+            __syncthreads();
+            // 16 lanes per entry, 9 of them add one sum each into the splat's
+            // 64-byte record: one memory request per (splat, tile)
+            for (int q = lane; q < (g1 - g0) * 16; q += 64) {
+                const int e = q >> 4, c = q & 15;
+                if (c < 9) unsafeAtomicAdd(grad + (size_t)s_gid[g0 + e] * 16 + c, s_acc[c][e]);
+            }
+            __syncthreads();
+        }
+    }
+}
+
+#ifdef GSVC_DIAG
+// Round 4's backward (diagnostic library, A/B knob 9 = 1): pixel-parallel, 256
+// threads = 256 pixels; per entry each wave sums its 9 partial gradients per
+// 16-lane row with DPP adds, the rows' last lanes add them to an LDS record
+// with LDS float atomics, and once per 256-entry chunk the tile's records go
+// to HBM as one 64-byte atomic request per (splat, tile).
+__global__ __launch_bounds__(256) void raster_alpha_bwd_kernel_r4(
     int tbx, int img_w, int img_h, int ntiles, const int *__restrict__ ids,
     const int2 *__restrict__ bins, const float2 *__restrict__ xys, const float *__restrict__ conics,
     const float *__restrict__ colors, const float *__restrict__ opac, const float *__restrict__ bg,
@@ -280,19 +476,11 @@ __global__ __launch_bounds__(256) void raster_alpha_bwd_kernel(
             // last lane of each row adds its row's sums into the entry's LDS
             // accumulator (the row order of these adds is not fixed: float
             // atomics, as the reference's warp sums + atomicAdd)
-            if (kDpp) {
+            {
                 const float gs[9] = {row_sum16(g_x), row_sum16(g_y), row_sum16(g_c0),
                                      row_sum16(g_c1), row_sum16(g_c2), row_sum16(g_r),
                                      row_sum16(g_g), row_sum16(g_b), row_sum16(g_o)};
                 if ((lane & 15) == 15) {
-#pragma unroll
-                    for (int c = 0; c < 9; ++c) atomicAdd(&s_acc[t][c], gs[c]);
-                }
-            } else {  // A/B (knob 9 = 1): butterfly shuffles over the wave
-                const float gs[9] = {wave_sum_shfl(g_x), wave_sum_shfl(g_y), wave_sum_shfl(g_c0),
-                                     wave_sum_shfl(g_c1), wave_sum_shfl(g_c2), wave_sum_shfl(g_r),
-                                     wave_sum_shfl(g_g), wave_sum_shfl(g_b), wave_sum_shfl(g_o)};
-                if (lane == 0) {
 #pragma unroll
                     for (int c = 0; c < 9; ++c) atomicAdd(&s_acc[t][c], gs[c]);
                 }
@@ -306,6 +494,8 @@ __global__ __launch_bounds__(256) void raster_alpha_bwd_kernel(
         __syncthreads();
     }
 }
+
+#endif
 
 }  // namespace gsvc
 
@@ -356,15 +546,27 @@ extern "C" int gsvc_rasterize_backward(unsigned img_height, unsigned img_width, 
     const int tbx = ceil_div((int)img_width, kTile), tby = ceil_div((int)img_height, kTile);
     const int ntiles = tbx * tby;
     if (ntiles == 0 || num_points == 0) return GSVC_OK;
-    auto bwd = raster_alpha_bwd_kernel<true>;  // per-row DPP sums
-    if constexpr (kDiag)
-        if (knob(9) == 1) bwd = raster_alpha_bwd_kernel<false>;  // A/B: the shuffle butterflies
     hipEvent_t tev[2];
     const int tslot = timing_begin(s, tev, kTimingAlphaBwd);
-    launch_timed(bwd, dim3(ntiles), dim3(256), 0, s, tev, tbx, (int)img_width, (int)img_height,
-                 ntiles, gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys, conics,
-                 colors, opacities, background, final_Ts, final_idx, v_output, v_output_alpha,
-                 grad_records);
+#ifdef GSVC_DIAG
+    if (knob(9) == 1) {  // A/B: round 4's 256-thread kernel
+        launch_timed(raster_alpha_bwd_kernel_r4, dim3(ntiles), dim3(256), 0, s, tev, tbx,
+                     (int)img_width, (int)img_height, ntiles, gaussian_ids_sorted,
+                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacities,
+                     background, final_Ts, final_idx, v_output, v_output_alpha, grad_records);
+        timing_end(s, tslot, kTimingAlphaBwd);
+        return check_launch("rasterize_backward");
+    }
+#endif
+    auto bwd = raster_alpha_bwd_kernel<0>;
+    if constexpr (kDiag) {
+        if (knob(30) == 1) bwd = raster_alpha_bwd_kernel<1>;
+        if (knob(30) == 2) bwd = raster_alpha_bwd_kernel<2>;
+    }
+    launch_timed(bwd, dim3(ntiles), dim3(64), 0, s, tev, tbx, (int)img_width,
+                 (int)img_height, ntiles, gaussian_ids_sorted, (const int2 *)tile_bins,
+                 (const float2 *)xys, conics, colors, opacities, background, final_Ts, final_idx,
+                 v_output, v_output_alpha, grad_records);
     timing_end(s, tslot, kTimingAlphaBwd);
     return check_launch("rasterize_backward");
 }
