@@ -317,12 +317,17 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
             // <= 64 slab records in fill order: staged at their rank by id
         float4 geo = spec0, col = spec1, bx = spec2;
         if (lane >= spec_slots && lane < cnt) {
-            // slab records at their slot, or (id slabs, no head) the record of
-            // the lane's id gathered from A.rec -- the same 48 bytes
-            const float4 *r = seg_head ? slot_rec(seg_head, seg_rec, lane) : A.rec + 3 * (size_t)spec_id;
-            geo = r[0];
-            col = r[1];
-            bx = r[2];
+            if (seg_head || A.rec) {
+                // slab records at their slot, or (id slabs, no head) the record of
+                // the lane's id gathered from A.rec -- the same 48 bytes
+                const float4 *r = seg_head ? slot_rec(seg_head, seg_rec, lane) : A.rec + 3 * (size_t)spec_id;
+                geo = r[0];
+                col = r[1];
+                bx = r[2];
+            } else {  // the op path: the lane's id's inputs
+                load_splat(A, spec_id, geo, col, bx.x);
+                bx.y = __int_as_float(spec_id);
+            }
         }
         const int id = lane < cnt ? __float_as_int(bx.y) : 0x7fffffff;
         // rank by id: the ids through LDS (the lists' bytes, free until the
@@ -332,11 +337,19 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         s_rid[lane] = id;
         wave_lds_sync();
         int rank = 0;
-        for (int k = 0; k < cnt; k += 4) {
-            const int4 q = *reinterpret_cast<const int4 *>(s_rid + k);
-            rank += (q.x < id ? 1 : 0) + (q.y < id ? 1 : 0) + (q.z < id ? 1 : 0) + (q.w < id ? 1 : 0);
+        if (kDiag && A.norank) {  // A/B only: slot order (the sums' order then follows the atomics)
+            rank = lane;
+        } else {
+            for (int k = 0; k < cnt; k += 4) {
+                const int4 q = *reinterpret_cast<const int4 *>(s_rid + k);
+                rank += (q.x < id ? 1 : 0) + (q.y < id ? 1 : 0) + (q.z < id ? 1 : 0) + (q.w < id ? 1 : 0);
+            }
         }
         wave_lds_sync();
+        if (A.bins_out) {  // the op path: the tile's ids in id order and its bins, for the backward
+            if (lane < cnt) A.ids_rw[(size_t)tile * kTilePix + rank] = id;
+            if (lane == 0) A.bins_out[tile] = make_int2(range.x, range.x + cnt);
+        }
         if (!kIdx) cut = A.cut && __ballot(lane < cnt && !entry_cut_ok(geo, col, bx.x)) == 0ull;
         if (lane < cnt) {
             s_geo[rank] = geo;
@@ -672,8 +685,9 @@ __global__ __launch_bounds__(kMode == kModeSparse || kMode == kModeSparseStamp |
 raster_sum_fwd_kernel(SumFwdArgs A) {
     constexpr bool kOneWave = kMode == kModeSparse || kMode == kModeSparseStamp || kMode == kModeSparsePrio ||
                               kMode == kModeSparseIds;
-    // id slabs: the op path's autograd forward (kIdx) and the render A/B mode
-    constexpr bool kIds = kIdx || kMode == kModeSparseIds;
+    // id slabs: the op path's autograd forward (kIdx, or sparse / banded
+    // without final_idx) and the single-frame render
+    constexpr bool kIds = kIdx || kMode == kModeSparseIds || kMode == kModeBanded;
     __shared__ float4 s_buf[kOneWave ? 1 : 2][kSlice];
     __shared__ int s_ids[1][kTilePix];  // the tile's sorted ids (one copy per tile)
     // raised wave priority over the staging (loads, ranking, lists): the
@@ -756,9 +770,12 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         seg.ids = A.ids_rw + (size_t)tile * kTilePix;
         seg.recs = nullptr;
         seg.head = nullptr;
-        // render, <= 64 entries: records gathered by id and ranked straight
-        // into the staging, as the slab records are (sum_fwd_sparse)
-        if (kMode == kModeSparseIds && n_all <= kChunk) seg_rec = A.rec;
+        // <= 64 entries: records gathered by id and ranked straight into the
+        // staging, as the slab records are (sum_fwd_sparse) -- the render's
+        // packed records (A.rec), or the op path's inputs (seg_rec then only
+        // flags the path: sum_fwd_sparse gathers from xys / conics / colours)
+        if (kMode == kModeSparseIds && n_all <= kChunk)
+            seg_rec = A.rec ? A.rec : reinterpret_cast<const float4 *>(A.xys);
     } else {
         range = A.bins[tile];
         n_all = range.y - range.x;
@@ -787,7 +804,9 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
             n = ((A.slab || (kIds && A.id_counts)) && n_all > kTilePix)
                     ? wave_brute_tile_ids(A, tile, s_ids[0])
                     : wave_sorted_tile_ids(seg, n_all, s_ids[0], reinterpret_cast<unsigned *>(s_buf[0]));
-        if (kIdx && A.id_counts) write_sorted_ids(A, tile, range.x, n, s_ids[0]);
+        // the op path: the tile's sorted ids and bins for the backward (a tile
+        // staged straight from its id slab writes them in sum_fwd_sparse)
+        if (A.bins_out && A.id_counts && !seg_rec) write_sorted_ids(A, tile, range.x, n, s_ids[0]);
         sum_fwd_sparse<kMode, kIdx>(A, tile, range, n, s_buf[0], init, by_ids, s_ids[0], seg_rec,
                                     seg.head, spec0, spec1, spec2, seg.head ? A.spec_slots : 0,
                                     spec_id);
@@ -806,7 +825,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
             }
             __syncthreads();
             n = s_n;
-            if (kIdx && A.id_counts && w == 0) write_sorted_ids(A, tile, range.x, n, s_ids[0]);
+            if (A.bins_out && A.id_counts && w == 0) write_sorted_ids(A, tile, range.x, n, s_ids[0]);
         }
         if (ty * kTile + w * 8 >= A.img_h) return;  // band below the image
         sum_fwd_band<kMode, kIdx>(A, tile, w, range, n, s_buf[w], init, by_ids, s_ids[0], seg_rec,
@@ -1369,6 +1388,7 @@ void sum_fwd_args_init(SumFwdArgs &A) {
     A.spec_slots = knob(10) > 0 && knob(10) < kHeadSlots ? knob(10) : kHeadSlots;
     A.group_min = knob(15) > 0 ? knob(15) - 1 : kGroupMinDefault;
     A.cut = knob(19) != 1;
+    A.norank = knob(31) == 1;
     A.layout = kLayoutHWC;
     A.frames = 1;
 }
@@ -1393,7 +1413,10 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
     int mode = knob(0);
     if (mode == 0) mode = sum_forward_dense(density_hint, ntiles, A.frames) ? kModeBanded : kModeSparse;
     if (knob(17) == 1 && mode == kModeSparse) mode = kModeSparsePrio;  // A/B knob 17
-    if (A.id_counts && !A.final_idx) mode = kModeSparseIds;  // render over id slabs: one instance
+    // id slabs without final_idx (the render; the op path's forward, whose
+    // backward needs no final_idx): the one-wave id-slab instance, or the
+    // banded kernel for a dense op-path frame
+    if (A.id_counts && !A.final_idx && mode != kModeBanded) mode = kModeSparseIds;
     if (mode == kModeStamp && A.layout != kLayoutHWC)
         return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: stamp mode needs the HWC layout");
     if (A.frames > 1 && (mode == kModeStamp || mode == kModeSparseStamp))
@@ -1523,7 +1546,7 @@ static int forward_slabs_impl(
     const int ntiles = tbx * tby;
     if (!workspace || workspace_bytes < gsvc_rasterize_sum_slabs_workspace_bytes(ntiles))
         return set_error(GSVC_ERR_WORKSPACE, "rasterize_sum_forward_slabs: workspace too small");
-    if (!gaussian_ids || !tile_bins || !meta || !out_img || !final_idx || !background ||
+    if (!gaussian_ids || !tile_bins || !meta || !out_img || !background ||
         (num_points > 0 && (!xys || !radii || !conics || !colors || !opacities)))
         return set_error(GSVC_ERR_ARG, "rasterize_sum_forward_slabs: missing input");
     hipStream_t s = (hipStream_t)stream;

@@ -281,7 +281,9 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
         const auto i = f.dtype(at::kInt);
         void *st = stream_of(xys);
         Tensor gids = at::empty({(int64_t)nt * kTileKeep}, i), bins = at::empty({nt, 2}, i);
-        Tensor meta = at::empty({2}, i), out = at::empty({H, W, 3}, f), idx = at::empty({H, W}, i);
+        // no final_idx: the backward (raster_sum_bwd_kernel) does not read it --
+        // an entry past a pixel's final index fails the alpha test there anyway
+        Tensor meta = at::empty({2}, i), out = at::empty({H, W, 3}, f);
         Tensor rec;
         if (capturing(st)) {
             // Graph capture: the slab workspace's parity is host state a replay
@@ -303,7 +305,7 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
                                                 ip(gids), ip(bins), fp(xys), fp(conics), fp(colors),
                                                 fp(opacity), fp(background), ip(meta),
                                                 hint_cached(xys.device().index()), 0, fp(out),
-                                                nullptr, ip(idx), st),
+                                                nullptr, nullptr, st),
                   "gsvc_rasterize_sum_forward_ex");
         } else {
             rec = need_grad ? at::empty({n, 16}, f) : Tensor();
@@ -315,7 +317,7 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
             const int rc = gsvc_rasterize_sum_forward_slabs_ordered(
                 (int)n, fp(xys), ip(radii), fp(conics), fp(colors), fp(opacity), fp(background),
                 (unsigned)H, (unsigned)W, ws.calls, hint, ws.buf.data_ptr(),
-                4 * (size_t)ws.buf.numel(), ip(gids), ip(bins), ip(meta), fp(rec), fp(out), ip(idx),
+                4 * (size_t)ws.buf.numel(), ip(gids), ip(bins), ip(meta), fp(rec), fp(out), nullptr,
                 st, oflags ? ws.order.data_ptr() : nullptr, oflags ? (size_t)ws.order.numel() : 0,
                 oflags);
             if (rc != 0) ws.tiles = -1;  // counters and order in an unknown state: rebuild
@@ -325,7 +327,7 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
             hint_refresh(meta, st);
         }
         Tensor m_dev = meta.narrow(0, 0, 1);
-        ctx->save_for_backward({gids, bins, xys, conics, colors, opacity, idx});
+        ctx->save_for_backward({gids, bins, xys, conics, colors, opacity});
         ctx->set_materialize_grads(false);  // M's gradient (always undefined): no fill
         ctx->saved_data["rec"] = rec;  // zeroed: the first backward adds into it
         ctx->saved_data["H"] = H;
@@ -337,7 +339,7 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
     static variable_list backward(AutogradContext *ctx, variable_list g) {
         const auto s = ctx->get_saved_variables();
         const Tensor &gids = s[0], &bins = s[1], &xys = s[2], &conics = s[3], &colors = s[4];
-        const Tensor &opacity = s[5], &idx = s[6];
+        const Tensor &opacity = s[5];
         const int64_t H = ctx->saved_data["H"].toInt(), W = ctx->saved_data["W"].toInt();
         const int64_t n = xys.size(0);
         // the gradient at its own strides (after GSVC's clamp + permute it
@@ -357,7 +359,7 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
         }
         check(gsvc_rasterize_sum_backward_zeroed_strided(
                   (unsigned)H, (unsigned)W, (int)n, ip(gids), ip(bins), fp(xys), fp(conics),
-                  fp(colors), fp(opacity), ip(idx), v_out.data_ptr<float>(), v_out.stride(0),
+                  fp(colors), fp(opacity), nullptr, v_out.data_ptr<float>(), v_out.stride(0),
                   v_out.stride(1), v_out.stride(2), fp(rec), stream_of(xys)),
               "gsvc_rasterize_sum_backward_zeroed_strided");
         Tensor v_opac = rec.narrow(1, 8, 1);

@@ -295,7 +295,8 @@ int gsvc_rasterize_sum_forward_ex(
  * reference's stable sort of (tile << 32 | depth 0) keys gives -- blends them
  * and writes them back sorted: gaussian_ids [T * 256] (tile t's at t * 256)
  * and tile_bins [T, 2] = [t * 256, t * 256 + n) are then the inputs of the
- * backward, final_idx (required) indexes gaussian_ids.  meta[0] <- M (device), meta[1] <-
+ * backward.  final_idx (optional; NULL: not written -- the backward below
+ * does not read it) indexes gaussian_ids.  meta[0] <- M (device), meta[1] <-
  * 0; M < 1 renders the background (rasterize_sum.py:121-127).
  * grad_records_zero (optional, [N, 16]) is zeroed for
  * gsvc_rasterize_sum_backward_zeroed.  workspace: the first
@@ -326,7 +327,11 @@ int gsvc_rasterize_sum_forward_slabs_ordered(
     int *meta, float *grad_records_zero, float *out_img, int *final_idx, void *stream,
     void *order_workspace, size_t order_workspace_bytes, int order_flags);
 /* gsvc_rasterize_sum_backward (backward.cu:696-862) into grad_records that
- * the caller has zeroed (gsvc_rasterize_sum_forward_slabs did): no memset. */
+ * the caller has zeroed (gsvc_rasterize_sum_forward_slabs did): no memset.
+ * final_idx is accepted and not read (may be NULL): an entry past a pixel's
+ * final index fails the alpha test there in the forward's own op sequence,
+ * which is what final_idx records, so the reference's k > final_idx skip is
+ * implied by the test itself. */
 int gsvc_rasterize_sum_backward_zeroed(
     unsigned img_height, unsigned img_width, int num_points,
     const int *gaussian_ids_sorted, const int *tile_bins, const float *xys,
