@@ -86,6 +86,63 @@ def load_yuv_frames(path: str, width: int, height: int, device, frames: Optional
     return out, total
 
 
+def textured_video(num_frames: int, height: int, width: int, seed: int = 0, cut_every: int = 0,
+                   device=None, objects: int = 14):
+    """A harder stand-in for the UVG sequences: per scene a
+    mid-frequency background (drifting sinusoids up to ~30 cycles across the
+    frame) under ``objects`` hard-edged elliptical objects, each with its own
+    striped / checkered texture (periods 6-24 px) and colours, moving (2-9 px
+    per frame) and turning from frame to frame, drawn back to front; a scene
+    cut every ``cut_every`` frames.  Sharp edges, texture and motion keep the
+    per-frame models training (the smooth pattern of ``synthetic_video``
+    converges in a few hundred iterations).  Computed with torch on ``device``
+    (CPU by default); frame(i) -> [1, 3, H, W] in [0, 1]."""
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    yy, xx = torch.meshgrid(torch.arange(height, device=dev, dtype=torch.float32),
+                            torch.arange(width, device=dev, dtype=torch.float32), indexing="ij")
+    diag = float(np.hypot(height, width))
+
+    def frame(i: int) -> torch.Tensor:
+        scene = i // cut_every if cut_every else 0
+        t = float(i - (scene * cut_every if cut_every else 0))
+        rng = np.random.default_rng(seed * 7919 + scene * 104729 + 17)
+        img = []
+        bg = rng.uniform(0, 1, (3, 4, 5))
+        for c in range(3):
+            acc = torch.zeros((height, width), device=dev)
+            for k in range(4):
+                fx, fy, ph, vx, vy = (float(v) for v in bg[c, k])
+                acc += torch.sin((60 * fx * xx + 60 * fy * yy) / diag * 3.0 +
+                                 6.28 * ph + 0.15 * t * (vx - vy))
+            img.append(0.5 + 0.35 * acc / 4)
+        img = torch.stack(img)
+        for _ in range(objects):
+            cx, cy = rng.uniform(0, width), rng.uniform(0, height)
+            rx, ry = rng.uniform(40, 260), rng.uniform(40, 260)
+            ang, w = rng.uniform(0, np.pi), rng.uniform(-0.03, 0.03)
+            vx, vy = rng.uniform(-9, 9), rng.uniform(-6, 6)
+            period = rng.uniform(6, 24)
+            kind = rng.integers(0, 2)
+            c1, c2 = rng.uniform(0, 1, 3), rng.uniform(0, 1, 3)
+            ox, oy = cx + vx * t, cy + vy * t
+            a = ang + w * t
+            ca, sa = float(np.cos(a)), float(np.sin(a))
+            u = (xx - ox) * ca + (yy - oy) * sa
+            v = -(xx - ox) * sa + (yy - oy) * ca
+            inside = (u / rx) ** 2 + (v / ry) ** 2 <= 1.0
+            if kind == 0:  # stripes
+                pat = (torch.floor(u / period) % 2) == 0
+            else:  # checks
+                pat = ((torch.floor(u / period) + torch.floor(v / period)) % 2) == 0
+            for ch in range(3):
+                col = torch.where(pat, torch.tensor(float(c1[ch]), device=dev),
+                                  torch.tensor(float(c2[ch]), device=dev))
+                img[ch] = torch.where(inside, col, img[ch])
+        return img.clamp(0, 1)[None].contiguous()
+
+    return frame
+
+
 def synthetic_video(num_frames: int, height: int, width: int, seed: int = 0, cut_every: int = 0,
                     device=None):
     """A seeded smooth moving RGB pattern (sum of drifting sinusoids per
@@ -185,8 +242,9 @@ class FrameTrainer:
     def __init__(self, image: torch.Tensor, frame_num: int, loss_type: str = "L2",
                  num_points: int = 2000, max_num_points: int = 2000, iterations: int = 30000,
                  lr: float = 1e-3, densification_interval: int = 100, trained_model=None,
-                 isdensity=False, isremoval=True, removal_rate=0.25):
+                 isdensity=False, isremoval=True, removal_rate=0.25, early_stop=True):
         self.device = image.device
+        self.early_stop = early_stop  # False: every frame trains for ``iterations``
         self.gt_image = image
         self.frame_num = frame_num
         self.iterations = iterations
@@ -227,6 +285,8 @@ class FrameTrainer:
         it = 0
         for it in range(1, int(self.iterations) + 1):
             loss, psnr = self.model.train_iter(self.gt_image, it)
+            if not self.early_stop:
+                continue
             lv = float(loss.detach())
             if self.isdensity or self.isremoval:
                 stable -= 1
@@ -335,12 +395,14 @@ def train_video(frame_fn, num_frames: int, k_frames: Sequence[int], args, rank: 
                 tr = FrameTrainer(img, f, args.loss_type, args.num_points, args.num_points,
                                   args.iterations, args.lr, args.densification_interval,
                                   isdensity=False, isremoval=args.is_rm,
-                                  removal_rate=args.removal_rate)
+                                  removal_rate=args.removal_rate,
+                                  early_stop=not args.no_early_stop)
             else:  # a P-frame: from the previous frame's model
                 tr = FrameTrainer(img, f, args.loss_type, npts, args.num_points, args.iterations,
                                   args.lr, args.densification_interval, trained_model=gmodel,
                                   isdensity=args.is_ad, isremoval=False,
-                                  removal_rate=args.removal_rate)
+                                  removal_rate=args.removal_rate,
+                                  early_stop=not args.no_early_stop)
             r = tr.train()
             gmodel, npts = r.pop("model"), r["num_gaussians"]
             models[f"frame_{f}"] = {k: v.cpu() for k, v in gmodel.items()}
@@ -357,6 +419,11 @@ def parse_args(argv=None):
     ap.add_argument("-d", "--dataset", type=str, default=None, help="I420 .yuv file")
     ap.add_argument("--synthetic", type=int, default=0, help="frames of a synthetic video")
     ap.add_argument("--cut_every", type=int, default=0, help="synthetic scene-cut period")
+    ap.add_argument("--synthetic_kind", choices=["smooth", "textured"], default="smooth",
+                    help="smooth drifting sinusoids, or textured moving objects (harder)")
+    ap.add_argument("--no_early_stop", action="store_true",
+                    help="train every frame for --iterations (SURVEY 8d config 4: fixed "
+                         "iterations per frame, early stopping off)")
     ap.add_argument("--data_name", type=str, default="Synthetic")
     ap.add_argument("--model_name", type=str, default="GaussianVideo")
     ap.add_argument("--savdir", type=str, default="result")
@@ -426,8 +493,8 @@ def main(argv=None):
             return _cache[i]
     else:
         num_frames = args.synthetic or args.image_length
-        gen = synthetic_video(num_frames, args.height, args.width, int(args.seed), args.cut_every,
-                              device=device)
+        make = textured_video if args.synthetic_kind == "textured" else synthetic_video
+        gen = make(num_frames, args.height, args.width, int(args.seed), args.cut_every, device=device)
 
         def frame_fn(i):
             return gen(i).to(device)

@@ -4,8 +4,10 @@ slab records (A/B knob 24 = 1, diagnostic library) and the banded kernel
 (knob 0 = 2, records).  Same entries per tile, same id order, same blend: the
 images must be bit-identical, including tiles past 256 entries (their first
 256 ids rebuilt from the bboxes), ragged image sizes and a frame with no
-intersections (rasterize_sum.py:121-127's background).  The calls go through
+intersections (rasterize_sum.py:121-127's background) -- and within 1e-5 of
+the C oracle's render of the same activations.  The calls go through
 render_frame_sum, i.e. the ordered projection after the first call."""
+import numpy as np
 import pytest
 import torch
 
@@ -32,7 +34,7 @@ def _frame(n, seed, chol, dev, cluster=0.0):
     (3000, 250, 333, 1.0, 0.0),    # ragged edge tiles
     (500, 128, 128, 0.0, 0.0),     # L = 0 (no bound): no intersections, the background
 ])
-def test_id_slab_render_bit_identical(cuda, n, H, W, chol, cluster):
+def test_id_slab_render_bit_identical(cuda, oracle, n, H, W, chol, cluster):
     from gsvc_amd.render import render_frame_sum
     xyz, c, f = _frame(n, 7 + n, chol, cuda, cluster)
     bound = torch.tensor([0.5, 0.0, 0.5], device=cuda) if chol > 0 else None
@@ -48,6 +50,15 @@ def test_id_slab_render_bit_identical(cuda, n, H, W, chol, cluster):
         assert torch.equal(g, ref[0])
     if chol == 0:
         assert torch.equal(ref[0][0], bg.view(3, 1, 1).expand(3, H, W))
+    else:
+        # and against the C oracle on the GPU's own activations (torch.tanh ==
+        # the kernel's tanhf, test_gpu_sync_free.test_tanh_matches_torch)
+        means = torch.tanh(xyz).cpu().numpy()
+        L = (c + bound).cpu().numpy()
+        r = oracle.render_sum(means, L, f.cpu().numpy(), np.ones((n, 1), np.float32), H, W)
+        want = np.clip(r["out"], 0, 1).transpose(2, 0, 1) if r["m"] > 0 else None
+        if want is not None:
+            np.testing.assert_allclose(ref[0][0].cpu().numpy(), want, rtol=0, atol=1e-5)
 
 
 def test_id_slab_batched_render_bit_identical(cuda):

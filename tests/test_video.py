@@ -340,3 +340,17 @@ def test_checkpoint_round_trip(cuda, tmp_path):
         assert p == r["psnr"], (f, p, r["psnr"])
         assert torch.equal(out, ref), f
     assert len(sizes) > 1  # I-frames pruned, P-frames densified: the models differ in size
+
+
+def test_textured_video_stand_in():
+    """The harder synthetic stand-in: seeded and
+    reproducible, moving from frame to frame, a new scene at each cut, values
+    in [0, 1]; the driver's --synthetic_kind / --no_early_stop flags parse."""
+    from gsvc_amd import video as V
+    g = V.textured_video(8, 96, 160, 3, cut_every=4)
+    f0, f1, f4 = g(0), g(1), g(4)
+    assert f0.shape == (1, 3, 96, 160) and float(f0.min()) >= 0 and float(f0.max()) <= 1
+    assert torch.equal(f0, V.textured_video(8, 96, 160, 3, cut_every=4)(0))
+    assert 0 < float((f1 - f0).abs().mean()) < float((f4 - f0).abs().mean())
+    a = V.parse_args(["--synthetic", "8", "--synthetic_kind", "textured", "--no_early_stop"])
+    assert a.synthetic_kind == "textured" and a.no_early_stop

@@ -10,6 +10,10 @@ and scored against its frame; the PSNR must equal the one the driver logged.
     python tools/video600.py --out gpurun_out/v600/c5.json -- \\
         --synthetic 600 --num_points 100000 --iterations 4100 --is_rm --is_ad --cut_every 120
 
+Round 5 adds the harder stand-in: --synthetic_kind textured
+(moving, turning textured objects over a mid-frequency background) and
+--no_early_stop (fixed iterations per frame).
+
 Writes a summary JSON (wall time, per-frame PSNR / iterations / splat counts,
 checkpoint bytes, load-back deviation) to --out; the checkpoint itself (1-2 GB)
 stays under --root.  Progress goes to stderr every --every frames.
@@ -68,8 +72,8 @@ def main():
     dev = torch.device("cuda:0")
     t1 = time.time()
     models = torch.load(ckpt, weights_only=True, map_location="cpu")
-    gen = V.synthetic_video(vargs.synthetic, vargs.height, vargs.width, int(vargs.seed),
-                            vargs.cut_every, device=dev)
+    make = V.textured_video if vargs.synthetic_kind == "textured" else V.synthetic_video
+    gen = make(vargs.synthetic, vargs.height, vargs.width, int(vargs.seed), vargs.cut_every, device=dev)
     dev_psnr = []
     for r in frames:
         f = r["frame"]
