@@ -627,6 +627,7 @@ def op_path_block(model, gt, device, steps=200, warmup=20):
     # the drop-in's own kernels in forward + backward calls, HIP events on
     # their dispatches (outside the timed loops)
     kt = time_channels(["composite", "sum_bwd"], fwd_bwd, 100)
+    host = op_host_us(op, steps)
     shape = frame_shape(op.get_xyz.detach(), op.get_cholesky_elements.detach(), op.tile_bounds)
     prof = load_profile("op_path")
     return {"workload": f"unchanged-caller op path at 1920x1080 / {n} splats (the bench's trained "
@@ -636,12 +637,46 @@ def op_path_block(model, gt, device, steps=200, warmup=20):
             "train_iters_per_s": round(1.0 / t_train, 1),
             "train_iters_per_s_foreach_adan": round(1.0 / t_train_fe, 1),
             "timing": f"wall clock over {steps} calls after {warmup} warm-ups, synchronized",
+            "host_us_per_call": host,
             "kernels": {
                 "raster_sum_fwd": roofline("raster_sum_fwd_kernel (op path: final_idx, id slabs)",
                                            op_composite_bytes(shape), kt["composite"], prof,
                                            "rasterize_sum_forward"),
                 "raster_sum_bwd": roofline("raster_sum_bwd_kernel", sum_bwd_bytes(shape, n),
                                            kt["sum_bwd"], prof, "rasterize_sum_backward")}}
+
+
+def op_host_us(op, calls):
+    """Host (CPU) time per call of the drop-in's own two operators on the
+    frame's activations -- the C++ Functions' forward calls and their backward
+    nodes, each call timed alone with the GPU work left asynchronous -- beside
+    GSVC's own op sequence around them (the rest of op_path's wall time)."""
+    from gsplat.project_gaussians_2d import project_gaussians_2d
+    from gsplat.rasterize_sum import rasterize_gaussians_sum
+    m = op.get_xyz.detach().clone().requires_grad_(True)
+    L = op.get_cholesky_elements.detach().clone().requires_grad_(True)
+    c = op.get_features.detach().clone().requires_grad_(True)
+    o = torch.ones(m.shape[0], 1, device=m.device)
+    bg = torch.ones(3, device=m.device)
+    tb = op.tile_bounds
+    v = torch.ones(H, W, 3, device=m.device)
+    t = {"project_gaussians_2d": 0.0, "rasterize_gaussians_sum": 0.0, "backward_both": 0.0}
+    for k in range(calls + 10):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        xys, depths, radii, conics, nth = project_gaussians_2d(m, L, H, W, tb)
+        t1 = time.perf_counter()
+        out = rasterize_gaussians_sum(xys, depths, radii, conics, nth, c, o, H, W, 16, 16,
+                                      background=bg)
+        t2 = time.perf_counter()
+        torch.autograd.grad(out, (m, L, c), v)
+        t3 = time.perf_counter()
+        if k >= 10:
+            t["project_gaussians_2d"] += t1 - t0
+            t["rasterize_gaussians_sum"] += t2 - t1
+            t["backward_both"] += t3 - t2
+    torch.cuda.synchronize()
+    return {k: round(x / calls * 1e6, 1) for k, x in t.items()}
 
 
 def alpha_block(device, n=50000, steps=100, warmup=10):

@@ -1310,7 +1310,8 @@ __global__ __launch_bounds__(kProjThreads) void tile_insert_ids_ordered_kernel(
     const int *__restrict__ radii, int tbx, int tby, unsigned *__restrict__ counts,
     int *__restrict__ ids, int *__restrict__ m_acc, int *__restrict__ m_clear,
     float4 *__restrict__ rec_zero, unsigned *__restrict__ key, int *__restrict__ key_id,
-    unsigned key_invisible) {
+    unsigned key_invisible, const float *__restrict__ conics, const float *__restrict__ colors,
+    const float *__restrict__ opac, float4 *__restrict__ rec) {
     __shared__ int s_hits[kProjThreads / 64];
     __shared__ unsigned s_cnt[kAggWin];
     __shared__ int s_box[4][kProjThreads / 64];
@@ -1335,6 +1336,15 @@ __global__ __launch_bounds__(kProjThreads) void tile_insert_ids_ordered_kernel(
         S.P.xy = c;
         S.P.rad = r;
         if (r > 0) tile_bbox(c.x, c.y, (float)r, tbx, tby, x0, y0, x1, y1);
+        if (rec) {
+            // the splat's 48-byte record for the composite's gather (the frame
+            // path's layout: {x, y, a/2, b}, {c/2, opacity, r, g}, {b, id, a, c}):
+            // one record per entry instead of eight scattered loads
+            const float a = conics[3 * (size_t)i], b = conics[3 * (size_t)i + 1], cc = conics[3 * (size_t)i + 2];
+            rec[3 * (size_t)i] = make_float4(c.x, c.y, 0.5f * a, b);
+            rec[3 * (size_t)i + 1] = make_float4(0.5f * cc, opac[i], colors[3 * (size_t)i], colors[3 * (size_t)i + 1]);
+            rec[3 * (size_t)i + 2] = make_float4(colors[3 * (size_t)i + 2], __int_as_float(i), a, cc);
+        }
         if (key) {
             key[i] = strip_key(c.x, c.y, r, tbx, tby, key_invisible);
             key_id[i] = i;
@@ -1351,6 +1361,7 @@ __global__ __launch_bounds__(kProjThreads) void tile_insert_ids_ordered_kernel(
 struct OpOrderWs {
     unsigned *okey, *skey, *kbuf;
     int *okey_id, *order, *vbuf;
+    float4 *rec;  // the splats' 48-byte records (the ordered insertion writes them)
     unsigned *sort_counts, *sort_offsets;
     size_t bytes;
 };
@@ -1372,6 +1383,7 @@ static OpOrderWs op_order_ws(char *base, int n) {
     const size_t cb = sort_u32_counts_bytes(n > 0 ? n : 1);
     w.sort_counts = (unsigned *)take(cb);
     w.sort_offsets = (unsigned *)take(cb);
+    w.rec = (float4 *)take(sizeof(float4) * 3 * nn);
     w.bytes = off;
     return w;
 }
@@ -1569,7 +1581,8 @@ static int forward_slabs_impl(
                            (const float2 *)xys, radii, tbx, tby, counts + (size_t)par * ntiles,
                            gaussian_ids, m_slots + par, m_slots + (par ^ 1),
                            (float4 *)grad_records_zero, refresh ? ow.okey : nullptr,
-                           refresh ? ow.okey_id : nullptr, strip_key_invisible(tbx, tby));
+                           refresh ? ow.okey_id : nullptr, strip_key_invisible(tbx, tby), conics,
+                           colors, opacities, ow.rec);
     } else if (num_points > 0) {
         hipLaunchKernelGGL(tile_insert_ids_kernel, dim3(ceil_div(num_points, kProjThreads)),
                            dim3(kProjThreads), 0, s, num_points, (const float2 *)xys, radii, tbx,
@@ -1600,6 +1613,9 @@ static int forward_slabs_impl(
     A.conics = conics;
     A.colors = colors;
     A.opac = opacities;
+    // the ordered insertion packs each splat's record: the composite gathers one
+    // 48-byte record per entry, as the frame render does
+    A.rec = (ordered && num_points > 0) ? ow.rec : nullptr;
     A.out = out_img;
     A.final_idx = final_idx;
     const int rc = sum_forward_launch(A, density_hint, s);

@@ -396,13 +396,13 @@ def train_video(frame_fn, num_frames: int, k_frames: Sequence[int], args, rank: 
                                   args.iterations, args.lr, args.densification_interval,
                                   isdensity=False, isremoval=args.is_rm,
                                   removal_rate=args.removal_rate,
-                                  early_stop=not args.no_early_stop)
+                                  early_stop=not getattr(args, "no_early_stop", False))
             else:  # a P-frame: from the previous frame's model
                 tr = FrameTrainer(img, f, args.loss_type, npts, args.num_points, args.iterations,
                                   args.lr, args.densification_interval, trained_model=gmodel,
                                   isdensity=args.is_ad, isremoval=False,
                                   removal_rate=args.removal_rate,
-                                  early_stop=not args.no_early_stop)
+                                  early_stop=not getattr(args, "no_early_stop", False))
             r = tr.train()
             gmodel, npts = r.pop("model"), r["num_gaussians"]
             models[f"frame_{f}"] = {k: v.cpu() for k, v in gmodel.items()}
@@ -493,7 +493,7 @@ def main(argv=None):
             return _cache[i]
     else:
         num_frames = args.synthetic or args.image_length
-        make = textured_video if args.synthetic_kind == "textured" else synthetic_video
+        make = textured_video if getattr(args, "synthetic_kind", "smooth") == "textured" else synthetic_video
         gen = make(num_frames, args.height, args.width, int(args.seed), args.cut_every, device=device)
 
         def frame_fn(i):

@@ -85,7 +85,7 @@ def _worker(rank, world, port, q):
         class StubTrainer:
             def __init__(self, image, frame_num, loss_type, num_points, max_num_points, iterations,
                          lr, densification_interval=100, trained_model=None, isdensity=False,
-                         isremoval=True, removal_rate=0.25):
+                         isremoval=True, removal_rate=0.25, early_stop=True):
                 self.f = frame_num
                 self.parent = None if trained_model is None else int(trained_model["frame"])
                 calls.append(dict(frame=frame_num, parent=self.parent, isdensity=isdensity,
