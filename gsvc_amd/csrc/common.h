@@ -16,6 +16,17 @@ namespace gsvc {
 
 constexpr int kTile = 16;          // BLOCK_X = BLOCK_Y (reference config.h:1-2)
 constexpr int kTilePix = 256;      // BLOCK_SIZE (config.h:3): entries blended per tile
+// The training step's carried candidate lists (GSVC_TRAIN_CARRY): slots per
+// tile.  A tile of more than 256 candidates (dense content: the textured video
+// stand-in passes 256 entries per tile after ~40 frames of training) sorts its
+// members from this list; only past kCarryCap does it rebuild from every
+// splat's bbox (tile_ids.h wave_brute_ids).
+constexpr int kCarryCap = 1024;
+// The record slabs (frame path) keep a tile's slots [256, kCarryCap) as ids in
+// an overflow area of kOvfSlots per tile: a tile of up to kCarryCap entries
+// sorts its ids from the slab and the area instead of the bbox rebuild.
+constexpr int kOvfSlots = kCarryCap - kTilePix;
+static_assert(kCarryCap == GSVC_SLABS_WIDE_IDS, "include/gsvc_amd.h GSVC_SLABS_WIDE_IDS");
 constexpr float kNegLog2e = -1.4426950408889634f;
 constexpr float kAlphaMin = 1.0f / 255.0f;
 // At unit opacity the reference's alpha cut (forward.cu:598-606:
@@ -46,7 +57,7 @@ int dev_copy(void *dst, const void *src, size_t bytes, hipStream_t s);
 // for tools/ and the variant-comparison tests).  In the product library every
 // knob is the constant 0 -- the production choice -- and the diagnostic
 // variants are not compiled (``if constexpr (kDiag)`` around their launches).
-constexpr int kKnobs = 32;
+constexpr int kKnobs = 40;
 #ifdef GSVC_DIAG
 constexpr bool kDiag = true;
 extern int g_knobs[kKnobs];  // gsvc_debug_set(); knob 0 = sum-forward variant, 8 = training tile kernel

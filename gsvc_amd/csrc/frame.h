@@ -18,6 +18,8 @@ inline int tiles_of(unsigned h, unsigned w) {
 // at 1080p, so a batch of frames touches few pages for them) followed by the
 // body [T][256][3] (slots from kHeadSlots on, at their slot index).
 constexpr int kHeadSlots = 8;
+// (a render's id slabs use the same memory: kCarryCap ids per tile)
+static_assert(4 * kCarryCap <= 16 * 3 * (kHeadSlots + kTilePix), "id slabs exceed the slab memory");
 __host__ __device__ inline size_t slab_frame_f4(int ntiles) {
     return (size_t)3 * (kHeadSlots + kTilePix) * (size_t)ntiles;
 }
@@ -37,6 +39,7 @@ struct FrameWs {
     unsigned *counts;  // [F][2][T]: per frame, this call's and the next call's
     int *m_slots;      // [F][2]
     float4 *slab;      // [F] x (head [T][kHeadSlots][3] + body [T][256][3]) splat records
+    int *ovf;          // [F][T][kOvfSlots]: the ids of record-slab slots 256 .. kCarryCap - 1
     float2 *xys;       // [N] (N = splats of all F frames)
     int *radii;        // [N]
     float4 *rec;       // [N][3] splat records

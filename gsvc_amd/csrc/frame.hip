@@ -37,7 +37,8 @@ template <int K>
 __device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, int tby, int sub,
                                            float4 r0, float4 r1, float4 r2,
                                            unsigned *__restrict__ counts,
-                                           float4 *__restrict__ slab, int wt) {
+                                           float4 *__restrict__ slab, int wt,
+                                           int *__restrict__ ovf) {
     unsigned x0, y0, x1, y1;
     tile_bbox(cx, cy, (float)r, tbx, tby, x0, y0, x1, y1);
     if (x1 <= x0 || y1 <= y0) return 0;
@@ -53,7 +54,9 @@ __device__ __forceinline__ int slab_insert(float cx, float cy, int r, int tbx, i
             if (k < cnt) sl[k] = atomicAdd(counts + tl[k], 1u);
 #pragma unroll
         for (int k = 0; k < kBatch; ++k)
-            if (k < cnt && sl[k] < (unsigned)kTilePix) {
+            if (k < cnt && sl[k] >= (unsigned)kTilePix && sl[k] < (unsigned)kCarryCap && ovf) {
+                ovf[(size_t)tl[k] * kOvfSlots + (sl[k] - kTilePix)] = __float_as_int(r2.y);
+            } else if (k < cnt && sl[k] < (unsigned)kTilePix) {
                 float4 *d = slab_rec(slab, ntiles, (int)tl[k], (int)sl[k]);
                 if (kDiag && (wt & 1)) {
                     store_wt(d, r0);
@@ -104,7 +107,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
     unsigned *__restrict__ counts, float4 *__restrict__ slab, int *__restrict__ m_acc,
     int *__restrict__ m_clear, float4 *__restrict__ grad_zero, long long *stamps,
     const int *__restrict__ frame_off, int counts_stride, int m_stride, size_t slab_stride,
-    int wt, int *__restrict__ ids) {
+    int wt, int *__restrict__ ids, int *__restrict__ ovf) {
     __shared__ int s_hits[kProjThreads / 64];
     // batched frames (grid.y): this block's frame owns splats [begin, end)
     int begin = 0, end = n;
@@ -115,6 +118,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
         counts += (size_t)b * counts_stride;
         slab += b * slab_stride;
         if (ids) ids += 4 * b * slab_stride;  // id slabs in the frame's slab memory
+        if (ovf) ovf += (size_t)b * kOvfSlots * (size_t)(tbx * tby);
         m_acc += (size_t)b * m_stride;
         m_clear += (size_t)b * m_stride;
     }
@@ -147,10 +151,11 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_kernel(
         if (S.P.rad > 0) {
             if (K == 1 && !(kDiag && (wt & 3)))  // paired atomics unless write-through / A/B knob 2 = 4
                 hits = slab_insert_pairs<8>(S.P.xy.x, S.P.xy.y, S.P.rad, tbx, tby, S.r0, S.r1,
-                                            S.r2, counts, slab, wt, ids);
+                                            S.r2, counts, slab, wt, ids, kCarryCap,
+                                            ids ? nullptr : ovf);
             else
                 hits = slab_insert<K>(S.P.xy.x, S.P.xy.y, S.P.rad, tbx, tby, sub, S.r0, S.r1,
-                                      S.r2, counts, slab, wt);
+                                      S.r2, counts, slab, wt, ovf);
         }
     }
     if (kStamp) {
@@ -185,7 +190,7 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_ordered_kernel(
     int *__restrict__ m_clear, float4 *__restrict__ grad_zero, unsigned *__restrict__ key,
     int *__restrict__ key_id, unsigned key_invisible, long long *stamps,
     int *__restrict__ carry_ids, uint2 *__restrict__ carry_box, uint2 *__restrict__ carry_hull,
-    int *__restrict__ id_slab) {
+    int *__restrict__ id_slab, int *__restrict__ ovf) {
     __shared__ int s_hits[kProjThreads / 64];
     __shared__ unsigned s_cnt[kAggWin];
     __shared__ int s_box[4][kProjThreads / 64];
@@ -224,7 +229,8 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_ordered_kernel(
     // ids in place of records: the carried bins' candidate lists, or the
     // render's id slabs (both 256 slots per tile)
     const int hits = slab_insert_window(S, x0, y0, x1, y1, tbx, tby, counts, slab, s_cnt, s_box, st,
-                                        carry_ids ? carry_ids : id_slab);
+                                        carry_ids ? carry_ids : id_slab, kCarryCap,
+                                        carry_ids || id_slab ? nullptr : ovf);
     if (kStamp) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) st[2] = proj_stamp();
@@ -259,6 +265,7 @@ FrameWs frame_ws(char *base, int n, int ntiles, int frames) {
     w.m_slots = (int *)(w.counts + 2 * nt * nf);
     w.zeroed = sizeof(unsigned) * 2 * nt * nf + 2 * nf * sizeof(int);
     w.slab = (float4 *)take(sizeof(float4) * slab_frame_f4((int)nt) * nf);
+    w.ovf = (int *)take(sizeof(int) * (size_t)kOvfSlots * nt * nf);
     w.xys = (float2 *)take(sizeof(float2) * nn);
     w.radii = (int *)take(sizeof(int) * nn);
     w.rec = (float4 *)take(sizeof(float4) * 3 * nn);
@@ -316,7 +323,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
                                ord->carry_ids ? ord->carry_counts : f.counts, w.slab, f.m_acc,
                                f.m_clear, grad_zero, ord->key, ord->key_id, strip_key_invisible(tbx, tby),
                                reinterpret_cast<long long *>(debug_ptr()), ord->carry_ids,
-                               ord->carry_box, ord->carry_hull, id_slab);
+                               ord->carry_box, ord->carry_hull, id_slab, w.ovf);
             return check_launch("frame projection (ordered)");
         }
         hipEvent_t tev[2];
@@ -326,7 +333,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
                      tby, w.xys, w.radii, w.rec, ord->carry_ids ? ord->carry_counts : f.counts,
                      w.slab, f.m_acc, f.m_clear, grad_zero, ord->key, ord->key_id,
                      strip_key_invisible(tbx, tby), (long long *)nullptr, ord->carry_ids,
-                     ord->carry_box, ord->carry_hull, id_slab);
+                     ord->carry_box, ord->carry_hull, id_slab, w.ovf);
         timing_end(s, tslot, kTimingProject);
         return check_launch("frame projection (ordered)");
     }
@@ -362,7 +369,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
                      xyz_tanh, chol, chol_bound, feat, rgb_w, opac, hw, hh, tbx, tby, w.xys,     \
                      w.radii, w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero,            \
                      (long long *)nullptr, frames > 1 ? frame_off : (const int *)nullptr,        \
-                     f.counts_stride, f.m_stride, slab_stride, wt, id_slab);                     \
+                     f.counts_stride, f.m_stride, slab_stride, wt, id_slab, w.ovf);              \
         timing_end(s, tslot, kTimingProject);                                                    \
     }
         if constexpr (kDiag) if (knob(5) == 1 && debug_ptr()) {  // diagnostic: per-wave stamps
@@ -372,7 +379,7 @@ int frame_project_launch(int n, const float *xyz, int xyz_tanh, const float *cho
                                w.rec, f.counts, w.slab, f.m_acc, f.m_clear, grad_zero,
                                reinterpret_cast<long long *>(debug_ptr()),
                                frames > 1 ? frame_off : nullptr, f.counts_stride, f.m_stride,
-                               slab_stride, wt, id_slab);
+                               slab_stride, wt, id_slab, w.ovf);
             return check_launch("frame projection");
         }
         if constexpr (kDiag) {
@@ -437,7 +444,8 @@ static int render_frames(int frames, const int *frame_off_host, const int *frame
     }
     // A single sparse frame renders over id slabs: the projection appends each
     // splat's id (4 B) in place of its 48-byte record and the composite gathers
-    // the records by id from w.rec (the slab memory holds the T x 256 ids).
+    // the records by id from w.rec (the slab memory holds T x kCarryCap ids: a
+    // tile of up to 1024 entries sorts its first 256 from them).
     // Batched frames and dense frames (the banded kernel) keep the records;
     // A/B knob 24 = 1 (diagnostic library) too.
     int *id_slab = nullptr;
@@ -474,8 +482,10 @@ static int render_frames(int frames, const int *frame_off_host, const int *frame
         A.id_counts = f.counts;
         A.id_counts_clear = f.counts_next;
         A.ids_rw = id_slab;
+        A.ids_cap = kCarryCap;  // 1024 ids per tile fit the tile's 12.4 KB of slab memory
     } else {
         A.slab = w.slab;
+        A.slab_ovf = w.ovf;
         A.slab_counts = f.counts;
         A.slab_counts_clear = f.counts_next;
     }

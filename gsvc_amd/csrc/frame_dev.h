@@ -18,14 +18,18 @@ constexpr int kProjThreads = 256;
 // (trained-like 1080p / 50k splats: 794k insertions).  kB slot atomics are
 // generated (unrolled, register-resident), issued, and only then waited for:
 // one round trip per kB of them.
-// ``ids`` (optional, the training step's carried bins): the splat's id into
-// ids[tile][slot] instead of its record into the slab.
+// ``ids`` (optional: id slabs, or the training step's carried bins): the
+// splat's id into ids[tile][slot] (ids_cap slots per tile) instead of its
+// record into the slab.  ``ovf`` (record slabs): slots [256, kCarryCap) as
+// ids into ovf[tile][slot - 256].
 template <int kB>
 __device__ __forceinline__ int slab_insert_pairs(float cx, float cy, int r, int tbx, int tby,
                                                  float4 r0, float4 r1, float4 r2,
                                                  unsigned *__restrict__ counts,
                                                  float4 *__restrict__ slab, int wt,
-                                                 int *__restrict__ ids = nullptr) {
+                                                 int *__restrict__ ids = nullptr,
+                                                 int ids_cap = kTilePix,
+                                                 int *__restrict__ ovf = nullptr) {
     unsigned x0, y0, x1, y1;
     tile_bbox(cx, cy, (float)r, tbx, tby, x0, y0, x1, y1);
     if (x1 <= x0 || y1 <= y0) return 0;
@@ -33,13 +37,15 @@ __device__ __forceinline__ int slab_insert_pairs(float cx, float cy, int r, int 
     const bool wide = x1 - x0 >= 3;  // narrow rows: single atomics (measured faster at 10k)
     const int ntiles = tbx * tby;
     auto put = [&](unsigned t, unsigned sl) {
-        if (sl < (unsigned)kTilePix && ids) {
-            ids[(size_t)t * kTilePix + sl] = __float_as_int(r2.y);
+        if (ids) {
+            if (sl < (unsigned)ids_cap) ids[(size_t)t * ids_cap + sl] = __float_as_int(r2.y);
         } else if (sl < (unsigned)kTilePix) {
             float4 *d = slab_rec(slab, ntiles, (int)t, (int)sl);
             d[0] = r0;
             d[1] = r1;
             d[2] = r2;
+        } else if (ovf && sl < (unsigned)kCarryCap) {
+            ovf[(size_t)t * kOvfSlots + (sl - kTilePix)] = __float_as_int(r2.y);
         }
     };
     int hits = 0;
@@ -147,6 +153,7 @@ __device__ __forceinline__ SplatOut load_project(int i, const float *__restrict_
 }
 
 // The block's hit total into this frame's M.
+template <int kThr = kProjThreads>
 __device__ __forceinline__ void add_hits(int hits, int *s_hits, int *m_acc) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) hits += __shfl_xor(hits, off, 64);
@@ -155,7 +162,7 @@ __device__ __forceinline__ void add_hits(int hits, int *s_hits, int *m_acc) {
     if (threadIdx.x == 0) {
         int tot = 0;
 #pragma unroll
-        for (int k = 0; k < kProjThreads / 64; ++k)
+        for (int k = 0; k < kThr / 64; ++k)
             if (k < (int)(blockDim.x >> 6)) tot += s_hits[k];
         if (tot) atomicAdd(m_acc, tot);
     }
@@ -188,13 +195,16 @@ __host__ __device__ inline unsigned strip_key_invisible(int tbx, int tby) {
 // whose window is too large, insert directly (slab_insert_pairs).  [x0, x1) x
 // [y0, y1): the lane's tile bbox (empty: nothing to insert).  Returns the
 // lane's insertions (its share of M).
+template <int kThr = kProjThreads>
 __device__ __forceinline__ int slab_insert_window(const SplatOut &S, unsigned x0, unsigned y0,
                                                   unsigned x1, unsigned y1, int tbx, int tby,
                                                   unsigned *__restrict__ counts,
                                                   float4 *__restrict__ slab, unsigned *s_cnt,
-                                                  int (*s_box)[kProjThreads / 64],
+                                                  int (*s_box)[kThr / 64],
                                                   long long *st = nullptr,
-                                                  int *__restrict__ ids = nullptr) {
+                                                  int *__restrict__ ids = nullptr,
+                                                  int ids_cap = kTilePix,
+                                                  int *__restrict__ ovf = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     // diagnostic (st != NULL): s_memrealtime per wave after each phase
     auto mark = [&](int k) {
@@ -225,7 +235,7 @@ __device__ __forceinline__ int slab_insert_window(const SplatOut &S, unsigned x0
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kProjThreads / 64; ++k) {
+    for (int k = 0; k < kThr / 64; ++k) {
         bx0 = min(bx0, s_box[0][k]);
         by0 = min(by0, s_box[1][k]);
         bx1 = max(bx1, s_box[2][k]);
@@ -237,10 +247,10 @@ __device__ __forceinline__ int slab_insert_window(const SplatOut &S, unsigned x0
     int hits = 0;
     if (vis && !(agg && small))
         hits = slab_insert_pairs<8>(S.P.xy.x, S.P.xy.y, S.P.rad, tbx, tby, S.r0, S.r1, S.r2,
-                                    counts, slab, 0, ids);
+                                    counts, slab, 0, ids, ids_cap, ovf);
     if (agg) {
         const int cells = ww * wh;
-        for (int c = tid; c < cells; c += kProjThreads) s_cnt[c] = 0u;
+        for (int c = tid; c < cells; c += kThr) s_cnt[c] = 0u;
         __syncthreads();
         if (small) {
             for (unsigned y = y0; y < y1; ++y)
@@ -250,7 +260,7 @@ __device__ __forceinline__ int slab_insert_window(const SplatOut &S, unsigned x0
         __syncthreads();
         mark(5);
         // one device-scope atomic per touched tile: the window's base slots
-        for (int c = tid; c < cells; c += kProjThreads) {
+        for (int c = tid; c < cells; c += kThr) {
             const unsigned v = s_cnt[c];
             if (v) {
                 const int ty = by0 + c / ww, tx = bx0 + c - (c / ww) * ww;
@@ -265,13 +275,15 @@ __device__ __forceinline__ int slab_insert_window(const SplatOut &S, unsigned x0
                 for (unsigned x = x0; x < x1; ++x) {
                     const unsigned sl = atomicAdd(&s_cnt[((int)y - by0) * ww + ((int)x - bx0)], 1u);
                     const int tl = (int)(y * (unsigned)tbx + x);
-                    if (sl < (unsigned)kTilePix && ids) {
-                        ids[(size_t)tl * kTilePix + sl] = __float_as_int(S.r2.y);
+                    if (ids) {
+                        if (sl < (unsigned)ids_cap) ids[(size_t)tl * ids_cap + sl] = __float_as_int(S.r2.y);
                     } else if (sl < (unsigned)kTilePix) {
                         float4 *d = slab_rec(slab, ntiles, tl, (int)sl);
                         d[0] = S.r0;
                         d[1] = S.r1;
                         d[2] = S.r2;
+                    } else if (ovf && sl < (unsigned)kCarryCap) {
+                        ovf[(size_t)tl * kOvfSlots + (sl - kTilePix)] = __float_as_int(S.r2.y);
                     }
                 }
             hits += (int)((x1 - x0) * (y1 - y0));

@@ -19,6 +19,7 @@ struct SumFwdArgs {
     int spec_slots;    // frame path: slab records loaded with the count (<= kHeadSlots)
     int group_min;     // sparse chunks of <= this many entries skip the lane-group lists
     int cut;           // sparse render chunks may take the sigma-threshold blend (knob 19 = 1: never)
+    int ids_cap;       // id slabs: slots per tile (kTilePix, or kCarryCap for wide slabs)
     int norank;        // diagnostic A/B (knob 31 = 1): <= 64 slab entries staged in slot order, not by id
     const int *m_dev;  // device num_intersects (NULL: > 0); 0 -> background
     const float *bg;
@@ -37,6 +38,7 @@ struct SumFwdArgs {
     // entries are rebuilt from the splats' bboxes (cull_xys, cull_radii,
     // num_points) and records (rec).
     const float4 *slab;
+    const int *slab_ovf;  // record slabs: the ids of slots 256 .. kCarryCap - 1 (frame.h FrameWs.ovf)
     const unsigned *slab_counts;
     unsigned *slab_counts_clear;
     const float2 *cull_xys;

@@ -347,7 +347,7 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         }
         wave_lds_sync();
         if (A.bins_out) {  // the op path: the tile's ids in id order and its bins, for the backward
-            if (lane < cnt) A.ids_rw[(size_t)tile * kTilePix + rank] = id;
+            if (lane < cnt) A.ids_rw[(size_t)tile * A.ids_cap + rank] = id;
             if (lane == 0) A.bins_out[tile] = make_int2(range.x, range.x + cnt);
         }
         if (!kIdx) cut = A.cut && __ballot(lane < cnt && !entry_cut_ok(geo, col, bx.x)) == 0ull;
@@ -671,7 +671,7 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
 __device__ __forceinline__ void write_sorted_ids(const SumFwdArgs &A, int tile, int begin, int n,
                                                  const int *s_ids) {
     const int lane = threadIdx.x & 63;
-    for (int j = lane; j < n; j += 64) A.ids_rw[(size_t)tile * kTilePix + j] = s_ids[j];
+    for (int j = lane; j < n; j += 64) A.ids_rw[(size_t)tile * A.ids_cap + j] = s_ids[j];
     if (lane == 0) A.bins_out[tile] = make_int2(begin, begin + n);
 }
 
@@ -701,6 +701,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         tile -= b * A.ntiles;
         if (A.slab) {  // (an offset null pointer would read as a slab)
             A.slab += b * A.slab_stride;
+            if (A.slab_ovf) A.slab_ovf += (size_t)b * kOvfSlots * (size_t)A.ntiles;
             A.slab_counts += (size_t)b * A.counts_stride;
             A.slab_counts_clear += (size_t)b * A.counts_stride;
         }
@@ -723,7 +724,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
     const float4 *seg_rec = nullptr;  // slab records, when the fast path applies
     float4 spec0 = make_float4(0.f, 0.f, 0.f, 0.f), spec1 = spec0, spec2 = spec0;
     int spec_id = 0;  // id slabs (render): the lane's slot, loaded with the count
-    if (A.slab) {
+    if (kMode != kModeSparseIds && A.slab) {  // (mode 9 renders over id slabs only)
         // this frame's count, and the first kSpecSlots records loaded in the
         // same round trip (speculatively: most tiles have that few)
         const int lane = threadIdx.x & 63;
@@ -747,6 +748,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         seg.ids = nullptr;
         seg.recs = recs;
         seg.head = slab_rec(A.slab, A.ntiles, tile, 0);
+        seg.ovf = A.slab_ovf ? A.slab_ovf + (size_t)tile * kOvfSlots : nullptr;
         if (n_all <= kChunk) seg_rec = recs;  // slots past the head, at their index
     } else if (kIds && A.id_counts) {
         // op path, unsorted id slabs (its autograd forward: kIdx instances
@@ -758,7 +760,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         // from these: slower, 44.3 vs 42.4 us per tools/slabbench.py call at
         // the trained 1080p / 50k frame -- its ids stay read after the count)
         if (kMode == kModeSparseIds)
-            spec_id = A.ids_rw[(size_t)tile * kTilePix + (threadIdx.x & 63)];
+            spec_id = A.ids_rw[(size_t)tile * A.ids_cap + (threadIdx.x & 63)];
         if (threadIdx.x == 0) {
             A.id_counts_clear[tile] = 0u;  // the next call's counts
             if (tile == 0) {
@@ -766,8 +768,9 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
                 A.meta_out[1] = 0;
             }
         }
-        range = make_int2(tile * kTilePix, tile * kTilePix + (n_all < kTilePix ? n_all : kTilePix));
-        seg.ids = A.ids_rw + (size_t)tile * kTilePix;
+        range = make_int2(tile * A.ids_cap, tile * A.ids_cap + (n_all < kTilePix ? n_all : kTilePix));
+        seg.ids = A.ids_rw + (size_t)tile * A.ids_cap;
+        seg.cap_ids = A.ids_cap;
         seg.recs = nullptr;
         seg.head = nullptr;
         // <= 64 entries: records gathered by id and ranked straight into the
@@ -801,7 +804,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
     if (sparse) {
         if (w != 0) return;
         if (by_ids)
-            n = ((A.slab || (kIds && A.id_counts)) && n_all > kTilePix)
+            n = ((A.slab || (kIds && A.id_counts)) && n_all > seg.cap())
                     ? wave_brute_tile_ids(A, tile, s_ids[0])
                     : wave_sorted_tile_ids(seg, n_all, s_ids[0], reinterpret_cast<unsigned *>(s_buf[0]));
         // the op path: the tile's sorted ids and bins for the backward (a tile
@@ -817,7 +820,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
             // slots a second sorting wave would still be reading
             __shared__ int s_n;
             if (w == 0) {
-                const int ns = ((A.slab || (kIds && A.id_counts)) && n_all > kTilePix)
+                const int ns = ((A.slab || (kIds && A.id_counts)) && n_all > seg.cap())
                                    ? wave_brute_tile_ids(A, tile, s_ids[0])
                                    : wave_sorted_tile_ids(seg, n_all, s_ids[0],
                                                           reinterpret_cast<unsigned *>(s_buf[0]));
@@ -1274,7 +1277,7 @@ static int check_tiles(const char *what, int bx, int by, int tbx, int tby, unsig
 __global__ __launch_bounds__(kProjThreads) void tile_insert_ids_kernel(
     int n, const float2 *__restrict__ xys, const int *__restrict__ radii, int tbx, int tby,
     unsigned *__restrict__ counts, int *__restrict__ ids, int *__restrict__ m_acc,
-    int *__restrict__ m_clear, float4 *__restrict__ rec_zero) {
+    int *__restrict__ m_clear, float4 *__restrict__ rec_zero, int ids_cap) {
     __shared__ int s_hits[kProjThreads / 64];
     const int i = blockIdx.x * kProjThreads + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x == 0) *m_clear = 0;  // the next call's M
@@ -1291,10 +1294,24 @@ __global__ __launch_bounds__(kProjThreads) void tile_insert_ids_kernel(
             const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
             hits = slab_insert_pairs<8>(c.x, c.y, r, tbx, tby, z, z,
                                         make_float4(0.f, __int_as_float(i), 0.f, 0.f), counts,
-                                        nullptr, 0, ids);
+                                        nullptr, 0, ids, ids_cap);
         }
     }
     add_hits(hits, s_hits, m_acc);
+}
+
+// Splat i's 48-byte record for the composite's gather (the frame path's
+// layout: {x, y, a/2, b}, {c/2, opacity, r, g}, {b, id, a, c}): one record per
+// entry instead of eight scattered loads.
+__device__ __forceinline__ void pack_record(int i, const float2 *__restrict__ xys,
+                                            const float *__restrict__ conics,
+                                            const float *__restrict__ colors,
+                                            const float *__restrict__ opac, float4 *__restrict__ rec) {
+    const float2 c = xys[i];
+    const float a = conics[3 * (size_t)i], b = conics[3 * (size_t)i + 1], cc = conics[3 * (size_t)i + 2];
+    rec[3 * (size_t)i] = make_float4(c.x, c.y, 0.5f * a, b);
+    rec[3 * (size_t)i + 1] = make_float4(0.5f * cc, opac[i], colors[3 * (size_t)i], colors[3 * (size_t)i + 1]);
+    rec[3 * (size_t)i + 2] = make_float4(colors[3 * (size_t)i + 2], __int_as_float(i), a, cc);
 }
 
 // The same insertion with a splat order (gsvc_rasterize_sum_forward_slabs_ordered):
@@ -1305,17 +1322,18 @@ __global__ __launch_bounds__(kProjThreads) void tile_insert_ids_kernel(
 // tile)).  The slabs hold the same ids per tile either way; the composite
 // sorts them.  ``key`` (the refresh call): each splat's strip key and id for
 // the next order.
-__global__ __launch_bounds__(kProjThreads) void tile_insert_ids_ordered_kernel(
+template <int kThr>
+__global__ __launch_bounds__(kThr) void tile_insert_ids_ordered_kernel(
     int n, const int *__restrict__ order, const float2 *__restrict__ xys,
     const int *__restrict__ radii, int tbx, int tby, unsigned *__restrict__ counts,
     int *__restrict__ ids, int *__restrict__ m_acc, int *__restrict__ m_clear,
     float4 *__restrict__ rec_zero, unsigned *__restrict__ key, int *__restrict__ key_id,
     unsigned key_invisible, const float *__restrict__ conics, const float *__restrict__ colors,
-    const float *__restrict__ opac, float4 *__restrict__ rec) {
-    __shared__ int s_hits[kProjThreads / 64];
+    const float *__restrict__ opac, float4 *__restrict__ rec, int scatter, int ids_cap) {
+    __shared__ int s_hits[kThr / 64];
     __shared__ unsigned s_cnt[kAggWin];
-    __shared__ int s_box[4][kProjThreads / 64];
-    const int t = blockIdx.x * kProjThreads + threadIdx.x;
+    __shared__ int s_box[4][kThr / 64];
+    const int t = blockIdx.x * kThr + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x == 0) *m_clear = 0;  // the next call's M
     const int i = t < n ? (order ? order[t] : t) : n;
     const bool have = (unsigned)i < (unsigned)n;  // (an unsorted order buffer: nothing)
@@ -1325,8 +1343,25 @@ __global__ __launch_bounds__(kProjThreads) void tile_insert_ids_ordered_kernel(
     S.r0 = S.r1 = make_float4(0.f, 0.f, 0.f, 0.f);
     S.r2 = make_float4(0.f, __int_as_float(i), 0.f, 0.f);  // the id (slab_insert_window's ids)
     unsigned x0 = 0, y0 = 0, x1 = 0, y1 = 0;
-    if (have) {
+    // the gradient records' zeroing, the 48-byte records and the strip keys go
+    // by position t, not by the ordered id i: every id in [0, n) is some t's,
+    // and the stores are coalesced (A/B knob 32 = 1: at i, scattered)
+    const bool by_pos = !(kDiag && scatter);
+    if (by_pos && t < n) {
         if (rec_zero) {
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rec_zero[4 * (size_t)t + q] = z;
+        }
+        if (rec) pack_record(t, xys, conics, colors, opac, rec);
+        if (key) {
+            const float2 c = xys[t];
+            key[t] = strip_key(c.x, c.y, radii[t], tbx, tby, key_invisible);
+            key_id[t] = t;
+        }
+    }
+    if (have) {
+        if (!by_pos && rec_zero) {
             const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
             for (int q = 0; q < 4; ++q) rec_zero[4 * (size_t)i + q] = z;
@@ -1336,24 +1371,16 @@ __global__ __launch_bounds__(kProjThreads) void tile_insert_ids_ordered_kernel(
         S.P.xy = c;
         S.P.rad = r;
         if (r > 0) tile_bbox(c.x, c.y, (float)r, tbx, tby, x0, y0, x1, y1);
-        if (rec) {
-            // the splat's 48-byte record for the composite's gather (the frame
-            // path's layout: {x, y, a/2, b}, {c/2, opacity, r, g}, {b, id, a, c}):
-            // one record per entry instead of eight scattered loads
-            const float a = conics[3 * (size_t)i], b = conics[3 * (size_t)i + 1], cc = conics[3 * (size_t)i + 2];
-            rec[3 * (size_t)i] = make_float4(c.x, c.y, 0.5f * a, b);
-            rec[3 * (size_t)i + 1] = make_float4(0.5f * cc, opac[i], colors[3 * (size_t)i], colors[3 * (size_t)i + 1]);
-            rec[3 * (size_t)i + 2] = make_float4(colors[3 * (size_t)i + 2], __int_as_float(i), a, cc);
-        }
-        if (key) {
+        if (!by_pos && rec) pack_record(i, xys, conics, colors, opac, rec);
+        if (!by_pos && key) {
             key[i] = strip_key(c.x, c.y, r, tbx, tby, key_invisible);
             key_id[i] = i;
         }
     }
     // every lane of the block (block-uniform control flow inside)
-    const int hits = slab_insert_window(S, x0, y0, x1, y1, tbx, tby, counts, nullptr, s_cnt, s_box,
-                                        nullptr, ids);
-    add_hits(hits, s_hits, m_acc);
+    const int hits = slab_insert_window<kThr>(S, x0, y0, x1, y1, tbx, tby, counts, nullptr, s_cnt,
+                                              s_box, nullptr, ids, ids_cap);
+    add_hits<kThr>(hits, s_hits, m_acc);
 }
 
 // The op path's splat-order buffers (n-sized): strip keys and ids, the sorted
@@ -1401,6 +1428,7 @@ void sum_fwd_args_init(SumFwdArgs &A) {
     A.group_min = knob(15) > 0 ? knob(15) - 1 : kGroupMinDefault;
     A.cut = knob(19) != 1;
     A.norank = knob(31) == 1;
+    A.ids_cap = kTilePix;
     A.layout = kLayoutHWC;
     A.frames = 1;
 }
@@ -1567,6 +1595,9 @@ static int forward_slabs_impl(
     unsigned *counts = (unsigned *)workspace;
     int *m_slots = (int *)(counts + 2 * (size_t)ntiles);
     const bool ordered = order_ws && (order_flags & (GSVC_TRAIN_ORDER | GSVC_TRAIN_ORDER_REFRESH));
+    // GSVC_SLABS_WIDE: gaussian_ids holds kCarryCap ids per tile (a tile of up
+    // to 1024 entries sorts its first 256 from them; past that, the bbox rebuild)
+    const int ids_cap = (order_flags & GSVC_SLABS_WIDE) ? kCarryCap : kTilePix;
     OpOrderWs ow{};
     if (ordered) {
         ow = op_order_ws((char *)order_ws, num_points);
@@ -1575,19 +1606,23 @@ static int forward_slabs_impl(
     }
     if (num_points > 0 && ordered) {
         const bool refresh = (order_flags & GSVC_TRAIN_ORDER_REFRESH) != 0;
-        hipLaunchKernelGGL(tile_insert_ids_ordered_kernel, dim3(ceil_div(num_points, kProjThreads)),
-                           dim3(kProjThreads), 0, s, num_points,
+        // A/B knob 33: 128 or 512 threads per workgroup (default kProjThreads)
+        const int thr = knob(33) == 128 || knob(33) == 512 ? knob(33) : kProjThreads;
+        auto kfn = thr == 128 ? tile_insert_ids_ordered_kernel<128>
+                              : (thr == 512 ? tile_insert_ids_ordered_kernel<512>
+                                            : tile_insert_ids_ordered_kernel<kProjThreads>);
+        hipLaunchKernelGGL(kfn, dim3(ceil_div(num_points, thr)), dim3(thr), 0, s, num_points,
                            (order_flags & GSVC_TRAIN_ORDER) ? (const int *)ow.order : nullptr,
                            (const float2 *)xys, radii, tbx, tby, counts + (size_t)par * ntiles,
                            gaussian_ids, m_slots + par, m_slots + (par ^ 1),
                            (float4 *)grad_records_zero, refresh ? ow.okey : nullptr,
                            refresh ? ow.okey_id : nullptr, strip_key_invisible(tbx, tby), conics,
-                           colors, opacities, ow.rec);
+                           colors, opacities, ow.rec, knob(32), ids_cap);
     } else if (num_points > 0) {
         hipLaunchKernelGGL(tile_insert_ids_kernel, dim3(ceil_div(num_points, kProjThreads)),
                            dim3(kProjThreads), 0, s, num_points, (const float2 *)xys, radii, tbx,
                            tby, counts + (size_t)par * ntiles, gaussian_ids, m_slots + par,
-                           m_slots + (par ^ 1), (float4 *)grad_records_zero);
+                           m_slots + (par ^ 1), (float4 *)grad_records_zero, ids_cap);
     } else if (dev_zero(m_slots, 2 * sizeof(int), s) != GSVC_OK) {
         return set_error(GSVC_ERR_HIP, "rasterize_sum_forward_slabs: memset failed");
     }
@@ -1605,6 +1640,7 @@ static int forward_slabs_impl(
     A.id_counts = counts + (size_t)par * ntiles;
     A.id_counts_clear = counts + (size_t)(par ^ 1) * ntiles;
     A.ids_rw = gaussian_ids;
+    A.ids_cap = ids_cap;
     A.bins_out = (int2 *)tile_bins;
     A.cull_xys = (const float2 *)xys;
     A.cull_radii = radii;
@@ -1648,9 +1684,9 @@ extern "C" int gsvc_rasterize_sum_forward_slabs_ordered(
     int *gaussian_ids, int *tile_bins, int *meta, float *grad_records_zero, float *out_img,
     int *final_idx, void *stream, void *order_workspace, size_t order_workspace_bytes,
     int order_flags) {
-    if (order_flags & ~(GSVC_TRAIN_ORDER | GSVC_TRAIN_ORDER_REFRESH))
+    if (order_flags & ~(GSVC_TRAIN_ORDER | GSVC_TRAIN_ORDER_REFRESH | GSVC_SLABS_WIDE))
         return set_error(GSVC_ERR_ARG, "rasterize_sum_forward_slabs_ordered: unknown flags");
-    if (order_flags && !order_workspace)
+    if ((order_flags & (GSVC_TRAIN_ORDER | GSVC_TRAIN_ORDER_REFRESH)) && !order_workspace)
         return set_error(GSVC_ERR_WORKSPACE, "rasterize_sum_forward_slabs_ordered: no order workspace");
     return forward_slabs_impl(num_points, xys, radii, conics, colors, opacities, background,
                               img_height, img_width, call_index, density_hint, workspace,

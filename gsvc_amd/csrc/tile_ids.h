@@ -31,10 +31,15 @@ struct SegIds {
     const int *ids;
     const float4 *recs;  // slab body (slots >= kHeadSlots at their index) ...
     const float4 *head;  // ... and the tile's head slots
+    const int *ovf = nullptr;  // record slabs: slots [256, kCarryCap) as ids
+    int cap_ids = kTilePix;    // id segments: slots per tile (wide id slabs: kCarryCap)
     __device__ __forceinline__ int operator[](int j) const {
         if (!recs) return ids[j];
+        if (j >= kTilePix) return ovf[j - kTilePix];
         return __float_as_int(j < kHeadSlots ? head[3 * j + 2].y : recs[3 * j + 2].y);
     }
+    // slots the segment holds (a longer tile takes the bbox rebuild)
+    __device__ __forceinline__ int cap() const { return recs ? (ovf ? kCarryCap : kTilePix) : cap_ids; }
 };
 
 __device__ __forceinline__ int rank_below(int v, int n) {
@@ -44,12 +49,53 @@ __device__ __forceinline__ int rank_below(int v, int n) {
     return rank;
 }
 
+// The id-window bitmap of the sorts below: 32 * kSortWords ids from ``base``.
+__device__ __forceinline__ void bitmap_clear(unsigned *bm) {
+    for (int w = threadIdx.x & 63; w < kSortWords; w += 64) bm[w] = 0u;
+    wave_lds_sync();
+}
+__device__ __forceinline__ void bitmap_set(unsigned *bm, long long d) {
+    if (d >= 0 && d < 32 * kSortWords) atomicOr(bm + (d >> 5), 1u << (d & 31));
+}
+// The window's ids in ascending order into s_ids[written, 256); returns the
+// new count (possibly past 256: only the first 256 are stored).
+__device__ __forceinline__ int bitmap_emit(const unsigned *bm, long long base, int written,
+                                           int *s_ids) {
+    const int lane = threadIdx.x & 63;
+    constexpr int kPer = kSortWords / 64;  // words per lane, in order
+    unsigned wv[kPer];
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        wv[q] = bm[kPer * lane + q];
+        cnt += __popc(wv[q]);
+    }
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int u = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += u;
+    }
+    int pos = written + incl - cnt;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        unsigned bits = wv[q];
+        while (bits && pos < kTilePix) {
+            s_ids[pos++] = (int)(base + 32 * (kPer * lane + q) + (__ffs(bits) - 1));
+            bits &= bits - 1u;
+        }
+    }
+    written += __shfl(incl, 63, 64);
+    wave_lds_sync();
+    return written;
+}
+
 __device__ inline int wave_sorted_tile_ids(SegIds ids, int n_all, int *s_ids, unsigned *bm) {
     const int lane = threadIdx.x & 63;
     if (n_all <= 0) return 0;
-    // a segment holds at most 256 slots (the slabs' size; a longer tile takes
-    // the bbox rebuild): never read past them, whatever the count says
-    n_all = min(n_all, kTilePix);
+    // a segment holds at most seg.cap() slots (a longer tile takes the bbox
+    // rebuild): never read past them, whatever the count says
+    n_all = min(n_all, ids.cap());
     if (n_all <= 64) {
         const int v = lane < n_all ? ids[lane] : 0x7fffffff;
         const int rank = rank_below(v, n_all);
@@ -70,38 +116,10 @@ __device__ inline int wave_sorted_tile_ids(SegIds ids, int n_all, int *s_ids, un
     }
     int written = 0;
     for (long long base = lo; base <= hi && written < kTilePix; base += 32 * kSortWords) {
-        for (int w = lane; w < kSortWords; w += 64) bm[w] = 0u;
+        bitmap_clear(bm);
+        for (int j = lane; j < n_all; j += 64) bitmap_set(bm, (long long)ids[j] - base);
         wave_lds_sync();
-        for (int j = lane; j < n_all; j += 64) {
-            const long long d = (long long)ids[j] - base;
-            if (d >= 0 && d < 32 * kSortWords) atomicOr(bm + (d >> 5), 1u << (d & 31));
-        }
-        wave_lds_sync();
-        constexpr int kPer = kSortWords / 64;  // words per lane, in order
-        unsigned wv[kPer];
-        int cnt = 0;
-#pragma unroll
-        for (int q = 0; q < kPer; ++q) {
-            wv[q] = bm[kPer * lane + q];
-            cnt += __popc(wv[q]);
-        }
-        int incl = cnt;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int u = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += u;
-        }
-        int pos = written + incl - cnt;
-#pragma unroll
-        for (int q = 0; q < kPer; ++q) {
-            unsigned bits = wv[q];
-            while (bits && pos < kTilePix) {
-                s_ids[pos++] = (int)(base + 32 * (kPer * lane + q) + (__ffs(bits) - 1));
-                bits &= bits - 1u;
-            }
-        }
-        written += __shfl(incl, 63, 64);
-        wave_lds_sync();
+        written = bitmap_emit(bm, base, written, s_ids);
     }
     return min(written, kTilePix);
 }
@@ -109,29 +127,40 @@ __device__ inline int wave_sorted_tile_ids(SegIds ids, int n_all, int *s_ids, un
 // A tile with more than 256 entries on the frame path (its slab kept an
 // arbitrary 256): its first 256 ids are rebuilt by testing every splat's tile
 // bbox (the binning's own tile_bbox of xys and radii) in id order, 64 at a
-// time, compacting the hits by ballot -- sorted by construction.
+// time, compacting the hits by ballot -- sorted by construction.  The
+// fallback of every tile kernel for a tile past its slab's capacity.
 __device__ __forceinline__ int wave_brute_ids(const float2 *xys, const int *radii, int begin,
                                               int end, int tbx, int tby, int tile, int *s_ids) {
     const int lane = threadIdx.x & 63;
     const unsigned ty = (unsigned)(tile / tbx), tx = (unsigned)(tile - (int)ty * tbx);
     const unsigned long long lt = (1ull << lane) - 1ull;
+    // kQ batches of 64 splats per round, every load issued before the first
+    // test (one round trip per 64 kQ splats; a load per batch behind the
+    // previous batch's ballot made it one per 64, ~0.6 ms at 50k splats)
+    constexpr int kQ = 4;
     int written = 0;
-    for (int base = begin; base < end && written < kTilePix; base += 64) {
-        const int j = base + lane;
-        bool hit = false;
-        if (j < end) {
-            const int r = radii[j];
-            if (r > 0) {
-                const float2 c = xys[j];
+    for (int base = begin; base < end && written < kTilePix; base += 64 * kQ) {
+        int r[kQ];
+        float2 c[kQ];
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const int j = min(base + 64 * q + lane, end - 1);
+            r[q] = radii[j];
+            c[q] = xys[j];
+        }
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            bool hit = false;
+            if (base + 64 * q + lane < end && r[q] > 0) {
                 unsigned x0, y0, x1, y1;
-                tile_bbox(c.x, c.y, (float)r, tbx, tby, x0, y0, x1, y1);
+                tile_bbox(c[q].x, c[q].y, (float)r[q], tbx, tby, x0, y0, x1, y1);
                 hit = tx >= x0 && tx < x1 && ty >= y0 && ty < y1;
             }
+            const unsigned long long m = __ballot(hit);
+            const int pos = written + __popcll(m & lt);
+            if (hit && pos < kTilePix) s_ids[pos] = base + 64 * q + lane;
+            written += __popcll(m);
         }
-        const unsigned long long m = __ballot(hit);
-        const int pos = written + __popcll(m & lt);
-        if (hit && pos < kTilePix) s_ids[pos] = j;
-        written += __popcll(m);
     }
     wave_lds_sync();
     return min(written, kTilePix);

@@ -280,12 +280,17 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
         const auto f = xys.options();
         const auto i = f.dtype(at::kInt);
         void *st = stream_of(xys);
-        Tensor gids = at::empty({(int64_t)nt * kTileKeep}, i), bins = at::empty({nt, 2}, i);
+        // the slab route's ids: GSVC_SLABS_WIDE_IDS per tile (a tile of up to 1024
+        // entries sorts its first 256 from its slab; the capture route's
+        // counted binning keeps 256)
+        const bool capture = capturing(st);
+        Tensor gids = at::empty({(int64_t)nt * (capture ? kTileKeep : GSVC_SLABS_WIDE_IDS)}, i);
+        Tensor bins = at::empty({nt, 2}, i);
         // no final_idx: the backward (raster_sum_bwd_kernel) does not read it --
         // an entry past a pixel's final index fails the alpha test there anyway
         Tensor meta = at::empty({2}, i), out = at::empty({H, W, 3}, f);
         Tensor rec;
-        if (capturing(st)) {
+        if (capture) {
             // Graph capture: the slab workspace's parity is host state a replay
             // would freeze, so the capturable route -- the counted binning (its
             // scratch allocated per call, from the graph's pool) and the
@@ -319,7 +324,7 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
                 (unsigned)H, (unsigned)W, ws.calls, hint, ws.buf.data_ptr(),
                 4 * (size_t)ws.buf.numel(), ip(gids), ip(bins), ip(meta), fp(rec), fp(out), nullptr,
                 st, oflags ? ws.order.data_ptr() : nullptr, oflags ? (size_t)ws.order.numel() : 0,
-                oflags);
+                oflags | GSVC_SLABS_WIDE);
             if (rc != 0) ws.tiles = -1;  // counters and order in an unknown state: rebuild
             check(rc, "gsvc_rasterize_sum_forward_slabs_ordered");
             ++ws.calls;

@@ -44,6 +44,7 @@ struct TrainTileArgs {
     int tbx, img_w, img_h, ntiles, num_points, loss_l1;
     float norm;  // d loss / d pixel scale: float(2 / numel) for L2, 1.0f / numel for L1
     float4 *slab;  // read; a dense tile parks its sorted ids in its own slab
+    const int *ovf;  // the slab's slots 256 .. kCarryCap - 1 as ids (frame.h FrameWs.ovf)
     const unsigned *counts;
     unsigned *counts_clear;
     const int *m_dev;
@@ -602,6 +603,57 @@ __device__ __forceinline__ void publish_loss(const float2 *err, int ntiles, doub
 }
 
 
+// Carried bins of a tile with 256 < n <= kCarryCap candidates (wave 0): the
+// ascending ids of the candidates whose current box holds the tile -- the
+// first <= 256 members -- into s_out, by the id-window bitmap (tile_ids.h).
+// Ids are unique within a tile's candidates.  Per lane a mask of which of its
+// candidates (lane + 64 k) are members; each window re-reads the candidate
+// ids (L2-resident) four rows at a time.
+__device__ int wave_sorted_members(const int *cand, int n, const uint2 *cbox, unsigned tx,
+                                   unsigned ty, int *s_out, unsigned *bm) {
+    const int lane = threadIdx.x & 63;
+    constexpr int kRows = kCarryCap / 64, kQ = 4;
+    n = min(n, kCarryCap);
+    unsigned mem = 0u;
+    int lo = 0x7fffffff, hi = -1;
+    for (int k0 = 0; k0 < kRows && 64 * k0 < n; k0 += kQ) {
+        int id[kQ];
+        uint2 b[kQ];
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) id[q] = cand[min(lane + 64 * (k0 + q), n - 1)];
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) b[q] = cbox[id[q]];
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            if (lane + 64 * (k0 + q) < n && box_has(b[q], tx, ty)) {
+                mem |= 1u << (k0 + q);
+                lo = min(lo, id[q]);
+                hi = max(hi, id[q]);
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = min(lo, __shfl_xor(lo, off, 64));
+        hi = max(hi, __shfl_xor(hi, off, 64));
+    }
+    int written = 0;
+    for (long long base = lo; base <= hi && written < kTilePix; base += 32 * kSortWords) {
+        bitmap_clear(bm);
+        for (int k0 = 0; k0 < kRows && 64 * k0 < n; k0 += kQ) {
+            int id[kQ];
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) id[q] = cand[min(lane + 64 * (k0 + q), n - 1)];
+#pragma unroll
+            for (int q = 0; q < kQ; ++q)
+                if ((mem >> (k0 + q)) & 1u) bitmap_set(bm, (long long)id[q] - base);
+        }
+        wave_lds_sync();
+        written = bitmap_emit(bm, base, written, s_out);
+    }
+    return min(written, kTilePix);
+}
+
 struct BandLds {
     float v[3][kTile * kVRow];     // v_out planes, rows padded to kVRow words
     float4 geo[kBChunk + 1];       // staged entries (rank order): x, y, a/2, b
@@ -655,7 +707,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     const unsigned srt_raw = kCarry && A.csorted ? A.csorted[tile] : 0u;
     float4 r0, r1, r2;
     int cid = 0;  // carried bins: the lane's candidate id
-    int *tcids = carry ? A.cids + (size_t)tile * kTilePix : nullptr;
+    int *tcids = carry ? A.cids + (size_t)tile * kCarryCap : nullptr;
     if (carry) {
         cid = tcids[tid < spec_of(A) ? tid : 0];
     } else {
@@ -776,8 +828,23 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
         }
     } else if (brute) {
         if (w == 0) {
-            n = wave_brute_ids(A.xys, A.radii, 0, A.num_points, A.tbx,
-                               (A.img_h + kTile - 1) / kTile, tile, s_key);
+            // carried bins of <= kCarryCap candidates: the members sorted from
+            // the list (the bbox rebuild over every splat costs ~0.6 ms)
+            unsigned *bm = reinterpret_cast<unsigned *>(&S.part[4][0]);
+            if (carry && n_all <= kCarryCap) {
+                n = wave_sorted_members(tcids, n_all, A.cbox, (unsigned)tx, (unsigned)ty, s_key, bm);
+            } else if (!carry && A.ovf && n_all <= kCarryCap) {
+                // record slab + its overflow ids: the first 256 ids sorted from both
+                SegIds seg;
+                seg.ids = nullptr;
+                seg.recs = slab_rec(A.slab, A.ntiles, tile, kHeadSlots) - 3 * kHeadSlots;
+                seg.head = slab_rec(A.slab, A.ntiles, tile, 0);
+                seg.ovf = A.ovf + (size_t)tile * kOvfSlots;
+                n = wave_sorted_tile_ids(seg, n_all, s_key, bm);
+            } else {
+                n = wave_brute_ids(A.xys, A.radii, 0, A.num_points, A.tbx,
+                                   (A.img_h + kTile - 1) / kTile, tile, s_key);
+            }
             if (lane == 0) S.nsel = n;
         }
         // both waves: wave_brute_ids finds >= 256 of them (carried bins: the
@@ -1322,7 +1389,7 @@ __device__ __forceinline__ int carry_splat(const TrainSplatArgs &A, int i, const
                 if (hv && x >= hx0 && x < hx1 && y >= hy0 && y < hy1) continue;
                 const unsigned t = y * (unsigned)A.tbx + x;
                 const unsigned sl = atomicAdd(A.ccount + t, 1u);
-                if (sl < (unsigned)kTilePix) A.cids[(size_t)t * kTilePix + sl] = i;
+                if (sl < (unsigned)kCarryCap) A.cids[(size_t)t * kCarryCap + sl] = i;
             }
         A.chull[i] = pack_box(ux0, uy0, ux1, uy1);
     }
@@ -1573,7 +1640,7 @@ static TrainWs train_ws(char *base, int n, int ntiles) {
     };
     w.grad = (float4 *)take(sizeof(float4) * 4 * nn);
     w.err = (float2 *)take(sizeof(float2) * nt);
-    w.cids = (int *)take(sizeof(int) * kTilePix * nt);
+    w.cids = (int *)take(sizeof(int) * kCarryCap * nt);
     w.ccount = (unsigned *)take(sizeof(unsigned) * 2 * nt);  // ccount[T], csorted[T]
     w.csorted = w.ccount ? w.ccount + nt : nullptr;
     w.cbox = (uint2 *)take(sizeof(uint2) * nn);
@@ -1746,6 +1813,7 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     T.loss_l1 = loss_kind;
     T.norm = loss_kind ? 1.0f / (float)count : (float)(2.0 / count);
     T.slab = w.f.slab;
+    T.ovf = w.f.ovf;
     T.xys = w.f.xys;
     T.radii = w.f.radii;
     T.rec = w.f.rec;

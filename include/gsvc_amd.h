@@ -317,7 +317,14 @@ int gsvc_rasterize_sum_forward_slabs(
  * num_points sorted (by the tile strip of their centres), so a workgroup's
  * slot atomics aggregate per tile; GSVC_TRAIN_ORDER_REFRESH sorts a new one
  * from this call's xys.  order_workspace: gsvc_rasterize_sum_order_workspace_bytes
- * (num_points) bytes, no initial contents.  Not part of the reference. */
+ * (num_points) bytes, no initial contents.  order_flags GSVC_SLABS_WIDE (with
+ * or without an order): gaussian_ids holds GSVC_SLABS_WIDE_IDS ids per tile
+ * ([T * 1024], tile t's at t * 1024, tile_bins [t * 1024, t * 1024 + n)): a
+ * tile of up to 1024 entries sorts its first 256 from its slab instead of
+ * rebuilding them from every splat's bbox (dense content).  Not part of the
+ * reference. */
+#define GSVC_SLABS_WIDE 0x80000
+#define GSVC_SLABS_WIDE_IDS 1024
 size_t gsvc_rasterize_sum_order_workspace_bytes(int num_points);
 int gsvc_rasterize_sum_forward_slabs_ordered(
     int num_points, const float *xys, const int *radii, const float *conics,

@@ -5,7 +5,7 @@ are split into groups that each walk only the entries whose alpha >= 1/255
 rectangle reaches the group's sub-rectangle (iterations = the longest group
 list), against the whole band walking the band's union (the current kernel).
 
-    python tools/fwd_sim.py gpurun_out/trained_50k.npz [--tiles 4]
+    python tests/analysis/fwd_sim.py gpurun_out/trained_50k.npz [--tiles 4]
 """
 from __future__ import annotations
 
@@ -15,7 +15,7 @@ import sys
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tools"))
 

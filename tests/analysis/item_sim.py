@@ -4,7 +4,7 @@ tools/dump_trained.py: per tile and 8-row band, the entries' alpha >= 1/255
 rectangles, the work items each layout makes of them, and the rounds of 64
 items a wave runs -- so item layouts can be compared without a GPU.
 
-    python tools/item_sim.py gpurun_out/trained_50k.npz
+    python tests/analysis/item_sim.py gpurun_out/trained_50k.npz
 
 Cost model (VALU instructions per wave, calibrated against PMC
 SQ_INSTS_VALU of the kernel): a round costs R + P * (its longest item's
@@ -18,7 +18,7 @@ import sys
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, REPO)
 
 from oracle import oracle as O  # noqa: E402  (checker/analysis only)

@@ -1,6 +1,6 @@
 """Microbenchmark of the composite kernels (rasterize_sum forward/backward).
 
-    python tools/kbench.py [--splats 10000 50000] [--variants 0 1] [--iters 200]
+    python tests/analysis/kbench.py [--splats 10000 50000] [--variants 0 1] [--iters 200]
 
 Sets up a 1920x1080 frame (reference init distributions), bins it, then for
 each kernel variant (C-ABI knob gsvc_debug_set(0, v); 0 = automatic) captures ``iters``
@@ -17,7 +17,7 @@ import json
 import os
 import sys
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 

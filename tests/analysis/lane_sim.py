@@ -13,9 +13,9 @@ runs (= the longest list among its lanes / lane groups) and how many of the
                    row-span test, what a kernel can compute per (entry, row))
   lane 2x2 span    lanes own 2x2 quads
 
-    python tools/lane_sim.py STATE.npz [--tiles 4]
+    python tests/analysis/lane_sim.py STATE.npz [--tiles 4]
 
-STATE.npz: tools/train_oracle_state.py / dump_trained.py output (raw
+STATE.npz: tests/analysis/train_oracle_state.py / dump_trained.py output (raw
 parameters) or a fixture with state_* keys.
 """
 from __future__ import annotations
@@ -26,7 +26,7 @@ import sys
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 

@@ -6,7 +6,7 @@ span of sigma <= the cut (the quadratic's roots, with a margin).  A round of 64
 items costs its longest item; items are laid out longest first in four classes
 as the kernel does.  Analysis only (CPU).
 
-    python tools/span_sim.py [--tiles 8160]
+    python tests/analysis/span_sim.py [--tiles 8160]
 """
 import argparse
 import os
@@ -14,7 +14,7 @@ import sys
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 import oracle as O  # noqa: E402

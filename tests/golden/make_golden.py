@@ -23,7 +23,7 @@ committed.  Five kinds of fixtures are produced:
    the reference model on CPU, oracle injected.
 4. ``train_state_1080p_n50k.npz`` (``make_golden.py trained STATE.npz``): the
    state bench.py times -- its 1080p / 50k frame after 2020 training
-   iterations, trained on the CPU by the oracle (tools/train_oracle_state.py)
+   iterations, trained on the CPU by the oracle (tests/analysis/train_oracle_state.py)
    -- and the reference's own forward / backward / three train_iter steps
    from it (make_trained_state_case).
 5. ``prune_controls.npz``: ``removal_control`` / ``adaptive_control``
@@ -431,7 +431,7 @@ def make_trained_state_case(state_path, name="train_state_1080p_n50k", steps=3, 
     """BASELINE configs[2] at the state bench.py times: the bench's 1080p / 50k
     frame (seed 1000, target seed 8) after its settle + warmup iterations
     (trained density, M ~ 230-240k), trained on the CPU by the oracle's
-    train_iter_sum (tools/train_oracle_state.py), loaded here into the
+    train_iter_sum (tests/analysis/train_oracle_state.py), loaded here into the
     reference model.  Records, from the reference's own Python with the oracle
     injected (GaussianSplats_Represent.py:83-90,191-207, fresh Adan):
 

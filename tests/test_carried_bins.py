@@ -62,13 +62,16 @@ def test_carried_equals_reprojected_through_rebuilds(cuda, deterministic):
     _same(_run(cuda, True, 256, 256, 2000, 70), _run(cuda, False, 256, 256, 2000, 70))
 
 
-def test_carried_fast_motion_and_overflow(cuda, deterministic):
+@pytest.mark.parametrize("every", [4, 12])
+def test_carried_fast_motion_and_overflow(cuda, deterministic, every):
     """lr 0.05: splats jump tiles every step (many appends, hulls growing
-    across the image); a quarter of 6000 splats piled on one spot overflows
-    that tile's 256 candidates (the bbox rebuild path); no rebuild for 40 steps."""
+    across the image); every 4th of 6000 splats piled on one spot overflows
+    that tile's kCarryCap = 1024 candidates (the bbox rebuild path), every 12th
+    (500) passes 256 but not 1024 (the members sorted from the candidate list,
+    train.hip wave_sorted_members); no rebuild for 40 steps."""
     def pile(m):
         with torch.no_grad():
-            sel = torch.arange(0, m._xyz.shape[0], 4, device=m._xyz.device)
+            sel = torch.arange(0, m._xyz.shape[0], every, device=m._xyz.device)
             m._xyz[sel] = torch.atanh(torch.full((len(sel), 2), -0.25, device=m._xyz.device)
                                       + 0.05 * torch.rand(len(sel), 2, device=m._xyz.device))
             m._cholesky[sel] = torch.tensor([2.5, 0.3, 1.5], device=m._xyz.device)

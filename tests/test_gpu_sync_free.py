@@ -327,8 +327,9 @@ def test_tanh_matches_torch(cuda):
     from gsvc_amd.render import _workspaces
     fw = _workspaces[(0, torch.cuda.current_stream().cuda_stream)]
     # counts + M slots (256-aligned), then one tile's slab region: the 8-record
-    # head and the 256-record body (frame.h slab_frame_f4), 256-aligned
-    off = 256 + ((8 + 256) * 48 + 255) // 256 * 256
+    # head and the 256-record body (frame.h slab_frame_f4), then its overflow
+    # ids (768 ints: slots 256 .. 1023), each 256-aligned
+    off = 256 + ((8 + 256) * 48 + 255) // 256 * 256 + (768 * 4 + 255) // 256 * 256
     xys = fw.buf[off: off + 8 * n].view(torch.float32).view(n, 2)
     assert torch.equal(xys, ref)
 

@@ -2,8 +2,9 @@
 default for sparse frames) against the render over 48-byte
 slab records (A/B knob 24 = 1, diagnostic library) and the banded kernel
 (knob 0 = 2, records).  Same entries per tile, same id order, same blend: the
-images must be bit-identical, including tiles past 256 entries (their first
-256 ids rebuilt from the bboxes), ragged image sizes and a frame with no
+images must be bit-identical, including tiles past 256 entries (the id
+slabs: their first 256 ids rebuilt from the bboxes; the record slabs: sorted
+from the slab and its overflow ids up to 1024 entries, rebuilt past that), ragged image sizes and a frame with no
 intersections (rasterize_sum.py:121-127's background) -- and within 1e-5 of
 the C oracle's render of the same activations.  The calls go through
 render_frame_sum, i.e. the ordered projection after the first call."""
@@ -31,6 +32,7 @@ def _frame(n, seed, chol, dev, cluster=0.0):
     (10000, 1080, 1920, 1.0, 0.0),
     (50000, 1080, 1920, 3.0, 0.0),
     (20000, 360, 640, 1.0, 0.2),   # tiles past 256 entries
+    (20000, 360, 640, 1.0, 0.03),  # past 256 but within the record slabs' overflow ids (1024)
     (3000, 250, 333, 1.0, 0.0),    # ragged edge tiles
     (500, 128, 128, 0.0, 0.0),     # L = 0 (no bound): no intersections, the background
 ])

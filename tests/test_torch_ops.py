@@ -214,7 +214,7 @@ def test_cpp_functions_splat_order_bit_identical(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,chol", [(9000, 0.4), (24000, 0.4)])
+@pytest.mark.parametrize("n,chol", [(9000, 0.4), (24000, 0.4), (60000, 0.4)])
 def test_cpp_function_banded_id_slabs(cuda, n, chol):
     """A dense frame (> 96 entries per tile on average): once the lazy M hint
     has seen it, the C++ Function's composite takes the banded kernel over the
@@ -223,7 +223,8 @@ def test_cpp_function_banded_id_slabs(cuda, n, chol):
     the slots wave 0 rewrites).  Every call (the first sparse, the rest
     banded) equals the Python Function (counted binning) bit for bit in the
     image, and its gradients within the atomics' order; 24k splats on 64 tiles
-    also pass 256 entries per tile (the bbox rebuild)."""
+    pass 256 entries per tile (sorted from the wide id slabs, GSVC_SLABS_WIDE:
+    1024 ids per tile), 60k pass 1024 (the bbox rebuild)."""
     H = W = 128
     means, L, col = _inputs(n, H, W, 77 + n, cuda, chol)
     v_out = torch.randn(H, W, 3, generator=torch.Generator().manual_seed(5)).to(cuda)

@@ -7,7 +7,7 @@ occupancy).
 
 Fixture ``train_state_1080p_n50k`` (tests/golden/make_golden.py ``trained``):
 the state was trained on the CPU by the oracle's train_iter_sum
-(tools/train_oracle_state.py); from it the reference's own Python
+(tests/analysis/train_oracle_state.py); from it the reference's own Python
 (GaussianSplats_Represent.py:83-90,191-207, gsplat glue, Adan; oracle kernels
 injected, fresh optimizer) recorded the render (checksums + crops), the L2
 loss, the parameter gradients and three train_iter steps.

@@ -4,7 +4,11 @@ bench's trained 1080p / 50k state, with an optional A/B pass of
 gsvc_debug_set(KEY, VALUE).  Run it under
 ``rocprofv3 --kernel-trace --stats`` for the two kernels' times.
 
-    python tools/slabbench.py [--calls 200] [--knob KEY VALUE]
+    python tools/slabbench.py [--calls 200] [--knob KEY VALUE] [--ordered]
+
+--ordered: the C++ operator's call (torch_ops.cpp RasterSumFn): the ordered
+insertion with its order workspace (refreshed every 64 calls), the gradient
+records zeroed by the insertion, no final_idx.
 """
 import argparse
 import json
@@ -29,6 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=200)
     ap.add_argument("--knob", type=int, nargs=2, action="append", default=[])
+    ap.add_argument("--ordered", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     lib = L.load()
@@ -53,13 +58,28 @@ def main():
     idx = torch.empty((H, W), dtype=torch.int32, device=dev)
     calls = [0]
 
-    def fwd():
+    ORDER, REFRESH = 0x200, 0x400
+    ows = torch.empty(L.size("gsvc_rasterize_sum_order_workspace_bytes", n), dtype=torch.uint8,
+                      device=dev)
+    rec = torch.empty((n, 16), device=dev)
+
+    def fwd_ordered():
+        k = calls[0]
+        flags = REFRESH if k == 0 else (ORDER | (REFRESH if k % 64 == 63 else 0))
+        L.call("gsvc_rasterize_sum_forward_slabs_ordered", n, L.ptr(xys), L.ptr(radii),
+               L.ptr(conics), L.ptr(feat), L.ptr(opac), L.ptr(bg), H, W, k, 250000, L.ptr(ws),
+               4 * ws.numel(), L.ptr(gids), L.ptr(bins), L.ptr(meta), L.ptr(rec), L.ptr(out),
+               None, L.stream(dev), L.ptr(ows), ows.numel(), flags)
+        calls[0] += 1
+
+    def fwd_plain():
         L.call("gsvc_rasterize_sum_forward_slabs", n, L.ptr(xys), L.ptr(radii), L.ptr(conics),
                L.ptr(feat), L.ptr(opac), L.ptr(bg), H, W, calls[0], 250000, L.ptr(ws),
                4 * ws.numel(), L.ptr(gids), L.ptr(bins), L.ptr(meta), None, L.ptr(out), L.ptr(idx),
                L.stream(dev))
         calls[0] += 1
 
+    fwd = fwd_ordered if a.ordered else fwd_plain
     ref = None
     for kv in [None] + a.knob:
         if kv and lib.gsvc_debug_set(kv[0], kv[1]) < 0:
