@@ -475,6 +475,9 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         for (int j = 0; j < 3; ++j) {
             const int c = j * 64 + lane;
             const int row = c / 12, cc = c - row * 12;
+            // plain stores: written through (sc1 nt, as the planes are) this
+            // layout lost whole 192-byte tile rows now and then (round 5,
+            // tools/op_mismatch.py: 70-100 random tiles per 1080p frame)
             if (ty * kTile + row < A.img_h)
                 *reinterpret_cast<float4 *>(A.out + tile_base + (size_t)row * A.img_w * 3 + cc * 4) =
                     s_slice[c];
@@ -679,23 +682,35 @@ __device__ __forceinline__ void write_sorted_ids(const SumFwdArgs &A, int tile, 
 // mode 128-thread workgroups (two waves per tile).
 // kIdx: final_idx is written (the autograd forward); the render paths launch
 // the kIdx = false instance, which tracks no indices.
-template <int kMode, bool kIdx>
+// kTPW (one-wave modes): tiles per workgroup, one per wave (A/B knob 35: the
+// workgroup dispatch rate sets a 2.4 us spread over 8160 one-wave workgroups)
+template <int kMode, bool kIdx, int kTPW = 1>
 __global__ __launch_bounds__(kMode == kModeSparse || kMode == kModeSparseStamp || kMode == kModeSparsePrio ||
-                              kMode == kModeSparseIds ? 64 : 128, 8) void
+                              kMode == kModeSparseIds ? 64 * kTPW : 128, 8) void
 raster_sum_fwd_kernel(SumFwdArgs A) {
     constexpr bool kOneWave = kMode == kModeSparse || kMode == kModeSparseStamp || kMode == kModeSparsePrio ||
                               kMode == kModeSparseIds;
+    static_assert(kTPW == 1 || kOneWave, "several tiles per workgroup: one-wave modes only");
     // id slabs: the op path's autograd forward (kIdx, or sparse / banded
     // without final_idx) and the single-frame render
     constexpr bool kIds = kIdx || kMode == kModeSparseIds || kMode == kModeBanded;
-    __shared__ float4 s_buf[kOneWave ? 1 : 2][kSlice];
-    __shared__ int s_ids[1][kTilePix];  // the tile's sorted ids (one copy per tile)
+    __shared__ float4 s_buf[kOneWave ? kTPW : 2][kSlice];
+    __shared__ int s_ids[kTPW][kTilePix];  // the tile's sorted ids (one copy per tile)
     // raised wave priority over the staging (loads, ranking, lists): the
     // arbiter favours older waves, so a young wave would otherwise wait behind
     // its elders' blending to issue its round trips (train.hip, same reason)
     if (kMode == kModeSparsePrio) __builtin_amdgcn_s_setprio(3);
     const int w = kOneWave ? 0 : (threadIdx.x >> 6);
-    int tile = xcd_remap(blockIdx.x, A.ntiles * A.frames);
+    // this wave's tile of the workgroup's (wave-uniform: a scalar register)
+    const int sub = kTPW > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+    int tile;
+    if (kTPW > 1) {
+        const int total = A.ntiles * A.frames;
+        tile = xcd_remap(blockIdx.x, (total + kTPW - 1) / kTPW) * kTPW + sub;
+        if (tile >= total) return;  // (one-wave modes: no workgroup barrier)
+    } else {
+        tile = xcd_remap(blockIdx.x, A.ntiles * A.frames);
+    }
     if (A.frames > 1) {  // batched frames: this block's frame and tile
         const int b = tile / A.ntiles;
         tile -= b * A.ntiles;
@@ -737,7 +752,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
             spec1 = h[1];
             spec2 = h[2];
         }
-        if (threadIdx.x == 0) {
+        if ((threadIdx.x & 63) == 0) {
             A.slab_counts_clear[tile] = 0u;  // the next frame's counts
             if (tile == 0) {
                 A.meta_out[0] = *A.m_dev;
@@ -761,7 +776,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         // the trained 1080p / 50k frame -- its ids stay read after the count)
         if (kMode == kModeSparseIds)
             spec_id = A.ids_rw[(size_t)tile * A.ids_cap + (threadIdx.x & 63)];
-        if (threadIdx.x == 0) {
+        if ((threadIdx.x & 63) == 0) {
             A.id_counts_clear[tile] = 0u;  // the next call's counts
             if (tile == 0) {
                 A.meta_out[0] = *A.m_dev;
@@ -795,7 +810,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         init = make_float3(A.bg[0], A.bg[1], A.bg[2]);
     }
     const int ty = tile / A.tbx;
-    if (kMode == kModeSparseStamp && threadIdx.x == 0) A.stamps[4 * (size_t)tile] = t0;
+    if (kMode == kModeSparseStamp && (threadIdx.x & 63) == 0) A.stamps[4 * (size_t)tile] = t0;
     const bool sparse = kMode == kModeSparse || kMode == kModeSparseStamp || kMode == kModeSparsePrio ||
                         kMode == kModeSparseIds ||
                         ((kMode == kModeAdaptive || kMode == kModeStamp) && n <= A.sparse_max);
@@ -805,12 +820,12 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         if (w != 0) return;
         if (by_ids)
             n = ((A.slab || (kIds && A.id_counts)) && n_all > seg.cap())
-                    ? wave_brute_tile_ids(A, tile, s_ids[0])
-                    : wave_sorted_tile_ids(seg, n_all, s_ids[0], reinterpret_cast<unsigned *>(s_buf[0]));
+                    ? wave_brute_tile_ids(A, tile, s_ids[sub])
+                    : wave_sorted_tile_ids(seg, n_all, s_ids[sub], reinterpret_cast<unsigned *>(s_buf[sub]));
         // the op path: the tile's sorted ids and bins for the backward (a tile
         // staged straight from its id slab writes them in sum_fwd_sparse)
-        if (A.bins_out && A.id_counts && !seg_rec) write_sorted_ids(A, tile, range.x, n, s_ids[0]);
-        sum_fwd_sparse<kMode, kIdx>(A, tile, range, n, s_buf[0], init, by_ids, s_ids[0], seg_rec,
+        if (A.bins_out && A.id_counts && !seg_rec) write_sorted_ids(A, tile, range.x, n, s_ids[sub]);
+        sum_fwd_sparse<kMode, kIdx>(A, tile, range, n, s_buf[sub], init, by_ids, s_ids[sub], seg_rec,
                                     seg.head, spec0, spec1, spec2, seg.head ? A.spec_slots : 0,
                                     spec_id);
     } else {
@@ -821,17 +836,17 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
             __shared__ int s_n;
             if (w == 0) {
                 const int ns = ((A.slab || (kIds && A.id_counts)) && n_all > seg.cap())
-                                   ? wave_brute_tile_ids(A, tile, s_ids[0])
-                                   : wave_sorted_tile_ids(seg, n_all, s_ids[0],
-                                                          reinterpret_cast<unsigned *>(s_buf[0]));
+                                   ? wave_brute_tile_ids(A, tile, s_ids[sub])
+                                   : wave_sorted_tile_ids(seg, n_all, s_ids[sub],
+                                                          reinterpret_cast<unsigned *>(s_buf[sub]));
                 if ((threadIdx.x & 63) == 0) s_n = ns;
             }
             __syncthreads();
             n = s_n;
-            if (A.bins_out && A.id_counts && w == 0) write_sorted_ids(A, tile, range.x, n, s_ids[0]);
+            if (A.bins_out && A.id_counts && w == 0) write_sorted_ids(A, tile, range.x, n, s_ids[sub]);
         }
         if (ty * kTile + w * 8 >= A.img_h) return;  // band below the image
-        sum_fwd_band<kMode, kIdx>(A, tile, w, range, n, s_buf[w], init, by_ids, s_ids[0], seg_rec,
+        sum_fwd_band<kMode, kIdx>(A, tile, w, range, n, s_buf[w], init, by_ids, s_ids[sub], seg_rec,
                                   seg.head, spec0, spec1, spec2);
     }
     if (kMode == kModeStamp && (threadIdx.x & 63) == 0) {
@@ -1473,7 +1488,18 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
                                : raster_sum_fwd_kernel<kModeBanded, false>,
                    grid, dim3(128), s, tev, A);
     } else if (mode == kModeSparseIds) {
-        launch_fwd(raster_sum_fwd_kernel<kModeSparseIds, false>, grid, dim3(64), s, tev, A);
+        bool done = false;
+        if constexpr (kDiag) {
+            if (knob(35) == 2 || knob(35) == 4) {  // A/B: tiles per workgroup
+                const int k = knob(35);
+                const dim3 g2(ceil_div(ntiles * A.frames, k));
+                launch_fwd(k == 2 ? raster_sum_fwd_kernel<kModeSparseIds, false, 2>
+                                  : raster_sum_fwd_kernel<kModeSparseIds, false, 4>,
+                           g2, dim3(64 * k), s, tev, A);
+                done = true;
+            }
+        }
+        if (!done) launch_fwd(raster_sum_fwd_kernel<kModeSparseIds, false>, grid, dim3(64), s, tev, A);
     } else if constexpr (kDiag) {
         // diagnostic variants (libgsvc_amd_diag.so only)
         switch (mode) {

@@ -1340,6 +1340,7 @@ struct TrainSplatArgs {
     int *cids;
     int *m_next;
     long long *stamps;  // diagnostic: int64[waves][8]
+    int split;          // two waves per 64 splats (splat_step_split); 0: one lane per splat
 };
 
 // GSVC_TRAIN_CARRY: splat i's projection for the next frame from its updated
@@ -1584,6 +1585,179 @@ __device__ __forceinline__ int splat_step(const TrainSplatArgs &A, int i, long l
     return hits;
 }
 
+// splat_step over two waves per 64 splats (256-thread workgroups: 128
+// splats, waves 0 / 2 their geometry halves, 1 / 3 their colour halves): the
+// colour wave loads the colour gradient, the features, rgb_W and their Adan
+// rows, updates them and hands the new values over LDS; the geometry wave
+// does the projection VJP, the xyz / cholesky Adan elements and, after the
+// barrier, the carry (it needs all nine new values).  The same op sequence
+// per element as splat_step, so the same bits; twice the waves, each with
+// about half the loads and Adan work (782 one-wave latency chains on 1024
+// SIMDs were the kernel).  Not for the deterministic mode (its
+// partial sums stay in splat_step).
+__device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int base) {
+    __shared__ float s_cp[2][4][64];  // per splat group: new feature r g b, rgb_W
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, grp = w >> 1;
+    const int i = base + grp * 64 + lane;
+    const bool have = i < A.n;
+    const int ic = have ? i : 0;  // loads of lanes past n: splat 0, unused
+    const bool upd = A.update != 0;
+    int hits = 0;
+    float pnew[5];
+    uint2 hull = make_uint2(0u, 0u);
+    if (w & 1) {
+        // colour half: elements 5-7 (features) and 8 (rgb_W)
+        const float4 g1 = A.grad[4 * ic + 1];  // v_conic 2, v_colors r g b
+        const float f0 = A.feat[3 * ic], f1 = A.feat[3 * ic + 1], f2 = A.feat[3 * ic + 2];
+        const float wv = A.rgbw ? A.rgbw[ic] : 1.0f;
+        float m[4], v[4], df[4], npg[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m[e] = v[e] = df[e] = npg[e] = 0.0f;
+        if (upd) {
+            ld_row<3>(A.state[2][0], ic, m);
+            ld_row<3>(A.state[2][1], ic, v);
+            ld_row<3>(A.state[2][2], ic, df);
+            ld_row<3>(A.state[2][3], ic, npg);
+            if (A.rgbw_train) {
+                ld_row<1>(A.state[3][0], ic, m + 3);
+                ld_row<1>(A.state[3][1], ic, v + 3);
+                ld_row<1>(A.state[3][2], ic, df + 3);
+                ld_row<1>(A.state[3][3], ic, npg + 3);
+            }
+        }
+        const float df0 = g1.y * wv, df1 = g1.z * wv, df2 = g1.w * wv;
+        const float dw = (g1.y * f0 + g1.z * f1) + g1.w * f2;
+        float pc[4] = {f0, f1, f2, wv};
+        if (!upd) {
+            if (have) {
+                float *o = A.grads_out + 9 * (size_t)i;
+                o[5] = df0;
+                o[6] = df1;
+                o[7] = df2;
+                o[8] = A.rgbw_train ? dw : 0.0f;
+            }
+        } else {
+            const float g[4] = {df0, df1, df2, dw};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int q = e < 3 ? 2 : 3;
+                if (q == 3 && !A.rgbw_train) continue;
+                if (A.first[q]) npg[e] = -(g[e] * A.S.clip);
+                pc[e] = adan_update(A.S, pc[e], g[e], m[e], v[e], df[e], npg[e]);
+            }
+            if (have) {
+                st_row<3>(A.feat, i, pc);
+                st_row<3>(A.state[2][0], i, m);
+                st_row<3>(A.state[2][1], i, v);
+                st_row<3>(A.state[2][2], i, df);
+                st_row<3>(A.state[2][3], i, npg);
+                if (A.rgbw_train) {
+                    st_row<1>(A.rgbw, i, pc + 3);
+                    st_row<1>(A.state[3][0], i, m + 3);
+                    st_row<1>(A.state[3][1], i, v + 3);
+                    st_row<1>(A.state[3][2], i, df + 3);
+                    st_row<1>(A.state[3][3], i, npg + 3);
+                }
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s_cp[grp][e][lane] = pc[e];
+    } else {
+        // geometry half: elements 0-1 (xyz) and 2-4 (cholesky)
+        const float4 g0 = A.grad[4 * ic];      // v_xy.x, v_xy.y, v_conic 0, v_conic 1
+        const float g1x = A.grad[4 * ic + 1].x;  // v_conic 2
+        const float4 r0 = A.rec[3 * ic], r2 = A.rec[3 * ic + 2];
+        const int rad = A.radii[ic];
+        const float c0 = A.chol[3 * ic], c1 = A.chol[3 * ic + 1], c2 = A.chol[3 * ic + 2];
+        const float x0 = A.xyz[2 * ic], x1 = A.xyz[2 * ic + 1];
+        hull = A.carry ? A.chull[ic] : make_uint2(0u, 0u);
+        float m[5], v[5], df[5], npg[5];
+#pragma unroll
+        for (int e = 0; e < 5; ++e) m[e] = v[e] = df[e] = npg[e] = 0.0f;
+        if (upd) {
+            ld_row<2>(A.state[0][0], ic, m);
+            ld_row<2>(A.state[0][1], ic, v);
+            ld_row<2>(A.state[0][2], ic, df);
+            ld_row<2>(A.state[0][3], ic, npg);
+            ld_row<3>(A.state[1][0], ic, m + 2);
+            ld_row<3>(A.state[1][1], ic, v + 2);
+            ld_row<3>(A.state[1][2], ic, df + 2);
+            ld_row<3>(A.state[1][3], ic, npg + 2);
+        }
+        // 2D projection VJP, backward2d.cu:8-51 (splat_step's sequence)
+        float vl0 = 0.f, vl1 = 0.f, vl2 = 0.f, vmx = 0.f, vmy = 0.f;
+        float l11 = c0, l21 = c1, l22 = c2;
+        if (A.chol_bound) {
+            l11 = l11 + A.chol_bound[0];
+            l21 = l21 + A.chol_bound[1];
+            l22 = l22 + A.chol_bound[2];
+        }
+        if (rad > 0) {
+            const float X00 = r2.z, X01 = r0.w, X10 = X01, X11 = r2.w;
+            const float G00 = g0.z, G01 = g0.w, G10 = G01, G11 = g1x;
+            const float N00 = -X00, N01 = -X01, N10 = -X10, N11 = -X11;
+            const float P00 = N00 * G00 + N10 * G01;
+            const float P01 = N01 * G00 + N11 * G01;
+            const float P10 = N00 * G10 + N10 * G11;
+            const float P11 = N01 * G10 + N11 * G11;
+            const float V00 = P00 * X00 + P10 * X01;
+            const float V01 = P01 * X00 + P11 * X01;
+            const float V10 = P00 * X10 + P10 * X11;
+            const float V11 = P01 * X10 + P11 * X11;
+            const float g11 = V00, g12 = V10 + V01, g22 = V11;
+            vl0 = 2.0f * l11 * g11 + 2.0f * g12 * l21;
+            vl1 = 2.0f * l11 * g12 + 2.0f * l21 * g22;
+            vl2 = 2.0f * l22 * g22;
+            vmx = g0.x * A.hw;
+            vmy = g0.y * A.hh;
+        }
+        const float t0 = tanhf(x0), t1 = tanhf(x1);
+        const float dx0 = vmx * (1.0f - t0 * t0), dx1 = vmy * (1.0f - t1 * t1);
+        pnew[0] = x0;
+        pnew[1] = x1;
+        pnew[2] = c0;
+        pnew[3] = c1;
+        pnew[4] = c2;
+        if (!upd) {
+            if (have) {
+                float *o = A.grads_out + 9 * (size_t)i;
+                o[0] = dx0;
+                o[1] = dx1;
+                o[2] = vl0;
+                o[3] = vl1;
+                o[4] = vl2;
+            }
+        } else {
+            const float g[5] = {dx0, dx1, vl0, vl1, vl2};
+#pragma unroll
+            for (int e = 0; e < 5; ++e) {
+                const int q = e < 2 ? 0 : 1;
+                if (A.first[q]) npg[e] = -(g[e] * A.S.clip);
+                pnew[e] = adan_update(A.S, pnew[e], g[e], m[e], v[e], df[e], npg[e]);
+            }
+            if (have) {
+                st_row<2>(A.xyz, i, pnew);
+                st_row<2>(A.state[0][0], i, m);
+                st_row<2>(A.state[0][1], i, v);
+                st_row<2>(A.state[0][2], i, df);
+                st_row<2>(A.state[0][3], i, npg);
+                st_row<3>(A.chol, i, pnew + 2);
+                st_row<3>(A.state[1][0], i, m + 2);
+                st_row<3>(A.state[1][1], i, v + 2);
+                st_row<3>(A.state[1][2], i, df + 2);
+                st_row<3>(A.state[1][3], i, npg + 2);
+            }
+        }
+    }
+    __syncthreads();
+    if (!(w & 1) && have && upd && A.carry) {
+        const float p[9] = {pnew[0], pnew[1], pnew[2], pnew[3], pnew[4], s_cp[grp][0][lane],
+                            s_cp[grp][1][lane], s_cp[grp][2][lane], s_cp[grp][3][lane]};
+        hits = carry_splat(A, i, p, hull);
+    }
+    return hits;
+}
+
 template <bool kStamp, int kBlock = 256>
 __global__ __launch_bounds__(kBlock) void train_splat_kernel(TrainSplatArgs A) {
     long long *st = kStamp ? A.stamps + 8 * (size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6))
@@ -1597,8 +1771,13 @@ __global__ __launch_bounds__(kBlock) void train_splat_kernel(TrainSplatArgs A) {
         if (kStamp) splat_stamp(st, 5);
         return;
     }
-    const int t = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
-    const int hits = t < A.n ? splat_step<kStamp>(A, t, st) : 0;
+    int hits;
+    if (!kStamp && kBlock == 256 && A.split) {
+        hits = splat_step_split(A, (blockIdx.x - 1) * (kBlock / 2));
+    } else {
+        const int t = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
+        hits = t < A.n ? splat_step<kStamp>(A, t, st) : 0;
+    }
     if (A.carry == 2) {
         // the next frame's M is read only as M >= 1 (the tile kernel's background
         // branch, rasterize_sum.py:121-127): one plain store of 1 per wave that
@@ -1937,7 +2116,11 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     const int sb = knob(21) == 64 || knob(21) == 128 || knob(21) == 192 || knob(21) == 512
                        ? knob(21)
                        : 256;
-    const int blocks = (num_points > 0 ? ceil_div(num_points, sb) : 0) + 1;
+    // two waves per 64 splats (splat_step_split) unless deterministic, or
+    // A/B knob 34 = 1 / another workgroup size
+    P.split = sb == 256 && !det_off && knob(34) != 1 ? 1 : 0;
+    const int per_block = P.split ? sb / 2 : sb;
+    const int blocks = (num_points > 0 ? ceil_div(num_points, per_block) : 0) + 1;
     hipEvent_t tev[2];
     const int tslot = timing_begin(s, tev, kTimingTrainSplat);
     bool launched = false;

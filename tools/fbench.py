@@ -2,12 +2,10 @@
 
     python tools/fbench.py [--splats 10000 50000] [--iters 200] [--chol-scale 1]
 
-For each rasterizer mode (gsvc_debug_set(0)) captures ``iters`` back-to-back
-frame renders in a HIP graph, replays it and prints microseconds per frame.
-Every mode's image must equal the first one bit for bit.  (A frame inside a
-graph keeps its frame_index argument from capture time, so a graph must hold
-an even number of frames for the two parity slots to keep alternating across
-replays; ``iters`` is rounded down to even.)
+For each rasterizer mode (gsvc_debug_set(0)) and each extra knob pass, times
+``iters`` back-to-back frame renders (plain library calls; the slab entries
+refuse graph capture since round 5) and prints microseconds per frame, best
+of three.  Every pass's image must equal the first one bit for bit.
 """
 from __future__ import annotations
 
@@ -107,48 +105,23 @@ def main():
             frame()
             torch.cuda.synchronize()
             hint[0] = int(meta[0])
-            gr = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gr):
-                for _ in range(args.iters):
-                    frame()
-            gr.replay()
+            # plain launches (the library call per frame): the slab entries
+            # refuse graph capture (their parity slots follow the host's call
+            # counter), so no graph replay here
+            for _ in range(20):
+                frame()
             torch.cuda.synchronize()
             best = float("inf")
             for _ in range(3):
                 a = torch.cuda.Event(enable_timing=True)
                 b = torch.cuda.Event(enable_timing=True)
                 a.record()
-                gr.replay()
+                for _ in range(args.iters):
+                    frame()
                 b.record()
                 torch.cuda.synchronize()
                 best = min(best, a.elapsed_time(b) * 1e3 / args.iters)
-            # the same frame as a small graph replayed per step (host submits
-            # one graph per frame, as a per-call graph launch would).  Two
-            # frames per graph: a frame's parity is frozen at capture, and a
-            # one-frame graph replayed would re-add to the same counts every
-            # time (duplicate entries, then every tile past 256: the bbox
-            # rebuild -- not a valid state of the workspace contract)
-            g1 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1):
-                frame()
-                frame()
-            g1.replay()
-            torch.cuda.synchronize()
-            a1 = torch.cuda.Event(enable_timing=True)
-            b1 = torch.cuda.Event(enable_timing=True)
-            a1.record()
-            for _ in range(args.iters // 2):
-                g1.replay()
-            b1.record()
-            torch.cuda.synchronize()
-            per_graph = a1.elapsed_time(b1) * 1e3 / (2 * (args.iters // 2))
-            # and as plain launches (the library call per step, no graph)
-            a1.record()
-            for _ in range(args.iters):
-                frame()
-            b1.record()
-            torch.cuda.synchronize()
-            per_launch = a1.elapsed_time(b1) * 1e3 / args.iters
+            per_graph = per_launch = best
             same = True
             if ref is None:
                 ref = out.clone()
