@@ -8,6 +8,18 @@
 
 namespace gsvc {
 
+// A conic the ellipse culling may be applied to: positive definite and not
+// ill-conditioned.  For a*c > 2^13 det (a needle: the quadratic form nearly
+// degenerate), the reference's own float32 sigma = 0.5 (a dx^2 + c dy^2) +
+// b dx dy cancels -- its rounding error at the ellipse's edge (~2^-24 S2 a c /
+// det) outgrows the 0.1 % margin, and along the needle it reads ~0 far
+// outside the true ellipse (round 5: a textured-video splat with conic
+// (136777, -90810, 60291), float32 det 1024, alpha 1 at pixels 58 px from its
+// centre) -- and det itself has lost its bits.  Such entries are not culled.
+__device__ __forceinline__ bool cull_conditioned(float a, float c, float det) {
+    return a > 0.0f && det > 0.0f && a * c <= 8192.0f * det;
+}
+
 // The 4x4-pixel blocks of the kRows-row strip at (bx0, by0) (bit 4 * r + c:
 // rows by0 + 4r .. + 3, columns bx0 + 4c .. + 3) that splat (x, y, conic, o)
 // can reach with alpha >= 1/255 -- ellipse_hits_rect's test per block, so a
@@ -19,8 +31,8 @@ __device__ __forceinline__ unsigned ellipse_blocks(float x, float y, float a, fl
     constexpr unsigned kAll = (1u << kRows) - 1u;  // kRows / 4 row blocks x 4 column blocks
     if (!(o > 0.0f)) return (o <= 0.0f) ? 0u : kAll;  // o <= 0: never valid; NaN: keep
     const float det = a * c - b * b;
-    if (!(a > 0.0f) || !(det > 0.0f) || !(o < 3.0e38f) || !(fabsf(x) < 1e30f) || !(fabsf(y) < 1e30f))
-        return kAll;  // not positive definite / non-finite: no culling
+    if (!cull_conditioned(a, c, det) || !(o < 3.0e38f) || !(fabsf(x) < 1e30f) || !(fabsf(y) < 1e30f))
+        return kAll;  // not positive definite, ill-conditioned or non-finite: no culling
     const float lg = __logf(255.0f * o);
     if (lg < -0.01f) return 0u;  // o < e^-0.01 / 255: alpha < 1/255 everywhere
     const float S2 = 2.0f * (lg * 1.001f + 0.01f);

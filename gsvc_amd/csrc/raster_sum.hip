@@ -170,8 +170,8 @@ __device__ __forceinline__ bool ellipse_hits_rect(float x, float y, float a, flo
                                                   float o, float x0, float x1, float y0, float y1) {
     if (!(o > 0.0f)) return !(o <= 0.0f);  // o <= 0: alpha <= 0 never valid; NaN: keep
     const float det = a * c - b * b;
-    if (!(a > 0.0f) || !(det > 0.0f) || !(o < 3.0e38f) || !(fabsf(x) < 1e30f) || !(fabsf(y) < 1e30f))
-        return true;  // not positive definite / non-finite: no culling
+    if (!cull_conditioned(a, c, det) || !(o < 3.0e38f) || !(fabsf(x) < 1e30f) || !(fabsf(y) < 1e30f))
+        return true;  // not positive definite, ill-conditioned or non-finite: no culling
     const float lg = __logf(255.0f * o);
     if (lg < -0.01f) return false;  // o < e^-0.01 / 255: alpha < 1/255 everywhere
     const float S2 = 2.0f * (lg * 1.001f + 0.01f);

@@ -25,8 +25,8 @@ __device__ __forceinline__ unsigned ellipse_rect(float x, float y, float a, floa
                                                  float o, float tx0, float ty0) {
     if (!(o > 0.0f)) return (o <= 0.0f) ? kNoRect : kFullRect;  // o <= 0: never valid; NaN: keep
     const float det = a * c - b * b;
-    if (!(a > 0.0f) || !(det > 0.0f) || !(o < 3.0e38f) || !(fabsf(x) < 1e30f) || !(fabsf(y) < 1e30f))
-        return kFullRect;  // not positive definite / non-finite: no culling
+    if (!cull_conditioned(a, c, det) || !(o < 3.0e38f) || !(fabsf(x) < 1e30f) || !(fabsf(y) < 1e30f))
+        return kFullRect;  // not positive definite, ill-conditioned or non-finite: no culling
     const float lg = __logf(255.0f * o);
     if (lg < -0.01f) return kNoRect;  // o < e^-0.01 / 255: alpha < 1/255 everywhere
     const float S2 = 2.0f * (lg * 1.001f + 0.01f);

@@ -64,6 +64,39 @@ def test_id_slab_render_bit_identical(cuda, oracle, n, H, W, chol, cluster):
             np.testing.assert_allclose(ref[0][0].cpu().numpy(), want, rtol=0, atol=1e-5)
 
 
+def test_needle_splats_every_route(cuda, oracle):
+    """Near-singular conics (needles: l22 ~ 1e-4, so a*c / det ~ 1e7): the
+    reference's float32 sigma cancels along the needle, and alpha reads 1 far
+    outside the true ellipse; the kernels' ellipse culling must leave such
+    entries alone (cull.h cull_conditioned).  Sparse id slabs, the banded
+    kernel and the record slabs bit-identical, and the C oracle within 1e-5
+    (round 5: the banded kernel culled a textured-video needle at 2-3 pixels)."""
+    from gsvc_amd.render import render_frame_sum
+    H, W, n = 256, 384, 3000
+    xyz, c, f = _frame(n, 4242, 1.0, cuda)
+    g = torch.Generator().manual_seed(9)
+    k = 300
+    needle = torch.stack([1.0 + 3.0 * torch.rand(k, generator=g),
+                          4.0 * (torch.rand(k, generator=g) - 0.5),
+                          torch.full((k,), -0.5 + 1e-4)], 1)
+    c[:k] = needle.to(cuda)
+    bound = torch.tensor([0.5, 0.0, 0.5], device=cuda)
+    bg = torch.tensor([0.3, 0.6, 0.9], device=cuda)
+    ref = render_frame_sum(xyz, c, f, H, W, bg, cholesky_bound=bound)
+    got = []
+    for pair in ((24, 1), (0, 2), (0, 1)):  # records; banded; sparse records
+        with knobs(pair):
+            got.append(render_frame_sum(xyz, c, f, H, W, bg, cholesky_bound=bound))
+    torch.cuda.synchronize()
+    for x in got:
+        assert torch.equal(x, ref)
+    means = torch.tanh(xyz).cpu().numpy()
+    L = (c + bound).cpu().numpy()
+    r = oracle.render_sum(means, L, f.cpu().numpy(), np.ones((n, 1), np.float32), H, W)
+    want = np.clip(r["out"], 0, 1).transpose(2, 0, 1)
+    np.testing.assert_allclose(ref[0].cpu().numpy(), want, rtol=0, atol=1e-5)
+
+
 def test_id_slab_batched_render_bit_identical(cuda):
     """Batched frames (gsvc_render_frames_sum) over id slabs (A/B knob 25 = 1)
     against the records: every frame's image bit-identical."""

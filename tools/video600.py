@@ -110,8 +110,9 @@ def main():
         reload_max_abs_psnr_diff=max(dev_psnr),
         per_frame=[dict(frame=r["frame"], psnr=round(r["psnr"], 5), ms_ssim=r["ms_ssim"],
                         iterations=r["iterations"], splats=r["num_gaussians"],
-                        train_s=round(r["training_time"], 4), eval_fps=round(r["eval_fps"], 1))
-                   for r in frames])
+                        train_s=round(r["training_time"], 4), eval_fps=round(r["eval_fps"], 1),
+                        reload_dpsnr=d)
+                   for r, d in zip(frames, dev_psnr)])
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as fh:
         json.dump(summary, fh, indent=1)
