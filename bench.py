@@ -169,15 +169,18 @@ def composite_bytes(shape):
 
 
 def op_composite_bytes(shape):
-    """SURVEY §8d B_fwd of the autograd forward (op path): the render's bytes
-    plus final_idx 4 P."""
-    return composite_bytes(shape) + 4 * shape["P"]
+    """The op path's autograd forward: the render's bytes (the image in HWC,
+    12 P) plus the tiles' sorted ids and bins written back for the backward
+    (4 M_eff + 8 T).  No final_idx: the round-5 backward does not read it
+    (SURVEY §8d's B_fwd counts the reference's 4 P of it)."""
+    return composite_bytes(shape) + 4 * shape["M_eff"] + 8 * shape["T"]
 
 
 def sum_bwd_bytes(shape, n):
-    """SURVEY §8d B_bwd: v_out 12 P + final_idx 4 P + the visible splats 36 N_vis
-    + the tile id lists 4 M_eff + bins 8 T (read) + the gradients 36 N (written)."""
-    return 16 * shape["P"] + 36 * shape["N_vis"] + 4 * shape["M_eff"] + 8 * shape["T"] + 36 * n
+    """SURVEY §8d B_bwd without final_idx (the round-5 kernel does not read it):
+    v_out 12 P + the visible splats 36 N_vis + the tile id lists 4 M_eff + bins
+    8 T (read) + the gradients 36 N (written)."""
+    return 12 * shape["P"] + 36 * shape["N_vis"] + 4 * shape["M_eff"] + 8 * shape["T"] + 36 * n
 
 
 def alpha_fwd_bytes(shape):
@@ -639,7 +642,7 @@ def op_path_block(model, gt, device, steps=200, warmup=20):
             "timing": f"wall clock over {steps} calls after {warmup} warm-ups, synchronized",
             "host_us_per_call": host,
             "kernels": {
-                "raster_sum_fwd": roofline("raster_sum_fwd_kernel (op path: final_idx, id slabs)",
+                "raster_sum_fwd": roofline("raster_sum_fwd_kernel (op path: id slabs, sorted-id write-back)",
                                            op_composite_bytes(shape), kt["composite"], prof,
                                            "rasterize_sum_forward"),
                 "raster_sum_bwd": roofline("raster_sum_bwd_kernel", sum_bwd_bytes(shape, n),

@@ -17,6 +17,7 @@
 #                                      on frozen trained-density steps
 #   fbench_ab TAG [fbench args]        composite A/B by fbench + kernel trace
 #   shared_ranks TAG                   N = 1, 2, 4 bench ranks sharing one GPU (gloo)
+#   final TAG                          bench.py (full) + rocprofv3 kernel trace of the bench
 #   alpha_ab TAG [KNOB ['V1 V2']]      alpha path A/B (default knob 9: backward DPP vs shuffle sums;
 #                                      knob 18 = 100000: forward without lane-group lists),
 #                                      interleaved twice
@@ -117,6 +118,11 @@ shared_ranks)
   for n in 2 4; do
     GSVC_BENCH_SHARED_GPU=1 run n$n 400 python bench.py --gpus $n --backend gloo --no-cpu
   done ;;
+final)
+  # the round's bench line (with the CPU baselines) and the kernel trace of the
+  # same workload (the bench without its CPU legs), for profiles/rNN/final
+  run bench 900 python bench.py
+  run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o b --output-format csv -- python3 bench.py --no-cpu ;;
 alpha_ab)
   KN=${1:-9}; VALS=${2:-"0 1"}
   for rep in 1 2; do
