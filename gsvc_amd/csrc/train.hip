@@ -1347,6 +1347,10 @@ struct TrainSplatArgs {
 // parameters p = {xyz 2, cholesky 3, features 3, rgb_w} -- load_project's op
 // sequence (frame_dev.h), so the record bits equal a projection kernel's --
 // and the upkeep of its carried bins.  Returns its box area (its share of M).
+// kPart (splat_step_split, both waves project, each its share of the stores):
+// 0 all, 1 the geometry wave's (record row 0, xys, radii, gradient zeroing), 2
+// the colour wave's (record rows 1-2, the box and the bins' upkeep; its share of M).
+template <int kPart = 0>
 __device__ __forceinline__ int carry_splat(const TrainSplatArgs &A, int i, const float (&p)[9],
                                            uint2 h) {
     const float mx = tanhf(p[0]), my = tanhf(p[1]);
@@ -1363,17 +1367,20 @@ __device__ __forceinline__ int carry_splat(const TrainSplatArgs &A, int i, const
         b = b * p[8];
     }
     const SplatOut S = splat_out(i, mx, my, l11, l21, l22, r, g, b, 1.0f, A.hw, A.hh, A.tbx, A.tby);
-    A.rec[3 * i] = S.r0;
+    if (kPart != 2) {
+        A.rec[3 * i] = S.r0;
+        A.xys[i] = S.P.xy;
+        A.radii[i] = S.P.rad;
+        // the record's first 32 bytes (v_xy, v_conic, v_colors: what the tile
+        // kernel adds and this kernel reads; v_opacity and the padding stay as a
+        // projection zeroed them -- nothing in the fused step writes them)
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        A.grad[4 * i] = z;
+        A.grad[4 * i + 1] = z;
+    }
+    if (kPart == 1) return 0;
     A.rec[3 * i + 1] = S.r1;
     A.rec[3 * i + 2] = S.r2;
-    A.xys[i] = S.P.xy;
-    A.radii[i] = S.P.rad;
-    // the record's first 32 bytes (v_xy, v_conic, v_colors: what the tile
-    // kernel adds and this kernel reads; v_opacity and the padding stay as a
-    // projection zeroed them -- nothing in the fused step writes them)
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    A.grad[4 * i] = z;
-    A.grad[4 * i + 1] = z;
     unsigned x0 = 0, y0 = 0, x1 = 0, y1 = 0;
     if (S.P.rad > 0) tile_bbox(S.P.xy.x, S.P.xy.y, (float)S.P.rad, A.tbx, A.tby, x0, y0, x1, y1);
     const uint2 nb = pack_box(x0, y0, x1, y1);
@@ -1593,10 +1600,11 @@ __device__ __forceinline__ int splat_step(const TrainSplatArgs &A, int i, long l
 // barrier, the carry (it needs all nine new values).  The same op sequence
 // per element as splat_step, so the same bits; twice the waves, each with
 // about half the loads and Adan work (782 one-wave latency chains on 1024
-// SIMDs were the kernel).  Not for the deterministic mode (its
-// partial sums stay in splat_step).
+// SIMDs were the kernel).  The deterministic mode's partial sums
+// are split the same way (each half its components, in splat_step's order).
 __device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int base) {
     __shared__ float s_cp[2][4][64];  // per splat group: new feature r g b, rgb_W
+    __shared__ float s_gp[2][5][64];  // per splat group: new xyz, cholesky (A.split == 2)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, grp = w >> 1;
     const int i = base + grp * 64 + lane;
     const bool have = i < A.n;
@@ -1605,9 +1613,29 @@ __device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int bas
     int hits = 0;
     float pnew[5];
     uint2 hull = make_uint2(0u, 0u);
+    // GSVC_TRAIN_DETERMINISTIC: the splat's (splat, tile) partials in bbox
+    // order plus the record's atomics, each half summing its own components in
+    // splat_step's order (the same bits per component)
+    long long db = 0, de = 0;
+    if (A.det_off && have) {
+        db = A.det_off[i];
+        de = min((long long)A.det_off[i + 1], A.det_cap);
+    }
     if (w & 1) {
         // colour half: elements 5-7 (features) and 8 (rgb_W)
-        const float4 g1 = A.grad[4 * ic + 1];  // v_conic 2, v_colors r g b
+        float4 g1 = A.grad[4 * ic + 1];  // v_conic 2, v_colors r g b
+        if (A.det_off) {
+            float sy = 0.f, sz = 0.f, sw = 0.f;
+            for (long long k = db; k < de; ++k) {
+                const float4 p1 = A.det_part[2 * k + 1];
+                sy += p1.y;
+                sz += p1.z;
+                sw += p1.w;
+            }
+            g1.y = sy + g1.y;
+            g1.z = sz + g1.z;
+            g1.w = sw + g1.w;
+        }
         const float f0 = A.feat[3 * ic], f1 = A.feat[3 * ic + 1], f2 = A.feat[3 * ic + 2];
         const float wv = A.rgbw ? A.rgbw[ic] : 1.0f;
         float m[4], v[4], df[4], npg[4];
@@ -1664,8 +1692,19 @@ __device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int bas
         for (int e = 0; e < 4; ++e) s_cp[grp][e][lane] = pc[e];
     } else {
         // geometry half: elements 0-1 (xyz) and 2-4 (cholesky)
-        const float4 g0 = A.grad[4 * ic];      // v_xy.x, v_xy.y, v_conic 0, v_conic 1
-        const float g1x = A.grad[4 * ic + 1].x;  // v_conic 2
+        float4 g0 = A.grad[4 * ic];      // v_xy.x, v_xy.y, v_conic 0, v_conic 1
+        float g1x = A.grad[4 * ic + 1].x;  // v_conic 2
+        if (A.det_off) {
+            float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f);
+            float sx = 0.f;
+            for (long long k = db; k < de; ++k) {
+                const float4 p0 = A.det_part[2 * k];
+                s0.x += p0.x; s0.y += p0.y; s0.z += p0.z; s0.w += p0.w;
+                sx += A.det_part[2 * k + 1].x;
+            }
+            g0 = make_float4(s0.x + g0.x, s0.y + g0.y, s0.z + g0.z, s0.w + g0.w);
+            g1x = sx + g1x;
+        }
         const float4 r0 = A.rec[3 * ic], r2 = A.rec[3 * ic + 2];
         const int rad = A.radii[ic];
         const float c0 = A.chol[3 * ic], c1 = A.chol[3 * ic + 1], c2 = A.chol[3 * ic + 2];
@@ -1748,12 +1787,27 @@ __device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int bas
                 st_row<3>(A.state[1][3], i, npg + 2);
             }
         }
+        if (A.split == 2) {
+#pragma unroll
+            for (int e = 0; e < 5; ++e) s_gp[grp][e][lane] = pnew[e];
+        }
     }
+    if (A.split == 2 && (w & 1) && A.carry) hull = A.chull[ic];  // the colour wave keeps the bins
     __syncthreads();
-    if (!(w & 1) && have && upd && A.carry) {
-        const float p[9] = {pnew[0], pnew[1], pnew[2], pnew[3], pnew[4], s_cp[grp][0][lane],
-                            s_cp[grp][1][lane], s_cp[grp][2][lane], s_cp[grp][3][lane]};
-        hits = carry_splat(A, i, p, hull);
+    if (have && upd && A.carry) {
+        if (A.split == 2) {
+            // both waves project; each writes its share (A/B knob 36 = 2)
+            const bool geo = !(w & 1);
+            const float p[9] = {geo ? pnew[0] : s_gp[grp][0][lane], geo ? pnew[1] : s_gp[grp][1][lane],
+                                geo ? pnew[2] : s_gp[grp][2][lane], geo ? pnew[3] : s_gp[grp][3][lane],
+                                geo ? pnew[4] : s_gp[grp][4][lane], s_cp[grp][0][lane],
+                                s_cp[grp][1][lane], s_cp[grp][2][lane], s_cp[grp][3][lane]};
+            hits = geo ? carry_splat<1>(A, i, p, hull) : carry_splat<2>(A, i, p, hull);
+        } else if (!(w & 1)) {
+            const float p[9] = {pnew[0], pnew[1], pnew[2], pnew[3], pnew[4], s_cp[grp][0][lane],
+                                s_cp[grp][1][lane], s_cp[grp][2][lane], s_cp[grp][3][lane]};
+            hits = carry_splat(A, i, p, hull);
+        }
     }
     return hits;
 }
@@ -2116,9 +2170,11 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     const int sb = knob(21) == 64 || knob(21) == 128 || knob(21) == 192 || knob(21) == 512
                        ? knob(21)
                        : 256;
-    // two waves per 64 splats (splat_step_split) unless deterministic, or
-    // A/B knob 34 = 1 / another workgroup size
-    P.split = sb == 256 && !det_off && knob(34) != 1 ? 1 : 0;
+    // two waves per 64 splats (splat_step_split) unless A/B knob 34 = 1 or
+    // another workgroup size
+    // (1: the carry in the geometry wave; A/B knob 36 = 2: both waves project and
+    // share its stores -- measured equal, 9.92-10.0 vs 9.85-9.98 us, not kept)
+    P.split = sb == 256 && knob(34) != 1 ? (knob(36) == 2 ? 2 : 1) : 0;
     const int per_block = P.split ? sb / 2 : sb;
     const int blocks = (num_points > 0 ? ceil_div(num_points, per_block) : 0) + 1;
     hipEvent_t tev[2];

@@ -80,6 +80,20 @@ def test_carried_fast_motion_and_overflow(cuda, deterministic, every):
     _same(a, b)
 
 
+@pytest.mark.parametrize("pair", [(34, 1), (36, 2)])
+def test_splat_kernel_layouts_bitwise(cuda, deterministic, pair):
+    """The splat kernel's layouts (train.hip): one lane per splat (knob 34 = 1),
+    two waves per 64 splats sharing the carry's stores (knob 36 = 2) and the
+    product's two waves with the carry in the geometry wave -- the same op
+    sequence per element, so bitwise the same trajectory, deterministic
+    partial sums included, through a bin rebuild."""
+    from conftest import knobs
+    ref = _run(cuda, True, 256, 256, 2000, 70)
+    with knobs(pair):
+        got = _run(cuda, True, 256, 256, 2000, 70)
+    _same(ref, got)
+
+
 def test_carried_bins_trained_density(cuda, deterministic):
     """The bench's frame at 1080p / 50k from its trained state (the
     train_state fixture): 20 carried steps bitwise equal to re-projected ones."""
