@@ -709,7 +709,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         tile = xcd_remap(blockIdx.x, (total + kTPW - 1) / kTPW) * kTPW + sub;
         if (tile >= total) return;  // (one-wave modes: no workgroup barrier)
     } else {
-        tile = xcd_remap(blockIdx.x, A.ntiles * A.frames);
+        tile = (kDiag && A.xcd_off) ? (int)blockIdx.x : xcd_remap(blockIdx.x, A.ntiles * A.frames);
     }
     if (A.frames > 1) {  // batched frames: this block's frame and tile
         const int b = tile / A.ntiles;
@@ -1444,6 +1444,7 @@ void sum_fwd_args_init(SumFwdArgs &A) {
     A.cut = knob(19) != 1;
     A.norank = knob(31) == 1;
     A.ids_cap = kTilePix;
+    A.xcd_off = knob(37) == 1;
     A.layout = kLayoutHWC;
     A.frames = 1;
 }
