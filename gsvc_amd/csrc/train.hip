@@ -1341,6 +1341,7 @@ struct TrainSplatArgs {
     int *m_next;
     long long *stamps;  // diagnostic: int64[waves][8]
     int split;          // two waves per 64 splats (splat_step_split); 0: one lane per splat
+    int no_loss;        // diagnostic (knob 38 = 1, wrong losses): the loss workgroup only releases the sequence word
 };
 
 // GSVC_TRAIN_CARRY: splat i's projection for the next frame from its updated
@@ -1821,6 +1822,12 @@ __global__ __launch_bounds__(kBlock) void train_splat_kernel(TrainSplatArgs A) {
         // the first workgroup (no splats): the loss; dispatched first so it
         // runs beside the splats
         __shared__ double s_l[2][4];
+        if (kDiag && A.no_loss) {  // the sequence word alone (the host waits for it)
+            if (threadIdx.x == 0 && A.loss_seq)
+                __hip_atomic_store(reinterpret_cast<unsigned *>(A.loss) + 2, A.loss_seq,
+                                   __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
         publish_loss<kBlock>(A.err, A.ntiles, A.inv_count, A.loss, A.loss_seq, A.det_off, A.n, s_l);
         if (kStamp) splat_stamp(st, 5);
         return;
@@ -2175,6 +2182,7 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     // (1: the carry in the geometry wave; A/B knob 36 = 2: both waves project and
     // share its stores -- measured equal, 9.92-10.0 vs 9.85-9.98 us, not kept)
     P.split = sb == 256 && knob(34) != 1 ? (knob(36) == 2 ? 2 : 1) : 0;
+    P.no_loss = knob(38) == 1;
     const int per_block = P.split ? sb / 2 : sb;
     const int blocks = (num_points > 0 ? ceil_div(num_points, per_block) : 0) + 1;
     hipEvent_t tev[2];
