@@ -52,6 +52,10 @@ def main():
                          "prints the tile kernel's event average")
     ap.add_argument("--shape", action="store_true",
                     help="also report N_vis, M, M_eff of the trained frame (op-path binning)")
+    ap.add_argument("--state", default=None, metavar="NPZ:FRAME",
+                    help="start from a saved model (tools/tile_counts.py --save, or a frame "
+                         "exported from a video checkpoint: xyz, cholesky, features) against "
+                         "frame FRAME of the textured synthetic video (dense content)")
     ap.add_argument("--channels", action="store_true",
                     help="also print HIP-event kernel averages (us) over 200 extra iterations")
     a = ap.parse_args()
@@ -69,9 +73,23 @@ def main():
             raise ValueError("unknown A/B knob key (gsvc_debug_set returned -1)")
     dev = torch.device("cuda:0")
     H, W = 1080, 1920
-    model = make_frame_model(H, W, a.splats, dev, seed=7,
-                             fused_train=False if a.op_by_op else None)
-    gt = synthetic_gt(H, W, 8, dev)
+    if a.state:
+        import numpy as np
+        from gsvc_amd.video import textured_video
+        path, fr = a.state.rsplit(":", 1)
+        z = np.load(path)
+        a.splats = int(z["xyz"].shape[0])
+        model = make_frame_model(H, W, a.splats, dev, seed=7,
+                                 fused_train=False if a.op_by_op else None)
+        with torch.no_grad():
+            model._xyz.copy_(torch.from_numpy(z["xyz"]))
+            model._cholesky.copy_(torch.from_numpy(z["cholesky"]))
+            model._features_dc.copy_(torch.from_numpy(z["features"]))
+        gt = textured_video(int(fr) + 1, H, W, device=dev)(int(fr))
+    else:
+        model = make_frame_model(H, W, a.splats, dev, seed=7,
+                                 fused_train=False if a.op_by_op else None)
+        gt = synthetic_gt(H, W, 8, dev)
     for it in range(1, a.warmup + 1):
         model.train_iter(gt, it)
     torch.cuda.synchronize()
