@@ -99,6 +99,19 @@ __device__ __forceinline__ int xcd_remap(int orig, int count) {
     return base + (orig >> 3);
 }
 
+// XCD-balanced variant: runs of kRun consecutive tiles (a strip of a tile row)
+// dealt round-robin over the XCDs, so a dense region of the frame spreads over
+// all eight while each run still shares its splats in one L2.  Blocks past the
+// last whole round of 8 runs map to themselves (bijective for any count).
+template <int kRun>
+__device__ __forceinline__ int xcd_runs(int orig, int count) {
+    constexpr int kGroup = 8 * kRun;
+    const int full = (count / kGroup) * kGroup;
+    if (orig >= full) return orig;
+    const int xcd = orig & 7, s = orig >> 3;
+    return ((s / kRun) * 8 + xcd) * kRun + (s % kRun);
+}
+
 // v_cvt_i32_f32 semantics: truncate, saturate, NaN -> 0.
 // 16-byte write-through store (sc1: agent scope): the line leaves the XCD's L2
 // as it is written, so the end-of-kernel release has no dirty line of it to
