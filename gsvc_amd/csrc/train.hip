@@ -74,7 +74,7 @@ struct TrainTileArgs {
     float4 *det_part;
     long long det_cap;
     int prio;  // raise the wave priority over the order phase (s_setprio; knob 16 = 1 off)
-    int xcd_off;  // diagnostic A/B (knob 37): 1 dispatch order, 2 / 3 xcd_runs<16 / 4>
+    int xcd_off;  // diagnostic A/B (knob 37): 1 dispatch order, 3 xcd_runs<4>, 4 xcd_remap ranges
     // GSVC_TRAIN_CARRY (band kernel): the tile's candidates are the splat ids
     // cids[tile][0, counts[tile]) -- a superset of its entries carried from
     // step to step (train_splat_kernel) -- and an entry is a candidate whose
@@ -684,10 +684,15 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     // 13th-16th, profiles/r03/stamps).  Raised over the order phase, a young
     // tile gets its round trips going while its elders compute.
     if (!kDiag || A.prio) __builtin_amdgcn_s_setprio(3);
-    const int tile = !(kDiag && A.xcd_off) ? xcd_remap(blockIdx.x, A.ntiles)
-                         : A.xcd_off == 1 ? (int)blockIdx.x
-                         : A.xcd_off == 2 ? xcd_runs<16>(blockIdx.x, A.ntiles)
-                                          : xcd_runs<4>(blockIdx.x, A.ntiles);
+    // runs of 16 tiles dealt over the XCDs: dense content (a textured frame's
+    // objects) spread over all eight instead of loading the one or two whose
+    // contiguous range covers them (tile kernel 273.7 -> 238.7 us on the
+    // textured video's frame 116, unchanged on the bench's frame).
+    // A/B knob 37: 1 dispatch order, 3 runs of 4, 4 contiguous ranges
+    const int tile = !(kDiag && A.xcd_off) ? xcd_runs<16>(blockIdx.x, A.ntiles)
+                     : A.xcd_off == 1      ? (int)blockIdx.x
+                     : A.xcd_off == 3      ? xcd_runs<4>(blockIdx.x, A.ntiles)
+                                           : xcd_remap(blockIdx.x, A.ntiles);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     long long *st = kStamp ? A.stamps + 8 * (size_t)tile : nullptr;
     if (kStamp && tid == 0) st[0] = tstamp();
@@ -2073,7 +2078,7 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     T.diag = knob(13);
     T.grouped = knob(14) != 1;
     T.prio = knob(16) != 1;  // A/B knob 16 = 1: no raised priority
-    T.xcd_off = knob(37);  // 1: dispatch order; 2 / 3: runs of 16 / 4 tiles dealt over the XCDs
+    T.xcd_off = knob(37);  // A/B: 1 dispatch order, 3 runs of 4 tiles, 4 contiguous XCD ranges
     T.det_off = det_off;
     T.det_part = det_part;
     T.det_cap = det_capacity;
