@@ -19,7 +19,7 @@ struct SumFwdArgs {
     int spec_slots;    // frame path: slab records loaded with the count (<= kHeadSlots)
     int group_min;     // sparse chunks of <= this many entries skip the lane-group lists
     int cut;           // sparse render chunks may take the sigma-threshold blend (knob 19 = 1: never)
-    int xcd_off;       // diagnostic A/B (knob 37 = 1): tiles in dispatch order, no XCD ranges
+    int xcd_off;       // diagnostic A/B (knob 37): 1 tiles in dispatch order, 4 xcd_remap ranges
     int ids_cap;       // id slabs: slots per tile (kTilePix, or kCarryCap for wide slabs)
     int norank;        // diagnostic A/B (knob 31 = 1): <= 64 slab entries staged in slot order, not by id
     const int *m_dev;  // device num_intersects (NULL: > 0); 0 -> background

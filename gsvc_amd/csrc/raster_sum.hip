@@ -709,7 +709,13 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         tile = xcd_remap(blockIdx.x, (total + kTPW - 1) / kTPW) * kTPW + sub;
         if (tile >= total) return;  // (one-wave modes: no workgroup barrier)
     } else {
-        tile = (kDiag && A.xcd_off) ? (int)blockIdx.x : xcd_remap(blockIdx.x, A.ntiles * A.frames);
+        // runs of 16 tiles dealt over the XCDs, as the training tile kernel
+        // (fbench: 10k frame 17.0 vs 17.3-17.4 us, the textured video's dense
+        // frame 116 at M = 894k 251.5-252.6 vs 263.9-264.6, trained 50k equal;
+        // A/B knob 37: 1 dispatch order, 4 contiguous XCD ranges)
+        tile = !(kDiag && A.xcd_off) ? xcd_runs<16>(blockIdx.x, A.ntiles * A.frames)
+               : A.xcd_off == 1      ? (int)blockIdx.x
+                                     : xcd_remap(blockIdx.x, A.ntiles * A.frames);
     }
     if (A.frames > 1) {  // batched frames: this block's frame and tile
         const int b = tile / A.ntiles;
@@ -1444,7 +1450,7 @@ void sum_fwd_args_init(SumFwdArgs &A) {
     A.cut = knob(19) != 1;
     A.norank = knob(31) == 1;
     A.ids_cap = kTilePix;
-    A.xcd_off = knob(37) == 1;
+    A.xcd_off = knob(37);
     A.layout = kLayoutHWC;
     A.frames = 1;
 }

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--splats", type=int, nargs="+", default=[10000, 50000])
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--chol-scale", type=float, default=1.0)
+    ap.add_argument("--state", default=None,
+                    help="render a saved model (npz: xyz, cholesky, features) instead")
     ap.add_argument("--trained", type=int, default=0,
                     help="render the bench's frame model after this many training iterations "
                          "(trained density) instead of random splats")
@@ -62,6 +64,13 @@ def main():
         chol = (torch.rand(n, 3, generator=g) * args.chol_scale).to(dev)
         feat = torch.rand(n, 3, generator=g).to(dev)
         bound = torch.tensor([0.5, 0.0, 0.5], device=dev)
+        if args.state:
+            import numpy as np
+            z = np.load(args.state)
+            xyz = torch.from_numpy(z["xyz"]).to(dev)
+            chol = torch.from_numpy(z["cholesky"]).to(dev)
+            feat = torch.from_numpy(z["features"]).to(dev)
+            n = xyz.shape[0]
         if args.trained > 0:
             from gsvc_amd.frame import make_frame_model, synthetic_gt
             model = make_frame_model(H, W, n, dev, seed=1000)
