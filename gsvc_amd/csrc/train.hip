@@ -1614,7 +1614,7 @@ __device__ __forceinline__ int splat_step(const TrainSplatArgs &A, int i, long l
 // are split the same way (each half its components, in splat_step's order).
 __device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int base) {
     __shared__ float s_cp[2][4][64];  // per splat group: new feature r g b, rgb_W
-    __shared__ float s_gp[2][5][64];  // per splat group: new xyz, cholesky (A.split == 2)
+    __shared__ float s_gp[2][5][64];  // per splat group: new xyz, cholesky (A.split == 2; xyz: 3)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, grp = w >> 1;
     const int i = base + grp * 64 + lane;
     const bool have = i < A.n;
@@ -1631,7 +1631,68 @@ __device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int bas
         db = A.det_off[i];
         de = min((long long)A.det_off[i + 1], A.det_cap);
     }
+    // A.split == 3: the xyz elements (0-1) on the colour wave as well -- their
+    // gradient needs only v_xy, not the projection VJP -- so the geometry wave
+    // is left the VJP, the three cholesky elements and the carry
+    // (diagnostic library only: measured equal, 10.49 / 10.74 vs 10.59 / 10.52 us,
+    // profiles/r05/splat_split/xy_*.log)
+    const bool xy_col = kDiag && A.split == 3;
     if (w & 1) {
+        if (xy_col) {
+            float4 g0 = A.grad[4 * ic];  // v_xy.x, v_xy.y
+            if (A.det_off) {
+                float sx = 0.f, sy = 0.f;
+                for (long long k = db; k < de; ++k) {
+                    const float4 p0 = A.det_part[2 * k];
+                    sx += p0.x;
+                    sy += p0.y;
+                }
+                g0.x = sx + g0.x;
+                g0.y = sy + g0.y;
+            }
+            const int rad = A.radii[ic];
+            const float x0 = A.xyz[2 * ic], x1 = A.xyz[2 * ic + 1];
+            float m[2], v[2], df[2], npg[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) m[e] = v[e] = df[e] = npg[e] = 0.0f;
+            if (upd) {
+                ld_row<2>(A.state[0][0], ic, m);
+                ld_row<2>(A.state[0][1], ic, v);
+                ld_row<2>(A.state[0][2], ic, df);
+                ld_row<2>(A.state[0][3], ic, npg);
+            }
+            float vmx = 0.f, vmy = 0.f;
+            if (rad > 0) {
+                vmx = g0.x * A.hw;
+                vmy = g0.y * A.hh;
+            }
+            const float t0 = tanhf(x0), t1 = tanhf(x1);
+            const float dx0 = vmx * (1.0f - t0 * t0), dx1 = vmy * (1.0f - t1 * t1);
+            float px[2] = {x0, x1};
+            if (!upd) {
+                if (have) {
+                    float *o = A.grads_out + 9 * (size_t)i;
+                    o[0] = dx0;
+                    o[1] = dx1;
+                }
+            } else {
+                const float g[2] = {dx0, dx1};
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    if (A.first[0]) npg[e] = -(g[e] * A.S.clip);
+                    px[e] = adan_update(A.S, px[e], g[e], m[e], v[e], df[e], npg[e]);
+                }
+                if (have) {
+                    st_row<2>(A.xyz, i, px);
+                    st_row<2>(A.state[0][0], i, m);
+                    st_row<2>(A.state[0][1], i, v);
+                    st_row<2>(A.state[0][2], i, df);
+                    st_row<2>(A.state[0][3], i, npg);
+                }
+            }
+            s_gp[grp][0][lane] = px[0];
+            s_gp[grp][1][lane] = px[1];
+        }
         // colour half: elements 5-7 (features) and 8 (rgb_W)
         float4 g1 = A.grad[4 * ic + 1];  // v_conic 2, v_colors r g b
         if (A.det_off) {
@@ -1718,16 +1779,18 @@ __device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int bas
         const float4 r0 = A.rec[3 * ic], r2 = A.rec[3 * ic + 2];
         const int rad = A.radii[ic];
         const float c0 = A.chol[3 * ic], c1 = A.chol[3 * ic + 1], c2 = A.chol[3 * ic + 2];
-        const float x0 = A.xyz[2 * ic], x1 = A.xyz[2 * ic + 1];
+        const float x0 = xy_col ? 0.f : A.xyz[2 * ic], x1 = xy_col ? 0.f : A.xyz[2 * ic + 1];
         hull = A.carry ? A.chull[ic] : make_uint2(0u, 0u);
         float m[5], v[5], df[5], npg[5];
 #pragma unroll
         for (int e = 0; e < 5; ++e) m[e] = v[e] = df[e] = npg[e] = 0.0f;
         if (upd) {
-            ld_row<2>(A.state[0][0], ic, m);
-            ld_row<2>(A.state[0][1], ic, v);
-            ld_row<2>(A.state[0][2], ic, df);
-            ld_row<2>(A.state[0][3], ic, npg);
+            if (!xy_col) {
+                ld_row<2>(A.state[0][0], ic, m);
+                ld_row<2>(A.state[0][1], ic, v);
+                ld_row<2>(A.state[0][2], ic, df);
+                ld_row<2>(A.state[0][3], ic, npg);
+            }
             ld_row<3>(A.state[1][0], ic, m + 2);
             ld_row<3>(A.state[1][1], ic, v + 2);
             ld_row<3>(A.state[1][2], ic, df + 2);
@@ -1770,8 +1833,10 @@ __device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int bas
         if (!upd) {
             if (have) {
                 float *o = A.grads_out + 9 * (size_t)i;
-                o[0] = dx0;
-                o[1] = dx1;
+                if (!xy_col) {
+                    o[0] = dx0;
+                    o[1] = dx1;
+                }
                 o[2] = vl0;
                 o[3] = vl1;
                 o[4] = vl2;
@@ -1781,15 +1846,18 @@ __device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int bas
 #pragma unroll
             for (int e = 0; e < 5; ++e) {
                 const int q = e < 2 ? 0 : 1;
+                if (q == 0 && xy_col) continue;
                 if (A.first[q]) npg[e] = -(g[e] * A.S.clip);
                 pnew[e] = adan_update(A.S, pnew[e], g[e], m[e], v[e], df[e], npg[e]);
             }
             if (have) {
-                st_row<2>(A.xyz, i, pnew);
-                st_row<2>(A.state[0][0], i, m);
-                st_row<2>(A.state[0][1], i, v);
-                st_row<2>(A.state[0][2], i, df);
-                st_row<2>(A.state[0][3], i, npg);
+                if (!xy_col) {
+                    st_row<2>(A.xyz, i, pnew);
+                    st_row<2>(A.state[0][0], i, m);
+                    st_row<2>(A.state[0][1], i, v);
+                    st_row<2>(A.state[0][2], i, df);
+                    st_row<2>(A.state[0][3], i, npg);
+                }
                 st_row<3>(A.chol, i, pnew + 2);
                 st_row<3>(A.state[1][0], i, m + 2);
                 st_row<3>(A.state[1][1], i, v + 2);
@@ -1814,6 +1882,10 @@ __device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int bas
                                 s_cp[grp][1][lane], s_cp[grp][2][lane], s_cp[grp][3][lane]};
             hits = geo ? carry_splat<1>(A, i, p, hull) : carry_splat<2>(A, i, p, hull);
         } else if (!(w & 1)) {
+            if (xy_col) {
+                pnew[0] = s_gp[grp][0][lane];
+                pnew[1] = s_gp[grp][1][lane];
+            }
             const float p[9] = {pnew[0], pnew[1], pnew[2], pnew[3], pnew[4], s_cp[grp][0][lane],
                                 s_cp[grp][1][lane], s_cp[grp][2][lane], s_cp[grp][3][lane]};
             hits = carry_splat(A, i, p, hull);
@@ -2190,8 +2262,9 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     // two waves per 64 splats (splat_step_split) unless A/B knob 34 = 1 or
     // another workgroup size
     // (1: the carry in the geometry wave; A/B knob 36 = 2: both waves project and
-    // share its stores -- measured equal, 9.92-10.0 vs 9.85-9.98 us, not kept)
-    P.split = sb == 256 && knob(34) != 1 ? (knob(36) == 2 ? 2 : 1) : 0;
+    // share its stores -- measured equal, 9.92-10.0 vs 9.85-9.98 us, not kept;
+    // 3: the xyz elements on the colour wave)
+    P.split = sb == 256 && knob(34) != 1 ? (knob(36) == 2 || knob(36) == 3 ? knob(36) : 1) : 0;
     P.no_loss = knob(38) == 1;
     const int per_block = P.split ? sb / 2 : sb;
     const int blocks = (num_points > 0 ? ceil_div(num_points, per_block) : 0) + 1;
