@@ -688,10 +688,12 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     // objects) spread over all eight instead of loading the one or two whose
     // contiguous range covers them (tile kernel 273.7 -> 238.7 us on the
     // textured video's frame 116, unchanged on the bench's frame).
-    // A/B knob 37: 1 dispatch order, 3 runs of 4, 4 contiguous ranges
+    // A/B knob 37: 1 dispatch order, 3 runs of 4, 5 of 8, 6 of 32, 4 contiguous ranges
     const int tile = !(kDiag && A.xcd_off) ? xcd_runs<16>(blockIdx.x, A.ntiles)
                      : A.xcd_off == 1      ? (int)blockIdx.x
                      : A.xcd_off == 3      ? xcd_runs<4>(blockIdx.x, A.ntiles)
+                     : A.xcd_off == 5      ? xcd_runs<8>(blockIdx.x, A.ntiles)
+                     : A.xcd_off == 6      ? xcd_runs<32>(blockIdx.x, A.ntiles)
                                            : xcd_remap(blockIdx.x, A.ntiles);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     long long *st = kStamp ? A.stamps + 8 * (size_t)tile : nullptr;
