@@ -120,7 +120,8 @@ __device__ __forceinline__ int xcd_runs(int orig, int count) {
 __device__ __forceinline__ void store_wt(float4 *p, float4 v) {
     typedef float f4 __attribute__((ext_vector_type(4)));
     const f4 x = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+    // s_nop 1: the gfx940+ store-data hazard (raster_sum.hip st_f4)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
 }
 
 __device__ __forceinline__ int cvt_i32(float f) {

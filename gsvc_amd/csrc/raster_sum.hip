@@ -186,6 +186,16 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 // (nt sc1, production: the lines leave L2 as they are written, so the
 // end-of-kernel release has ~25 MB less to write back -- composite 10.6 ->
 // 9.5 us at 1080p), plain (write-back L2), sc1, sc0 sc1, or nt alone.
+//
+// Every inline-asm store of more than 64 bits ends with ``s_nop 1``: the store
+// reads its data VGPRs after it issues, and on gfx940+ a VALU write to one of
+// them needs two wait states (LLVM GCNHazardRecognizer, VALU-after-VMEM-store
+// data hazard).  The compiler pads its own stores, and inline-asm ones inside a
+// basic block, but round 5's HWC write-through store ended an exec-masked block
+// and the next block's first VALU overwrote data VGPR 0 one wait state later --
+// one 16-lane pass of the wave stored the new value now and then (DESIGN.md
+// §12, tools/store_hazard_scan.py, tests/test_store_hazard.py).  The trailing
+// nop makes the asm safe wherever the compiler places it.
 enum { kStoreNtSc1 = 0, kStorePlain = 1, kStoreSc1 = 2, kStoreSc01 = 3, kStoreNt = 4 };
 
 __device__ __forceinline__ void st_f4(float *p, float a, float b, float c, float d, int policy) {
@@ -193,12 +203,12 @@ __device__ __forceinline__ void st_f4(float *p, float a, float b, float c, float
     if (!kDiag) policy = kStoreNtSc1;  // the product's one policy
     switch (policy) {
     case kStoreNt: __builtin_nontemporal_store(v, reinterpret_cast<v4f *>(p)); break;
-    case kStoreSc1: asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory"); break;
+    case kStoreSc1: asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory"); break;
     case kStoreSc01:
-        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
         break;
     case kStoreNtSc1:
-        asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+        asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
         break;
     default: *reinterpret_cast<v4f *>(p) = v; break;
     }
@@ -475,12 +485,13 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         for (int j = 0; j < 3; ++j) {
             const int c = j * 64 + lane;
             const int row = c / 12, cc = c - row * 12;
-            // plain stores: written through (sc1 nt, as the planes are) this
-            // layout lost whole 192-byte tile rows now and then (round 5,
-            // tools/op_mismatch.py: 70-100 random tiles per 1080p frame)
-            if (ty * kTile + row < A.img_h)
-                *reinterpret_cast<float4 *>(A.out + tile_base + (size_t)row * A.img_w * 3 + cc * 4) =
-                    s_slice[c];
+            // (round 5 wrote these rows as unpadded asm write-through stores and
+            // lost 16 floats in 1-4 % of the tiles: the store-data hazard above,
+            // tests/analysis/store_hazard_repro.py)
+            if (ty * kTile + row < A.img_h) {
+                float *o = A.out + tile_base + (size_t)row * A.img_w * 3 + cc * 4;
+                *reinterpret_cast<float4 *>(o) = s_slice[c];
+            }
         }
         if (pi < A.img_h && A.final_idx) {
             const size_t p0 = (size_t)pi * (size_t)A.img_w + (size_t)pj;
