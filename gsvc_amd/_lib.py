@@ -65,6 +65,8 @@ _SIGS = {
     "gsvc_rasterize_sum_backward_zeroed": [_U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "gsvc_rasterize_sum_backward_zeroed_strided": [_U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P, _LL,
                                                    _LL, _LL, _P, _P],
+    "gsvc_rasterize_sum_backward_zeroed_strided_ex": [_U, _U, _I, _P, _P, _P, _P, _P, _P, _P, _P,
+                                                      _LL, _LL, _LL, _P, _P, _I],
     "gsvc_compute_cov2d_bounds": [_I, _P, _P, _P, _P],
     "gsvc_cumsum_workspace_bytes": [_I],
     "gsvc_compute_cumulative_intersects": [_I, _P, _P, _P, _P, _P, _SZ, _P],

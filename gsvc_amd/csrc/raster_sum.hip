@@ -485,12 +485,14 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         for (int j = 0; j < 3; ++j) {
             const int c = j * 64 + lane;
             const int row = c / 12, cc = c - row * 12;
-            // (round 5 wrote these rows as unpadded asm write-through stores and
-            // lost 16 floats in 1-4 % of the tiles: the store-data hazard above,
-            // tests/analysis/store_hazard_repro.py)
+            // written through like the planes (the op composite 20.0 -> 18.6 us
+            // over 10k + 50k frames, tools/hwc_store_ab.py, profiles/r06/hwc_store/);
+            // round 5's unpadded asm form lost 16 floats in 1-4 % of the tiles
+            // (the store-data hazard above, tests/analysis/store_hazard_repro.py)
             if (ty * kTile + row < A.img_h) {
                 float *o = A.out + tile_base + (size_t)row * A.img_w * 3 + cc * 4;
-                *reinterpret_cast<float4 *>(o) = s_slice[c];
+                const float4 q = s_slice[c];
+                st_f4(o, q.x, q.y, q.z, q.w, A.store_policy);
             }
         }
         if (pi < A.img_h && A.final_idx) {
@@ -658,9 +660,11 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
             const int c = jj * 64 + lane;
             if (c < 96) {
                 const int row = c / 12, cc = c - row * 12;
-                if (row0 + row < A.img_h)
-                    *reinterpret_cast<float4 *>(A.out + base_off + (size_t)row * A.img_w * 3 + cc * 4) =
-                        s_slice[c];
+                if (row0 + row < A.img_h) {
+                    const float4 q = s_slice[c];
+                    st_f4(A.out + base_off + (size_t)row * A.img_w * 3 + cc * 4, q.x, q.y, q.z, q.w,
+                          A.store_policy);
+                }
             }
         }
         if (pi < A.img_h && A.final_idx) {
@@ -903,10 +907,13 @@ __host__ __device__ inline VStrides hwc_strides(unsigned img_w) {
 // adds an entry's items in a fixed tree order and the run's last lane adds the
 // run into the entry's LDS sums (fixed order, no LDS atomics); the two bands'
 // sums go to the splat's record with one 9-lane atomic request per (splat,
-// tile).  final_idx bounds no sum: an entry past a pixel's final_idx fails the
-// alpha test there in the forward's own op sequence (that is what final_idx
-// records), so the reference's k > final_idx skip is implied; entries past the
-// tile's 256th are skipped as there (final_idx < range.x + 256).
+// tile).  final_idx (kFinal, when the caller passes one): the reference's
+// per-pixel skip of entries k > final_idx[p] (backward.cu:783-786), the pixel's
+// bound staged in LDS beside its v_out; without one (the op path's C++ Function,
+// whose forward writes none) the bound is the one this library's own forward
+// implies -- an entry past a pixel's last contributor fails the alpha test
+// there in the same op sequence -- so nothing is read.  Entries past the tile's
+// 256th are skipped as there (final_idx < range.x + 256).
 // Round 4's entry-per-thread kernel (each thread looping over E pixels with
 // the skip, 9 block reductions per entry) is raster_sum_bwd_kernel_r4 below,
 // in the diagnostic library only (A/B knob 29 = 1).
@@ -923,7 +930,14 @@ struct SumBwdLds {
     signed char own[kSBThreads];        // per wave: the entry of the round's first items
     signed char perm[kSBThreads];       // per wave: the chunk's entries by item length
 };
+struct SumBwdLdsFinal : SumBwdLds {
+    int fi[kTile * kVRow];              // final_idx (kFinal), rows as v's
+};
 
+// kOpac false (GSVC_BWD_NO_OPACITY: the caller's opacity takes no gradient, as
+// GSVC's constant ones): the v_opacity sum is neither formed nor stored, so a
+// (splat, tile) request covers the record's first 32 bytes only.
+template <bool kFinal, bool kOpac>
 __global__ __launch_bounds__(kSBThreads, 8) void raster_sum_bwd_kernel(
     int tbx, int img_w, int img_h, int ntiles, const int *__restrict__ ids,
     const int2 *__restrict__ bins, const float2 *__restrict__ xys, const float *__restrict__ conics,
@@ -931,8 +945,7 @@ __global__ __launch_bounds__(kSBThreads, 8) void raster_sum_bwd_kernel(
     const int *__restrict__ final_idx, const float *__restrict__ v_out, VStrides vs,
     float *__restrict__ grad, const int *__restrict__ det_off, const int *__restrict__ det_radii,
     float *__restrict__ det_part, long long det_cap) {
-    (void)final_idx;
-    __shared__ SumBwdLds S;
+    __shared__ std::conditional_t<kFinal, SumBwdLdsFinal, SumBwdLds> S;
     const int tile = xcd_remap(blockIdx.x, ntiles);
     const int ty = tile / tbx, tx = tile - ty * tbx;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -956,6 +969,9 @@ __global__ __launch_bounds__(kSBThreads, 8) void raster_sum_bwd_kernel(
             S.v[0][prow * kVRow + pcol + q] = a;
             S.v[1][prow * kVRow + pcol + q] = b;
             S.v[2][prow * kVRow + pcol + q] = c;
+            if constexpr (kFinal)
+                S.fi[prow * kVRow + pcol + q] =
+                    n > 0 && pi < img_h && pj + q < img_w ? final_idx[(size_t)pi * img_w + pj + q] : 0;
         }
     }
     if (n == 0) return;  // (block-uniform)
@@ -1058,8 +1074,15 @@ __global__ __launch_bounds__(kSBThreads, 8) void raster_sum_bwd_kernel(
                     const float *vp = &S.v[0][0] + row * kVRow + cs;
                     const float *const ve = &S.v[0][0] + row * kVRow + ce;
                     float px = tx0 + (float)cs;
+                    // kFinal: the entry's sorted index against each pixel's bound
+                    const int kk = range.x + c0 + own;
+                    const int *fp = nullptr;
+                    if constexpr (kFinal) fp = &S.fi[0] + row * kVRow + cs;
                     auto walk = [&](auto kcut) {
                         for (; vp <= ve; ++vp, px += 1.0f) {
+                            if constexpr (kFinal) {
+                                if (kk > *fp++) continue;
+                            }
                             const float Px = vp[0], Py = vp[kTile * kVRow], Pz = vp[2 * kTile * kVRow];
                             const float dx = G.x - px;  // the forward's own dx
                             const float sgm = fmaf(fmaf(G.z, dx, bdy), dx, cq);
@@ -1077,7 +1100,7 @@ __global__ __launch_bounds__(kSBThreads, 8) void raster_sum_bwd_kernel(
                             g[5] = fmaf(al, Px, g[5]);
                             g[6] = fmaf(al, Py, g[6]);
                             g[7] = fmaf(al, Pz, g[7]);
-                            g[8] = fmaf(vis, v_alpha, g[8]);
+                            if constexpr (kOpac) g[8] = fmaf(vis, v_alpha, g[8]);
                             s0 += v_sigma;
                             const float vdx = v_sigma * dx;
                             s1 += vdx;
@@ -1097,11 +1120,14 @@ __global__ __launch_bounds__(kSBThreads, 8) void raster_sum_bwd_kernel(
                 }
             }
             // an entry has at most 8 rows in a band: runs of <= 8 lanes
-            wave_seg_sums<9, false>(g, own);
+            if constexpr (kOpac)
+                wave_seg_sums<9, false>(g, own);
+            else
+                wave_seg_sums<8, false>(*reinterpret_cast<float(*)[8]>(&g[0]), own);
             const int own_next = __shfl_down(own, 1, 64);
             if (item < total && (lane == 63 || item + 1 == total || own_next != own)) {
 #pragma unroll
-                for (int c = 0; c < 9; ++c) eacc[c * kSBChunk + own] += g[c];
+                for (int c = 0; c < (kOpac ? 9 : 8); ++c) eacc[c * kSBChunk + own] += g[c];
             }
             __builtin_amdgcn_wave_barrier();
         }
@@ -1110,7 +1136,7 @@ __global__ __launch_bounds__(kSBThreads, 8) void raster_sum_bwd_kernel(
         // splat's 64-byte record: one memory request per (splat, tile)
         for (int q = tid; q < gn * 16; q += kSBThreads) {
             const int e = q >> 4, c = q & 15;
-            if (c >= 9) continue;
+            if (c >= (kOpac ? 9 : 8)) continue;
             const float v = S.part[0][c][e] + S.part[1][c][e];
             if (det_off) {
                 const long long slot = det_slot(det_off, xys, det_radii, S.gid[e], tx, ty, tbx, tby);
@@ -1746,7 +1772,7 @@ static void sum_bwd_launch(hipStream_t s, int tbx, int img_w, int img_h, int nti
                            const int *ids, const int2 *bins, const float2 *xys, const float *conics,
                            const float *colors, const float *opac, const int *final_idx,
                            const float *v_out, VStrides vs, float *grad, const int *det_off,
-                           const int *det_radii, float *det_part, long long det_cap) {
+                           const int *det_radii, float *det_part, long long det_cap, int flags = 0) {
     hipEvent_t tev[2];
     const int tslot = timing_begin(s, tev, kTimingSumBwd);
 #ifdef GSVC_DIAG
@@ -1758,17 +1784,20 @@ static void sum_bwd_launch(hipStream_t s, int tbx, int img_w, int img_h, int nti
         return;
     }
 #endif
-    launch_timed(raster_sum_bwd_kernel, dim3(ntiles), dim3(kSBThreads), 0, s, tev, tbx, img_w, img_h,
-                 ntiles, ids, bins, xys, conics, colors, opac, final_idx, v_out, vs, grad, det_off,
-                 det_radii, det_part, det_cap);
+    // the deterministic slots always carry all 9 sums (det_gather reads them)
+    const bool opac_grad = !(flags & GSVC_BWD_NO_OPACITY) || det_off;
+    auto k = final_idx ? (opac_grad ? raster_sum_bwd_kernel<true, true> : raster_sum_bwd_kernel<true, false>)
+                       : (opac_grad ? raster_sum_bwd_kernel<false, true> : raster_sum_bwd_kernel<false, false>);
+    launch_timed(k, dim3(ntiles), dim3(kSBThreads), 0, s, tev, tbx, img_w, img_h, ntiles, ids, bins, xys,
+                 conics, colors, opac, final_idx, v_out, vs, grad, det_off, det_radii, det_part, det_cap);
     timing_end(s, tslot, kTimingSumBwd);
 }
 
-extern "C" int gsvc_rasterize_sum_backward_zeroed_strided(
+extern "C" int gsvc_rasterize_sum_backward_zeroed_strided_ex(
     unsigned img_height, unsigned img_width, int num_points, const int *gaussian_ids_sorted,
     const int *tile_bins, const float *xys, const float *conics, const float *colors,
     const float *opacities, const int *final_idx, const float *v_output, long long v_stride_h,
-    long long v_stride_w, long long v_stride_c, float *grad_records, void *stream) {
+    long long v_stride_w, long long v_stride_c, float *grad_records, void *stream, int flags) {
     const VStrides vs{v_stride_h, v_stride_w, v_stride_c};
     const int tbx = ceil_div((int)img_width, kTile), tby = ceil_div((int)img_height, kTile);
     if (num_points < 0)
@@ -1777,8 +1806,18 @@ extern "C" int gsvc_rasterize_sum_backward_zeroed_strided(
     if (ntiles == 0 || num_points == 0) return GSVC_OK;
     sum_bwd_launch((hipStream_t)stream, tbx, (int)img_width, (int)img_height, ntiles,
                    gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys, conics, colors,
-                   opacities, final_idx, v_output, vs, grad_records, nullptr, nullptr, nullptr, 0ll);
+                   opacities, final_idx, v_output, vs, grad_records, nullptr, nullptr, nullptr, 0ll, flags);
     return check_launch("rasterize_sum_backward_zeroed_strided");
+}
+
+extern "C" int gsvc_rasterize_sum_backward_zeroed_strided(
+    unsigned img_height, unsigned img_width, int num_points, const int *gaussian_ids_sorted,
+    const int *tile_bins, const float *xys, const float *conics, const float *colors,
+    const float *opacities, const int *final_idx, const float *v_output, long long v_stride_h,
+    long long v_stride_w, long long v_stride_c, float *grad_records, void *stream) {
+    return gsvc_rasterize_sum_backward_zeroed_strided_ex(
+        img_height, img_width, num_points, gaussian_ids_sorted, tile_bins, xys, conics, colors,
+        opacities, final_idx, v_output, v_stride_h, v_stride_w, v_stride_c, grad_records, stream, 0);
 }
 
 extern "C" int gsvc_rasterize_sum_backward_zeroed(

@@ -362,13 +362,20 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
         } else {
             rec = at::zeros({n, 16}, xys.options());
         }
-        check(gsvc_rasterize_sum_backward_zeroed_strided(
+        // GSVC's opacity is a constant (GaussianSplats_Represent.py:84): no
+        // v_opacity sum, 32-byte gradient requests instead of 64
+        const bool opac_grad = ctx->needs_input_grad(4);
+        check(gsvc_rasterize_sum_backward_zeroed_strided_ex(
                   (unsigned)H, (unsigned)W, (int)n, ip(gids), ip(bins), fp(xys), fp(conics),
                   fp(colors), fp(opacity), nullptr, v_out.data_ptr<float>(), v_out.stride(0),
-                  v_out.stride(1), v_out.stride(2), fp(rec), stream_of(xys)),
-              "gsvc_rasterize_sum_backward_zeroed_strided");
-        Tensor v_opac = rec.narrow(1, 8, 1);
-        if (opacity.dim() != 2) v_opac = v_opac.reshape(opacity.sizes());
+                  v_out.stride(1), v_out.stride(2), fp(rec), stream_of(xys),
+                  opac_grad ? 0 : GSVC_BWD_NO_OPACITY),
+              "gsvc_rasterize_sum_backward_zeroed_strided_ex");
+        Tensor v_opac;
+        if (opac_grad) {
+            v_opac = rec.narrow(1, 8, 1);
+            if (opacity.dim() != 2) v_opac = v_opac.reshape(opacity.sizes());
+        }
         return {rec.narrow(1, 0, 2), Tensor(), rec.narrow(1, 2, 3), rec.narrow(1, 5, 3), v_opac,
                 Tensor(), Tensor(), Tensor(), Tensor()};
     }

@@ -296,7 +296,7 @@ int gsvc_rasterize_sum_forward_ex(
  * and writes them back sorted: gaussian_ids [T * 256] (tile t's at t * 256)
  * and tile_bins [T, 2] = [t * 256, t * 256 + n) are then the inputs of the
  * backward.  final_idx (optional; NULL: not written -- the backward below
- * does not read it) indexes gaussian_ids.  meta[0] <- M (device), meta[1] <-
+ * needs none when the forward was this one) indexes gaussian_ids.  meta[0] <- M (device), meta[1] <-
  * 0; M < 1 renders the background (rasterize_sum.py:121-127).
  * grad_records_zero (optional, [N, 16]) is zeroed for
  * gsvc_rasterize_sum_backward_zeroed.  workspace: the first
@@ -335,10 +335,13 @@ int gsvc_rasterize_sum_forward_slabs_ordered(
     void *order_workspace, size_t order_workspace_bytes, int order_flags);
 /* gsvc_rasterize_sum_backward (backward.cu:696-862) into grad_records that
  * the caller has zeroed (gsvc_rasterize_sum_forward_slabs did): no memset.
- * final_idx is accepted and not read (may be NULL): an entry past a pixel's
- * final index fails the alpha test there in the forward's own op sequence,
- * which is what final_idx records, so the reference's k > final_idx skip is
- * implied by the test itself. */
+ * final_idx [H, W] (indices into gaussian_ids_sorted): when given, pixel p
+ * skips every entry k > final_idx[p], as the reference does
+ * (backward.cu:783-786), whatever forward produced it.  NULL: no per-pixel
+ * bound is read -- valid ONLY for the final_idx that this library's own sum
+ * forward kernels imply (an entry past a pixel's last contributor fails the
+ * alpha test there in the same op sequence); a forward with another alpha
+ * test (e.g. a fast-math build) must pass its final_idx. */
 int gsvc_rasterize_sum_backward_zeroed(
     unsigned img_height, unsigned img_width, int num_points,
     const int *gaussian_ids_sorted, const int *tile_bins, const float *xys,
@@ -355,6 +358,17 @@ int gsvc_rasterize_sum_backward_zeroed_strided(
     const float *conics, const float *colors, const float *opacities,
     const int *final_idx, const float *v_output, long long v_stride_h,
     long long v_stride_w, long long v_stride_c, float *grad_records, void *stream);
+/* The same with flags: GSVC_BWD_NO_OPACITY -- the caller's opacities take no
+ * gradient (GSVC's constant ones, GaussianSplats_Represent.py:84): v_opacity
+ * (record word 8) is neither computed nor written, and each (splat, tile)
+ * request covers the record's first 32 bytes.  Not part of the reference. */
+#define GSVC_BWD_NO_OPACITY 0x1
+int gsvc_rasterize_sum_backward_zeroed_strided_ex(
+    unsigned img_height, unsigned img_width, int num_points,
+    const int *gaussian_ids_sorted, const int *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacities,
+    const int *final_idx, const float *v_output, long long v_stride_h,
+    long long v_stride_w, long long v_stride_c, float *grad_records, void *stream, int flags);
 
 /* ---------------------------------------------------------------------------
  * Whole-frame render of GSVC's per-frame model (GaussianSplats_Represent.py:

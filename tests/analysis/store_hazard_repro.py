@@ -50,7 +50,7 @@ LIBDIR = os.path.join(REPO, "gsvc_amd", "lib")
 OUT = os.path.join(LIBDIR, "repro")
 VARIANTS = {"r5hwc": "bare", "r5hwc_nop": "padded"}
 
-_HWC_NOW = re.compile(r"                \*reinterpret_cast<float4 \*>\(o\) = s_slice\[c\];\n")
+_HWC_NOW = re.compile(r"                const float4 q = s_slice\[c\];\n                st_f4\(o, q\.x, q\.y, q\.z, q\.w, A\.store_policy\);\n")
 
 
 def _variant_source(form: str) -> str:
@@ -58,12 +58,10 @@ def _variant_source(form: str) -> str:
     m = _HWC_NOW.search(src)
     assert m, "HWC store block not found in raster_sum.hip"
     nop = "\\n\\ts_nop 1" if form == "padded" else ""
-    body = ("                {\n"
-            "                    const float4 q = s_slice[c];\n"
-            "                    const v4f v = {q.x, q.y, q.z, q.w};\n"
-            f"                    asm volatile(\"global_store_dwordx4 %0, %1, off sc1 nt{nop}\" "
-            "::\"v\"(o), \"v\"(v) : \"memory\");\n"
-            "                }\n")
+    body = ("                const float4 q = s_slice[c];\n"
+            "                const v4f v = {q.x, q.y, q.z, q.w};\n"
+            f"                asm volatile(\"global_store_dwordx4 %0, %1, off sc1 nt{nop}\" "
+            "::\"v\"(o), \"v\"(v) : \"memory\");\n")
     return src[:m.start()] + body + src[m.end():]
 
 

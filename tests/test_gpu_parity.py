@@ -223,6 +223,104 @@ def test_raster_sum_backward_vs_oracle(cuda, oracle, name):
         np.testing.assert_allclose(N(a), b, rtol=1e-4, atol=1e-4, err_msg=nm)
 
 
+def _lowered_final_idx(fi, bins, tbx, W, rng, share):
+    """final_idx with a random ``share`` of the pixels lowered to a random
+    index in [tile start - 1, final_idx] (share None: every pixel 0)."""
+    fi = np.array(fi, np.int32)
+    if share is None:
+        return np.zeros_like(fi)
+    H = fi.shape[0]
+    ys, xs = np.nonzero(rng.random(fi.shape) < share)
+    t = (ys // 16) * tbx + xs // 16
+    lo = np.asarray(bins)[t, 0] - 1
+    hi = fi[ys, xs]
+    fi[ys, xs] = np.where(hi > lo, lo + (rng.random(ys.size) * (hi - lo + 1)).astype(np.int32), hi)
+    return fi
+
+
+@pytest.mark.parametrize("share", [0.1, None])
+@pytest.mark.parametrize("name", [c for c in SUM_CASES if "empty" not in c] + ["1080p_n10000"])
+def test_raster_sum_backward_honours_a_callers_final_idx(cuda, oracle, name, share):
+    """the backward applies the reference's per-pixel skip of
+    entries k > final_idx[p] (backward.cu:783-786) for a final_idx that is NOT
+    the one this library's forward implies -- lowered on a random 10 % of the
+    pixels, or 0 everywhere -- through the reference-named op and the zeroed
+    C entry, each against oracle.raster_sum_backward on the same final_idx."""
+    from gsvc_amd import _lib as L
+    from gsvc_amd import ops
+    if name.startswith("1080p"):
+        H, W, n = 1080, 1920, 10000
+        rng0 = np.random.default_rng(5)
+        means = (2 * rng0.random((n, 2)) - 1).astype(np.float32)
+        Lc = (rng0.random((n, 3)) + np.array([0.5, 0, 0.5])).astype(np.float32)
+        cols = rng0.random((n, 3)).astype(np.float32)
+        r = oracle.render_sum(means, Lc, cols, np.ones((n, 1), np.float32), H, W)
+        z = dict(gaussian_ids_sorted=r["gids_sorted"], tile_bins=r["bins"], xys=r["xys"],
+                 conics=r["conics"], colors=cols, opacity=np.ones((n, 1), np.float32),
+                 final_idx=r["final_idx"])
+    else:
+        z = load_golden(name)
+        H, W = int(z["H"]), int(z["W"])
+    tb = _tb(H, W)
+    bins_t = ops._bins_for(T(np.asarray(z["tile_bins"], np.int32)), tb[0] * tb[1])[: tb[0] * tb[1]].contiguous()
+    rng = np.random.default_rng(17)
+    fi = _lowered_final_idx(z["final_idx"], N(bins_t), tb[0], W, rng, share)
+    assert share is None or (fi != np.asarray(z["final_idx"])).mean() > 0.01
+    v_out = rng.standard_normal((H, W, 3)).astype(np.float32)
+    ref = oracle.raster_sum_backward(tb, H, W, z["gaussian_ids_sorted"], z["tile_bins"], z["xys"],
+                                     z["conics"], z["colors"], z["opacity"], fi, v_out)
+    g = ops.rasterize_sum_backward(H, W, 16, 16, T(z["gaussian_ids_sorted"]), T(z["tile_bins"]),
+                                   T(z["xys"]), T(z["conics"]), T(z["colors"]), T(z["opacity"]),
+                                   T(np.ones(3, np.float32)), None, T(fi), T(v_out), None)
+    # the zeroed entry (the op path's), into a zeroed record
+    nn = np.asarray(z["xys"]).shape[0]
+    rec = torch.zeros((nn, 16), dtype=torch.float32, device=cuda)
+    args = [T(z["gaussian_ids_sorted"]), bins_t, T(z["xys"]), T(z["conics"]), T(z["colors"]),
+            T(z["opacity"]), T(fi), T(v_out)]
+    L.call("gsvc_rasterize_sum_backward_zeroed", H, W, nn, *[L.ptr(a) for a in args],
+           L.ptr(rec), L.stream(cuda))
+    g2 = ops.split_grad_records(rec)
+    for got in (g, g2):
+        for a, b, nm in zip(got, ref, ("v_xy", "v_conic", "v_colors", "v_opacity")):
+            scale = max(1.0, float(np.abs(b).max()))
+            np.testing.assert_allclose(N(a), b, rtol=1e-4, atol=1e-4 * scale, err_msg=nm)
+    if share is None:  # every entry skipped except sorted index 0
+        others = np.ones(nn, bool)
+        others[np.asarray(z["gaussian_ids_sorted"]).reshape(-1)[:1]] = False
+        assert np.abs(N(g[2])[others]).max() == 0
+
+
+@pytest.mark.parametrize("name", [c for c in SUM_CASES if "empty" not in c])
+def test_raster_sum_backward_no_opacity_flag(cuda, oracle, name):
+    """GSVC_BWD_NO_OPACITY (the C++ Function's backward when opacity takes no
+    gradient, as GSVC's constant ones): v_xy, v_conic and v_colors as the oracle
+    (1e-4), record word 8 untouched (still the zero the caller wrote)."""
+    from gsvc_amd import _lib as L
+    from gsvc_amd import ops
+    z = load_golden(name)
+    H, W = int(z["H"]), int(z["W"])
+    tb = _tb(H, W)
+    rng = np.random.default_rng(23)
+    v_out = rng.standard_normal((H, W, 3)).astype(np.float32)
+    ref = oracle.raster_sum_backward(tb, H, W, z["gaussian_ids_sorted"], z["tile_bins"], z["xys"],
+                                     z["conics"], z["colors"], z["opacity"], z["final_idx"], v_out)
+    nn = np.asarray(z["xys"]).shape[0]
+    bins_t = ops._bins_for(T(np.asarray(z["tile_bins"], np.int32)), tb[0] * tb[1])[: tb[0] * tb[1]].contiguous()
+    vo = T(v_out)
+    for flags in (1, 0):
+        rec = torch.zeros((nn, 16), dtype=torch.float32, device=cuda)
+        args = [T(z["gaussian_ids_sorted"]), bins_t, T(z["xys"]), T(z["conics"]), T(z["colors"]),
+                T(z["opacity"]), T(np.asarray(z["final_idx"], np.int32)), vo]
+        L.call("gsvc_rasterize_sum_backward_zeroed_strided_ex", H, W, nn, *[L.ptr(a) for a in args],
+               3 * W, 3, 1, L.ptr(rec), L.stream(cuda), flags)
+        got = ops.split_grad_records(rec)
+        for a, b, nm in list(zip(got, ref, ("v_xy", "v_conic", "v_colors", "v_opacity")))[: 4 - flags]:
+            scale = max(1.0, float(np.abs(b).max()))
+            np.testing.assert_allclose(N(a), b, rtol=1e-4, atol=1e-4 * scale, err_msg=f"{nm} flags={flags}")
+        if flags:
+            assert float(rec[:, 8:].abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("name", SUM_CASES)
 def test_autograd_end_to_end_matches_reference_glue(cuda, name):
     """gsplat.project_gaussians_2d -> rasterize_gaussians_sum -> backward, as
