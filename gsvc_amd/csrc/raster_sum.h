@@ -21,7 +21,6 @@ struct SumFwdArgs {
     int cut;           // sparse render chunks may take the sigma-threshold blend (knob 19 = 1: never)
     int xcd_off;       // diagnostic A/B (knob 37): 1 tiles in dispatch order, 4 xcd_remap ranges
     int ids_cap;       // id slabs: slots per tile (kTilePix, or kCarryCap for wide slabs)
-    int norank;        // diagnostic A/B (knob 31 = 1): <= 64 slab entries staged in slot order, not by id
     const int *m_dev;  // device num_intersects (NULL: > 0); 0 -> background
     const float *bg;
     const int *ids;

@@ -346,14 +346,12 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         int *s_rid = reinterpret_cast<int *>(s_list);
         s_rid[lane] = id;
         wave_lds_sync();
+        // (staging in slot order instead was measured, round 5: -3-5 %, at the
+        // cost of bit-identity with the op path and run-to-run determinism)
         int rank = 0;
-        if (kDiag && A.norank) {  // A/B only: slot order (the sums' order then follows the atomics)
-            rank = lane;
-        } else {
-            for (int k = 0; k < cnt; k += 4) {
-                const int4 q = *reinterpret_cast<const int4 *>(s_rid + k);
-                rank += (q.x < id ? 1 : 0) + (q.y < id ? 1 : 0) + (q.z < id ? 1 : 0) + (q.w < id ? 1 : 0);
-            }
+        for (int k = 0; k < cnt; k += 4) {
+            const int4 q = *reinterpret_cast<const int4 *>(s_rid + k);
+            rank += (q.x < id ? 1 : 0) + (q.y < id ? 1 : 0) + (q.z < id ? 1 : 0) + (q.w < id ? 1 : 0);
         }
         wave_lds_sync();
         if (A.bins_out) {  // the op path: the tile's ids in id order and its bins, for the backward
@@ -697,41 +695,32 @@ __device__ __forceinline__ void write_sorted_ids(const SumFwdArgs &A, int tile, 
 // mode 128-thread workgroups (two waves per tile).
 // kIdx: final_idx is written (the autograd forward); the render paths launch
 // the kIdx = false instance, which tracks no indices.
-// kTPW (one-wave modes): tiles per workgroup, one per wave (A/B knob 35: the
-// workgroup dispatch rate sets a 2.4 us spread over 8160 one-wave workgroups)
-template <int kMode, bool kIdx, int kTPW = 1>
+// (2 and 4 one-tile waves per workgroup were measured, round 5: within +-2 %,
+// not kept)
+template <int kMode, bool kIdx>
 __global__ __launch_bounds__(kMode == kModeSparse || kMode == kModeSparseStamp || kMode == kModeSparsePrio ||
-                              kMode == kModeSparseIds ? 64 * kTPW : 128, 8) void
+                              kMode == kModeSparseIds ? 64 : 128, 8) void
 raster_sum_fwd_kernel(SumFwdArgs A) {
     constexpr bool kOneWave = kMode == kModeSparse || kMode == kModeSparseStamp || kMode == kModeSparsePrio ||
                               kMode == kModeSparseIds;
-    static_assert(kTPW == 1 || kOneWave, "several tiles per workgroup: one-wave modes only");
     // id slabs: the op path's autograd forward (kIdx, or sparse / banded
     // without final_idx) and the single-frame render
     constexpr bool kIds = kIdx || kMode == kModeSparseIds || kMode == kModeBanded;
-    __shared__ float4 s_buf[kOneWave ? kTPW : 2][kSlice];
-    __shared__ int s_ids[kTPW][kTilePix];  // the tile's sorted ids (one copy per tile)
+    __shared__ float4 s_buf[kOneWave ? 1 : 2][kSlice];
+    __shared__ int s_ids[1][kTilePix];  // the tile's sorted ids
     // raised wave priority over the staging (loads, ranking, lists): the
     // arbiter favours older waves, so a young wave would otherwise wait behind
     // its elders' blending to issue its round trips (train.hip, same reason)
     if (kMode == kModeSparsePrio) __builtin_amdgcn_s_setprio(3);
     const int w = kOneWave ? 0 : (threadIdx.x >> 6);
-    // this wave's tile of the workgroup's (wave-uniform: a scalar register)
-    const int sub = kTPW > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
-    int tile;
-    if (kTPW > 1) {
-        const int total = A.ntiles * A.frames;
-        tile = xcd_remap(blockIdx.x, (total + kTPW - 1) / kTPW) * kTPW + sub;
-        if (tile >= total) return;  // (one-wave modes: no workgroup barrier)
-    } else {
-        // runs of 16 tiles dealt over the XCDs, as the training tile kernel
-        // (fbench: 10k frame 17.0 vs 17.3-17.4 us, the textured video's dense
-        // frame 116 at M = 894k 251.5-252.6 vs 263.9-264.6, trained 50k equal;
-        // A/B knob 37: 1 dispatch order, 4 contiguous XCD ranges)
-        tile = !(kDiag && A.xcd_off) ? xcd_runs<16>(blockIdx.x, A.ntiles * A.frames)
-               : A.xcd_off == 1      ? (int)blockIdx.x
-                                     : xcd_remap(blockIdx.x, A.ntiles * A.frames);
-    }
+    constexpr int sub = 0;
+    // runs of 16 tiles dealt over the XCDs, as the training tile kernel
+    // (fbench: 10k frame 17.0 vs 17.3-17.4 us, the textured video's dense
+    // frame 116 at M = 894k 251.5-252.6 vs 263.9-264.6, trained 50k equal;
+    // A/B knob 37: 1 dispatch order, 4 contiguous XCD ranges)
+    int tile = !(kDiag && A.xcd_off) ? xcd_runs<16>(blockIdx.x, A.ntiles * A.frames)
+                     : A.xcd_off == 1      ? (int)blockIdx.x
+                                           : xcd_remap(blockIdx.x, A.ntiles * A.frames);
     if (A.frames > 1) {  // batched frames: this block's frame and tile
         const int b = tile / A.ntiles;
         tile -= b * A.ntiles;
@@ -1485,7 +1474,6 @@ void sum_fwd_args_init(SumFwdArgs &A) {
     A.spec_slots = knob(10) > 0 && knob(10) < kHeadSlots ? knob(10) : kHeadSlots;
     A.group_min = knob(15) > 0 ? knob(15) - 1 : kGroupMinDefault;
     A.cut = knob(19) != 1;
-    A.norank = knob(31) == 1;
     A.ids_cap = kTilePix;
     A.xcd_off = knob(37);
     A.layout = kLayoutHWC;
@@ -1532,18 +1520,7 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
                                : raster_sum_fwd_kernel<kModeBanded, false>,
                    grid, dim3(128), s, tev, A);
     } else if (mode == kModeSparseIds) {
-        bool done = false;
-        if constexpr (kDiag) {
-            if (knob(35) == 2 || knob(35) == 4) {  // A/B: tiles per workgroup
-                const int k = knob(35);
-                const dim3 g2(ceil_div(ntiles * A.frames, k));
-                launch_fwd(k == 2 ? raster_sum_fwd_kernel<kModeSparseIds, false, 2>
-                                  : raster_sum_fwd_kernel<kModeSparseIds, false, 4>,
-                           g2, dim3(64 * k), s, tev, A);
-                done = true;
-            }
-        }
-        if (!done) launch_fwd(raster_sum_fwd_kernel<kModeSparseIds, false>, grid, dim3(64), s, tev, A);
+        launch_fwd(raster_sum_fwd_kernel<kModeSparseIds, false>, grid, dim3(64), s, tev, A);
     } else if constexpr (kDiag) {
         // diagnostic variants (libgsvc_amd_diag.so only)
         switch (mode) {
@@ -1676,11 +1653,9 @@ static int forward_slabs_impl(
     }
     if (num_points > 0 && ordered) {
         const bool refresh = (order_flags & GSVC_TRAIN_ORDER_REFRESH) != 0;
-        // A/B knob 33: 128 or 512 threads per workgroup (default kProjThreads)
-        const int thr = knob(33) == 128 || knob(33) == 512 ? knob(33) : kProjThreads;
-        auto kfn = thr == 128 ? tile_insert_ids_ordered_kernel<128>
-                              : (thr == 512 ? tile_insert_ids_ordered_kernel<512>
-                                            : tile_insert_ids_ordered_kernel<kProjThreads>);
+        // (128 and 512 threads per workgroup measured, round 5: no gain)
+        constexpr int thr = kProjThreads;
+        auto kfn = tile_insert_ids_ordered_kernel<kProjThreads>;
         hipLaunchKernelGGL(kfn, dim3(ceil_div(num_points, thr)), dim3(thr), 0, s, num_points,
                            (order_flags & GSVC_TRAIN_ORDER) ? (const int *)ow.order : nullptr,
                            (const float2 *)xys, radii, tbx, tby, counts + (size_t)par * ntiles,

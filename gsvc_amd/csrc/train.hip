@@ -74,7 +74,7 @@ struct TrainTileArgs {
     float4 *det_part;
     long long det_cap;
     int prio;  // raise the wave priority over the order phase (s_setprio; knob 16 = 1 off)
-    int xcd_off;  // diagnostic A/B (knob 37): 1 dispatch order, 3 xcd_runs<4>, 4 xcd_remap ranges
+    int xcd_off;  // diagnostic A/B (knob 37): 1 dispatch order, 4 xcd_remap ranges
     // GSVC_TRAIN_CARRY (band kernel): the tile's candidates are the splat ids
     // cids[tile][0, counts[tile]) -- a superset of its entries carried from
     // step to step (train_splat_kernel) -- and an entry is a candidate whose
@@ -688,12 +688,10 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     // objects) spread over all eight instead of loading the one or two whose
     // contiguous range covers them (tile kernel 273.7 -> 238.7 us on the
     // textured video's frame 116, unchanged on the bench's frame).
-    // A/B knob 37: 1 dispatch order, 3 runs of 4, 5 of 8, 6 of 32, 4 contiguous ranges
+    // A/B knob 37: 1 dispatch order, 4 contiguous ranges (runs of 4, 8 and 32
+    // were measured, round 5: within the dense frame's spread, not kept)
     const int tile = !(kDiag && A.xcd_off) ? xcd_runs<16>(blockIdx.x, A.ntiles)
                      : A.xcd_off == 1      ? (int)blockIdx.x
-                     : A.xcd_off == 3      ? xcd_runs<4>(blockIdx.x, A.ntiles)
-                     : A.xcd_off == 5      ? xcd_runs<8>(blockIdx.x, A.ntiles)
-                     : A.xcd_off == 6      ? xcd_runs<32>(blockIdx.x, A.ntiles)
                                            : xcd_remap(blockIdx.x, A.ntiles);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     long long *st = kStamp ? A.stamps + 8 * (size_t)tile : nullptr;
@@ -1352,17 +1350,12 @@ struct TrainSplatArgs {
     int *m_next;
     long long *stamps;  // diagnostic: int64[waves][8]
     int split;          // two waves per 64 splats (splat_step_split); 0: one lane per splat
-    int no_loss;        // diagnostic (knob 38 = 1, wrong losses): the loss workgroup only releases the sequence word
 };
 
 // GSVC_TRAIN_CARRY: splat i's projection for the next frame from its updated
 // parameters p = {xyz 2, cholesky 3, features 3, rgb_w} -- load_project's op
 // sequence (frame_dev.h), so the record bits equal a projection kernel's --
 // and the upkeep of its carried bins.  Returns its box area (its share of M).
-// kPart (splat_step_split, both waves project, each its share of the stores):
-// 0 all, 1 the geometry wave's (record row 0, xys, radii, gradient zeroing), 2
-// the colour wave's (record rows 1-2, the box and the bins' upkeep; its share of M).
-template <int kPart = 0>
 __device__ __forceinline__ int carry_splat(const TrainSplatArgs &A, int i, const float (&p)[9],
                                            uint2 h) {
     const float mx = tanhf(p[0]), my = tanhf(p[1]);
@@ -1379,18 +1372,15 @@ __device__ __forceinline__ int carry_splat(const TrainSplatArgs &A, int i, const
         b = b * p[8];
     }
     const SplatOut S = splat_out(i, mx, my, l11, l21, l22, r, g, b, 1.0f, A.hw, A.hh, A.tbx, A.tby);
-    if (kPart != 2) {
-        A.rec[3 * i] = S.r0;
-        A.xys[i] = S.P.xy;
-        A.radii[i] = S.P.rad;
-        // the record's first 32 bytes (v_xy, v_conic, v_colors: what the tile
-        // kernel adds and this kernel reads; v_opacity and the padding stay as a
-        // projection zeroed them -- nothing in the fused step writes them)
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        A.grad[4 * i] = z;
-        A.grad[4 * i + 1] = z;
-    }
-    if (kPart == 1) return 0;
+    A.rec[3 * i] = S.r0;
+    A.xys[i] = S.P.xy;
+    A.radii[i] = S.P.rad;
+    // the record's first 32 bytes (v_xy, v_conic, v_colors: what the tile
+    // kernel adds and this kernel reads; v_opacity and the padding stay as a
+    // projection zeroed them -- nothing in the fused step writes them)
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    A.grad[4 * i] = z;
+    A.grad[4 * i + 1] = z;
     A.rec[3 * i + 1] = S.r1;
     A.rec[3 * i + 2] = S.r2;
     unsigned x0 = 0, y0 = 0, x1 = 0, y1 = 0;
@@ -1616,7 +1606,6 @@ __device__ __forceinline__ int splat_step(const TrainSplatArgs &A, int i, long l
 // are split the same way (each half its components, in splat_step's order).
 __device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int base) {
     __shared__ float s_cp[2][4][64];  // per splat group: new feature r g b, rgb_W
-    __shared__ float s_gp[2][5][64];  // per splat group: new xyz, cholesky (A.split == 2; xyz: 3)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, grp = w >> 1;
     const int i = base + grp * 64 + lane;
     const bool have = i < A.n;
@@ -1633,68 +1622,10 @@ __device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int bas
         db = A.det_off[i];
         de = min((long long)A.det_off[i + 1], A.det_cap);
     }
-    // A.split == 3: the xyz elements (0-1) on the colour wave as well -- their
-    // gradient needs only v_xy, not the projection VJP -- so the geometry wave
-    // is left the VJP, the three cholesky elements and the carry
-    // (diagnostic library only: measured equal, 10.49 / 10.74 vs 10.59 / 10.52 us,
-    // profiles/r05/splat_split/xy_*.log)
-    const bool xy_col = kDiag && A.split == 3;
+    // (measured, round 5, and not kept: the xyz elements on the colour wave,
+    // and both waves projecting with each its share of the carry's stores --
+    // both within the noise; profiles/r05/splat_split/)
     if (w & 1) {
-        if (xy_col) {
-            float4 g0 = A.grad[4 * ic];  // v_xy.x, v_xy.y
-            if (A.det_off) {
-                float sx = 0.f, sy = 0.f;
-                for (long long k = db; k < de; ++k) {
-                    const float4 p0 = A.det_part[2 * k];
-                    sx += p0.x;
-                    sy += p0.y;
-                }
-                g0.x = sx + g0.x;
-                g0.y = sy + g0.y;
-            }
-            const int rad = A.radii[ic];
-            const float x0 = A.xyz[2 * ic], x1 = A.xyz[2 * ic + 1];
-            float m[2], v[2], df[2], npg[2];
-#pragma unroll
-            for (int e = 0; e < 2; ++e) m[e] = v[e] = df[e] = npg[e] = 0.0f;
-            if (upd) {
-                ld_row<2>(A.state[0][0], ic, m);
-                ld_row<2>(A.state[0][1], ic, v);
-                ld_row<2>(A.state[0][2], ic, df);
-                ld_row<2>(A.state[0][3], ic, npg);
-            }
-            float vmx = 0.f, vmy = 0.f;
-            if (rad > 0) {
-                vmx = g0.x * A.hw;
-                vmy = g0.y * A.hh;
-            }
-            const float t0 = tanhf(x0), t1 = tanhf(x1);
-            const float dx0 = vmx * (1.0f - t0 * t0), dx1 = vmy * (1.0f - t1 * t1);
-            float px[2] = {x0, x1};
-            if (!upd) {
-                if (have) {
-                    float *o = A.grads_out + 9 * (size_t)i;
-                    o[0] = dx0;
-                    o[1] = dx1;
-                }
-            } else {
-                const float g[2] = {dx0, dx1};
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    if (A.first[0]) npg[e] = -(g[e] * A.S.clip);
-                    px[e] = adan_update(A.S, px[e], g[e], m[e], v[e], df[e], npg[e]);
-                }
-                if (have) {
-                    st_row<2>(A.xyz, i, px);
-                    st_row<2>(A.state[0][0], i, m);
-                    st_row<2>(A.state[0][1], i, v);
-                    st_row<2>(A.state[0][2], i, df);
-                    st_row<2>(A.state[0][3], i, npg);
-                }
-            }
-            s_gp[grp][0][lane] = px[0];
-            s_gp[grp][1][lane] = px[1];
-        }
         // colour half: elements 5-7 (features) and 8 (rgb_W)
         float4 g1 = A.grad[4 * ic + 1];  // v_conic 2, v_colors r g b
         if (A.det_off) {
@@ -1781,18 +1712,16 @@ __device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int bas
         const float4 r0 = A.rec[3 * ic], r2 = A.rec[3 * ic + 2];
         const int rad = A.radii[ic];
         const float c0 = A.chol[3 * ic], c1 = A.chol[3 * ic + 1], c2 = A.chol[3 * ic + 2];
-        const float x0 = xy_col ? 0.f : A.xyz[2 * ic], x1 = xy_col ? 0.f : A.xyz[2 * ic + 1];
+        const float x0 = A.xyz[2 * ic], x1 = A.xyz[2 * ic + 1];
         hull = A.carry ? A.chull[ic] : make_uint2(0u, 0u);
         float m[5], v[5], df[5], npg[5];
 #pragma unroll
         for (int e = 0; e < 5; ++e) m[e] = v[e] = df[e] = npg[e] = 0.0f;
         if (upd) {
-            if (!xy_col) {
-                ld_row<2>(A.state[0][0], ic, m);
-                ld_row<2>(A.state[0][1], ic, v);
-                ld_row<2>(A.state[0][2], ic, df);
-                ld_row<2>(A.state[0][3], ic, npg);
-            }
+            ld_row<2>(A.state[0][0], ic, m);
+            ld_row<2>(A.state[0][1], ic, v);
+            ld_row<2>(A.state[0][2], ic, df);
+            ld_row<2>(A.state[0][3], ic, npg);
             ld_row<3>(A.state[1][0], ic, m + 2);
             ld_row<3>(A.state[1][1], ic, v + 2);
             ld_row<3>(A.state[1][2], ic, df + 2);
@@ -1835,10 +1764,8 @@ __device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int bas
         if (!upd) {
             if (have) {
                 float *o = A.grads_out + 9 * (size_t)i;
-                if (!xy_col) {
-                    o[0] = dx0;
-                    o[1] = dx1;
-                }
+                o[0] = dx0;
+                o[1] = dx1;
                 o[2] = vl0;
                 o[3] = vl1;
                 o[4] = vl2;
@@ -1848,18 +1775,15 @@ __device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int bas
 #pragma unroll
             for (int e = 0; e < 5; ++e) {
                 const int q = e < 2 ? 0 : 1;
-                if (q == 0 && xy_col) continue;
                 if (A.first[q]) npg[e] = -(g[e] * A.S.clip);
                 pnew[e] = adan_update(A.S, pnew[e], g[e], m[e], v[e], df[e], npg[e]);
             }
             if (have) {
-                if (!xy_col) {
-                    st_row<2>(A.xyz, i, pnew);
-                    st_row<2>(A.state[0][0], i, m);
-                    st_row<2>(A.state[0][1], i, v);
-                    st_row<2>(A.state[0][2], i, df);
-                    st_row<2>(A.state[0][3], i, npg);
-                }
+                st_row<2>(A.xyz, i, pnew);
+                st_row<2>(A.state[0][0], i, m);
+                st_row<2>(A.state[0][1], i, v);
+                st_row<2>(A.state[0][2], i, df);
+                st_row<2>(A.state[0][3], i, npg);
                 st_row<3>(A.chol, i, pnew + 2);
                 st_row<3>(A.state[1][0], i, m + 2);
                 st_row<3>(A.state[1][1], i, v + 2);
@@ -1867,31 +1791,12 @@ __device__ __forceinline__ int splat_step_split(const TrainSplatArgs &A, int bas
                 st_row<3>(A.state[1][3], i, npg + 2);
             }
         }
-        if (A.split == 2) {
-#pragma unroll
-            for (int e = 0; e < 5; ++e) s_gp[grp][e][lane] = pnew[e];
-        }
     }
-    if (A.split == 2 && (w & 1) && A.carry) hull = A.chull[ic];  // the colour wave keeps the bins
     __syncthreads();
-    if (have && upd && A.carry) {
-        if (A.split == 2) {
-            // both waves project; each writes its share (A/B knob 36 = 2)
-            const bool geo = !(w & 1);
-            const float p[9] = {geo ? pnew[0] : s_gp[grp][0][lane], geo ? pnew[1] : s_gp[grp][1][lane],
-                                geo ? pnew[2] : s_gp[grp][2][lane], geo ? pnew[3] : s_gp[grp][3][lane],
-                                geo ? pnew[4] : s_gp[grp][4][lane], s_cp[grp][0][lane],
-                                s_cp[grp][1][lane], s_cp[grp][2][lane], s_cp[grp][3][lane]};
-            hits = geo ? carry_splat<1>(A, i, p, hull) : carry_splat<2>(A, i, p, hull);
-        } else if (!(w & 1)) {
-            if (xy_col) {
-                pnew[0] = s_gp[grp][0][lane];
-                pnew[1] = s_gp[grp][1][lane];
-            }
-            const float p[9] = {pnew[0], pnew[1], pnew[2], pnew[3], pnew[4], s_cp[grp][0][lane],
-                                s_cp[grp][1][lane], s_cp[grp][2][lane], s_cp[grp][3][lane]};
-            hits = carry_splat(A, i, p, hull);
-        }
+    if (have && upd && A.carry && !(w & 1)) {
+        const float p[9] = {pnew[0], pnew[1], pnew[2], pnew[3], pnew[4], s_cp[grp][0][lane],
+                            s_cp[grp][1][lane], s_cp[grp][2][lane], s_cp[grp][3][lane]};
+        hits = carry_splat(A, i, p, hull);
     }
     return hits;
 }
@@ -1905,12 +1810,6 @@ __global__ __launch_bounds__(kBlock) void train_splat_kernel(TrainSplatArgs A) {
         // the first workgroup (no splats): the loss; dispatched first so it
         // runs beside the splats
         __shared__ double s_l[2][4];
-        if (kDiag && A.no_loss) {  // the sequence word alone (the host waits for it)
-            if (threadIdx.x == 0 && A.loss_seq)
-                __hip_atomic_store(reinterpret_cast<unsigned *>(A.loss) + 2, A.loss_seq,
-                                   __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            return;
-        }
         publish_loss<kBlock>(A.err, A.ntiles, A.inv_count, A.loss, A.loss_seq, A.det_off, A.n, s_l);
         if (kStamp) splat_stamp(st, 5);
         return;
@@ -2152,7 +2051,7 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     T.diag = knob(13);
     T.grouped = knob(14) != 1;
     T.prio = knob(16) != 1;  // A/B knob 16 = 1: no raised priority
-    T.xcd_off = knob(37);  // A/B: 1 dispatch order, 3 runs of 4 tiles, 4 contiguous XCD ranges
+    T.xcd_off = knob(37);  // A/B: 1 dispatch order, 4 contiguous XCD ranges
     T.det_off = det_off;
     T.det_part = det_part;
     T.det_cap = det_capacity;
@@ -2266,8 +2165,7 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     // (1: the carry in the geometry wave; A/B knob 36 = 2: both waves project and
     // share its stores -- measured equal, 9.92-10.0 vs 9.85-9.98 us, not kept;
     // 3: the xyz elements on the colour wave)
-    P.split = sb == 256 && knob(34) != 1 ? (knob(36) == 2 || knob(36) == 3 ? knob(36) : 1) : 0;
-    P.no_loss = knob(38) == 1;
+    P.split = sb == 256 && knob(34) != 1 ? 1 : 0;
     const int per_block = P.split ? sb / 2 : sb;
     const int blocks = (num_points > 0 ? ceil_div(num_points, per_block) : 0) + 1;
     hipEvent_t tev[2];

@@ -43,8 +43,8 @@ def test_id_slab_render_bit_identical(cuda, oracle, n, H, W, chol, cluster):
     bg = torch.tensor([0.3, 0.6, 0.9], device=cuda)
     ref = [render_frame_sum(xyz, c, f, H, W, bg, cholesky_bound=bound) for _ in range(2)]
     got = []
-    # records; banded; the order at any density; 2 and 4 tiles per workgroup
-    for pair in ((24, 1), (0, 2), (27, 1), (35, 2), (35, 4)):
+    # records; banded; the order at any density
+    for pair in ((24, 1), (0, 2), (27, 1)):
         with knobs(pair):
             got += [render_frame_sum(xyz, c, f, H, W, bg, cholesky_bound=bound) for _ in range(3)]
     torch.cuda.synchronize()
