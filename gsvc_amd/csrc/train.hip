@@ -1225,7 +1225,16 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                     // the reference's test as written
                     auto walk = [&](auto kcut) {
                         for (; vp <= ve; ++vp, dx -= 1.0f) {
-                            const float Px = vp[0], Py = vp[kTile * kVRow], Pz = vp[2 * kTile * kVRow];
+                            float Px, Py, Pz;
+                            if (kDiag && (A.diag & 256)) {  // diag 256: no v_out reads (wrong)
+                                Px = dx;
+                                Py = 0.5f * dx;
+                                Pz = bdy;
+                            } else {
+                                Px = vp[0];
+                                Py = vp[kTile * kVRow];
+                                Pz = vp[2 * kTile * kVRow];
+                            }
                             const float sgm = fmaf(fmaf(eha, dx, bdy), dx, cq);
                             const float vis = exp_neg(sgm);
                             float al;
