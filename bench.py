@@ -494,7 +494,7 @@ def render_block(model, steps, warmup):
     shape = frame_shape(model.get_xyz.detach(), model.get_cholesky_elements.detach(),
                         model.tile_bounds)
     prof = load_profile(f"render_{model._xyz.shape[0]}")
-    roof = roofline("raster_sum_fwd_kernel (composite)", composite_bytes(shape),
+    roof = roofline("raster_render_ids_kernel (composite: the single-frame render)", composite_bytes(shape),
                     times["composite"], prof, "rasterize_sum_forward")
     vr = valu_roofline(f"render_{model._xyz.shape[0]}",
                        roof.get("trace_avg_kernel_us") or roof["avg_kernel_us"])

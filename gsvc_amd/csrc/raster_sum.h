@@ -20,6 +20,9 @@ struct SumFwdArgs {
     int group_min;     // sparse chunks of <= this many entries skip the lane-group lists
     int cut;           // sparse render chunks may take the sigma-threshold blend (knob 19 = 1: never)
     int xcd_off;       // diagnostic A/B (knob 37): 1 tiles in dispatch order, 4 xcd_remap ranges
+    int ablate;        // diagnostic (knob 36, wrong results): sparse tile phases skipped --
+                       // 1 blend, 2 stores, 4 record loads, 8 ranking,
+                       // 16 every load (raster_render_ids_kernel)
     int ids_cap;       // id slabs: slots per tile (kTilePix, or kCarryCap for wide slabs)
     const int *m_dev;  // device num_intersects (NULL: > 0); 0 -> background
     const float *bg;

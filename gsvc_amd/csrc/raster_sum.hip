@@ -101,6 +101,25 @@ __device__ __forceinline__ long long stamp() {
 
 typedef float v2f __attribute__((ext_vector_type(2)));
 
+// Diagnostic library only: the id-slab render's phases stamped per tile when
+// A.stamps is set (knob 39 = 1 with gsvc_debug_set_ptr; int64[ntiles][8]: start,
+// ids arrived, staged, blended, stores drained, entry count)
+template <int kMode>
+constexpr bool kIdStampMode = kDiag && kMode == kModeSparseIds;
+
+// phase stamp k4 (kModeSparseStamp's 4-slot layout) or k8 (the id-slab 8-slot one)
+template <int kMode>
+__device__ __forceinline__ void phase_stamp(const SumFwdArgs &A, int tile, int k4, int k8) {
+    if (kMode == kModeSparseStamp) {
+        if ((threadIdx.x & 63) == 0) A.stamps[4 * (size_t)tile + k4] = stamp();
+    } else if (kIdStampMode<kMode>) {
+        if (A.stamps) {
+            const long long t = stamp();
+            if ((threadIdx.x & 63) == 0) A.stamps[8 * (size_t)tile + k8] = t;
+        }
+    }
+}
+
 // One splat against two pixels of a row (packed v_pk_fma / v_pk_mul): the
 // reference's per-pixel op sequence (common.h splat_sigma_h, exp_neg) on both
 // lanes of a v2f.  A pair that fails sigma >= 0 and alpha >= 1/255 keeps its
@@ -326,7 +345,11 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         const int cnt = n;
             // <= 64 slab records in fill order: staged at their rank by id
         float4 geo = spec0, col = spec1, bx = spec2;
-        if (lane >= spec_slots && lane < cnt) {
+        if (kIdStampMode<kMode> && A.stamps) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            phase_stamp<kMode>(A, tile, 0, 1);
+        }
+        if (lane >= spec_slots && lane < cnt && !(kDiag && (A.ablate & 4))) {
             if (seg_head || A.rec) {
                 // slab records at their slot, or (id slabs, no head) the record of
                 // the lane's id gathered from A.rec -- the same 48 bytes
@@ -349,6 +372,8 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         // (staging in slot order instead was measured, round 5: -3-5 %, at the
         // cost of bit-identity with the op path and run-to-run determinism)
         int rank = 0;
+        if (kDiag && (A.ablate & 8)) rank = lane;
+        else
         for (int k = 0; k < cnt; k += 4) {
             const int4 q = *reinterpret_cast<const int4 *>(s_rid + k);
             rank += (q.x < id ? 1 : 0) + (q.y < id ? 1 : 0) + (q.z < id ? 1 : 0) + (q.w < id ? 1 : 0);
@@ -413,8 +438,8 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
             if (kMode == kModeSparsePrio) __builtin_amdgcn_s_setprio(0);
             // a few entries: every lane walks them all (the lists would cost
             // more than the pairs they skip)
-            if (kMode == kModeSparseStamp && base == 0 && lane == 0) A.stamps[4 * (size_t)tile + 1] = stamp();
-            for (int t = 0; t < cnt; ++t) {
+            if (base == 0) phase_stamp<kMode>(A, tile, 1, 2);
+            for (int t = 0; t < cnt && !(kDiag && (A.ablate & 1)); ++t) {
                 if (!kIdx && cut)
                     blend(t, std::true_type{});
                 else
@@ -438,7 +463,7 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         }
         wave_lds_sync();
         if (kMode == kModeSparsePrio) __builtin_amdgcn_s_setprio(0);
-        if (kMode == kModeSparseStamp && base == 0 && lane == 0) A.stamps[4 * (size_t)tile + 1] = stamp();
+        if (base == 0) phase_stamp<kMode>(A, tile, 1, 2);
         // the lane's 4x4 block of the tile
         const unsigned char *ml = s_list + (((lane >> 4) << 2) | (lane & 3));
         for (int it = 0; it < maxlen; ++it) {
@@ -449,13 +474,13 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         }
         wave_lds_sync();
     }
-    if (kMode == kModeSparseStamp && lane == 0) A.stamps[4 * (size_t)tile + 2] = stamp();
+    phase_stamp<kMode>(A, tile, 2, 3);
     const float r0 = ar01.x, r1 = ar01.y, r2 = ar23.x, r3 = ar23.y;
     const float g0 = ag01.x, g1 = ag01.y, g2 = ag23.x, g3 = ag23.y;
     const float b0 = ab01.x, b1 = ab01.y, b2 = ab23.x, b3 = ab23.y;
     if (A.layout == kLayoutCHWClamped && A.vec_chw && (tx + 1) * kTile <= A.img_w) {
         // 4 lanes write a 64-byte row segment of each plane
-        if (pi < A.img_h) {
+        if (pi < A.img_h && !(kDiag && (A.ablate & 2))) {
             const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
             float *o = A.out + (size_t)pi * (size_t)A.img_w + (size_t)pj;
             st_f4(o, clamp01(r0), clamp01(r1), clamp01(r2), clamp01(r3), A.store_policy);
@@ -464,9 +489,9 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
             if (A.final_idx)
                 *reinterpret_cast<int4 *>(A.final_idx + (o - A.out)) = make_int4(l0, l1, l2, l3);
         }
-        if (kMode == kModeSparseStamp) {
+        if (kMode == kModeSparseStamp || (kIdStampMode<kMode> && A.stamps)) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) A.stamps[4 * (size_t)tile + 3] = stamp();
+            phase_stamp<kMode>(A, tile, 3, 4);
         }
         return;
     }
@@ -741,8 +766,12 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         A.splat_begin = A.frame_off[b];
         A.num_points = A.frame_off[b + 1];
     }
+    // M in the first round trip, before any store: read after the counts'
+    // clearing store it could not be a scalar load and waited a round trip of
+    // its own between the count and the records
+    const int m_val = A.m_dev ? *A.m_dev : 1;
     long long t0 = 0;
-    if (kMode == kModeStamp || kMode == kModeSparseStamp) t0 = stamp();
+    if (kMode == kModeStamp || kMode == kModeSparseStamp || (kIdStampMode<kMode> && A.stamps)) t0 = stamp();
     int2 range;
     SegIds seg;  // the tile's ids (unsorted when A.sort_ids)
     int n_all;
@@ -765,7 +794,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         if ((threadIdx.x & 63) == 0) {
             A.slab_counts_clear[tile] = 0u;  // the next frame's counts
             if (tile == 0) {
-                A.meta_out[0] = *A.m_dev;
+                A.meta_out[0] = m_val;
                 A.meta_out[1] = 0;
             }
         }
@@ -789,7 +818,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         if ((threadIdx.x & 63) == 0) {
             A.id_counts_clear[tile] = 0u;  // the next call's counts
             if (tile == 0) {
-                A.meta_out[0] = *A.m_dev;
+                A.meta_out[0] = m_val;
                 A.meta_out[1] = 0;
             }
         }
@@ -815,12 +844,16 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
     int n = n_all > kTilePix ? kTilePix : n_all;
     // rasterize_sum.py:121-127: a frame without intersections is the background
     float3 init = make_float3(0.f, 0.f, 0.f);
-    if (A.m_dev && *A.m_dev < 1) {
+    if (m_val < 1) {
         n = n_all = 0;
         init = make_float3(A.bg[0], A.bg[1], A.bg[2]);
     }
     const int ty = tile / A.tbx;
     if (kMode == kModeSparseStamp && (threadIdx.x & 63) == 0) A.stamps[4 * (size_t)tile] = t0;
+    if (kIdStampMode<kMode> && A.stamps && (threadIdx.x & 63) == 0) {
+        A.stamps[8 * (size_t)tile] = t0;
+        A.stamps[8 * (size_t)tile + 5] = n_all;
+    }
     const bool sparse = kMode == kModeSparse || kMode == kModeSparseStamp || kMode == kModeSparsePrio ||
                         kMode == kModeSparseIds ||
                         ((kMode == kModeAdaptive || kMode == kModeStamp) && n <= A.sparse_max);
@@ -864,6 +897,76 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
         st[w == 0 ? 0 : 2] = t0;
         st[w == 0 ? 1 : 3] = stamp();
     }
+}
+
+// The single-frame render over id slabs (render_frames with one frame: CHW
+// clamped planes, no final_idx, 1024-id slabs) -- the configs[1] render and
+// the frame render of configs[2] -- as W one-tile waves per workgroup
+// (production W = 2: workgroup b takes tiles 2b, 2b + 1) with a prologue of
+// its own.  raster_sum_fwd_kernel<kModeSparseIds>'s tile: the same device
+// functions (sum_fwd_sparse, wave_sorted_tile_ids, wave_brute_tile_ids) in the
+// same order, so the same bits (tools/fbench.py checks every A/B pass's image
+// against the first).  Measured against the generic kernel, interleaved on
+// three boxes (profiles/r06/render_ids/): one wave per workgroup -0.65 us at
+// 1080p / 10k; two -1.1 us at 10k (-9 %) and -1.2 to -1.5 us at the trained
+// 50k frame (-6 %), frame time -1.0 to -1.3 us; four: the composite -1.5 us
+// but 4.3 us between the projection's end and its start (the frame no
+// faster); two with XCD runs of 16 tiles instead of pairs: equal.  K tiles
+// per wave with every tile's loads issued before the first blends (K = 2, 4):
+// slower (12.7 vs 12.0 us; 4: 26 vs 20 us per frame).  A/B knob 38 = 1: the
+// generic kernel.
+template <int W>
+__global__ __launch_bounds__(64 * W, 8) void raster_render_ids_kernel(SumFwdArgs A) {
+    __shared__ float4 s_bufw[W][kSlice];
+    __shared__ int s_idsw[W][kTilePix];
+    const int lane = threadIdx.x & 63, w = W > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+    float4 *s_buf = s_bufw[w];
+    int *s_ids = s_idsw[w];
+    // W one-tile waves per workgroup: workgroup b (XCD b % 8) takes tiles W b .. W b + W - 1
+    const int tile = W == 1 ? xcd_runs<16>(blockIdx.x, A.ntiles) : (int)blockIdx.x * W + w;
+    if (tile >= A.ntiles) return;
+    // M, the count and slot `lane` in one round trip
+    const bool no_loads = kDiag && (A.ablate & 16);  // diagnostic: the stores alone
+    const int m_val = no_loads ? 1 : *A.m_dev;
+    const int n_all = no_loads ? 0 : (int)__builtin_amdgcn_readfirstlane(A.id_counts[tile]);
+    const int spec_id = no_loads ? 0 : A.ids_rw[(size_t)tile * kCarryCap + lane];
+    long long t0 = 0;
+    if (kIdStampMode<kModeSparseIds> && A.stamps) t0 = stamp();
+    if (lane == 0) {
+        A.id_counts_clear[tile] = 0u;  // the next frame's counts
+        if (tile == 0 && A.meta_out) {
+            A.meta_out[0] = m_val;
+            A.meta_out[1] = 0;
+        }
+    }
+    int n = n_all < kTilePix ? n_all : kTilePix;
+    // rasterize_sum.py:121-127: a frame without intersections is the background
+    float3 init = make_float3(0.f, 0.f, 0.f);
+    if (m_val < 1) {
+        n = 0;
+        init = make_float3(A.bg[0], A.bg[1], A.bg[2]);
+    }
+    if (kIdStampMode<kModeSparseIds> && A.stamps && lane == 0) {
+        A.stamps[8 * (size_t)tile] = t0;
+        A.stamps[8 * (size_t)tile + 5] = m_val < 1 ? 0 : n_all;
+    }
+    const int2 range = make_int2(tile * kCarryCap, tile * kCarryCap + n);
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (n <= kChunk) {
+        // <= 64 entries: the records gathered by id and ranked into the staging
+        sum_fwd_sparse<kModeSparseIds, false>(A, tile, range, n, s_buf, init, false, s_ids,
+                                              n > 0 ? A.rec : nullptr, nullptr, z, z, z, 0, spec_id);
+        return;
+    }
+    SegIds seg;
+    seg.ids = A.ids_rw + (size_t)tile * kCarryCap;
+    seg.cap_ids = kCarryCap;
+    seg.recs = nullptr;
+    seg.head = nullptr;
+    n = n_all > kCarryCap ? wave_brute_tile_ids(A, tile, s_ids)
+                          : wave_sorted_tile_ids(seg, n_all, s_ids, reinterpret_cast<unsigned *>(s_buf));
+    sum_fwd_sparse<kModeSparseIds, false>(A, tile, range, n, s_buf, init, true, s_ids, nullptr, nullptr, z,
+                                          z, z, 0, spec_id);
 }
 
 __device__ __forceinline__ int ceil_log2(int n) { return n <= 1 ? 0 : 32 - __clz(n - 1); }
@@ -1476,6 +1579,7 @@ void sum_fwd_args_init(SumFwdArgs &A) {
     A.cut = knob(19) != 1;
     A.ids_cap = kTilePix;
     A.xcd_off = knob(37);
+    A.ablate = knob(36);
     A.layout = kLayoutHWC;
     A.frames = 1;
 }
@@ -1520,7 +1624,15 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
                                : raster_sum_fwd_kernel<kModeBanded, false>,
                    grid, dim3(128), s, tev, A);
     } else if (mode == kModeSparseIds) {
-        launch_fwd(raster_sum_fwd_kernel<kModeSparseIds, false>, grid, dim3(64), s, tev, A);
+        if (kDiag && knob(39) == 1 && A.frames == 1) A.stamps = reinterpret_cast<long long *>(debug_ptr());
+        // the single-frame render: two one-tile waves per workgroup (A/B knob 38 = 1:
+        // the generic kernel)
+        const bool render = A.frames == 1 && !A.bins_out && !A.final_idx && A.m_dev &&
+                            A.ids_cap == kCarryCap && A.layout == kLayoutCHWClamped && A.rec && A.sort_ids;
+        if (render && knob(38) != 1)
+            launch_fwd(raster_render_ids_kernel<2>, dim3((A.ntiles + 1) / 2), dim3(128), s, tev, A);
+        else
+            launch_fwd(raster_sum_fwd_kernel<kModeSparseIds, false>, grid, dim3(64), s, tev, A);
     } else if constexpr (kDiag) {
         // diagnostic variants (libgsvc_amd_diag.so only)
         switch (mode) {

@@ -2169,11 +2169,12 @@ static int train_step_impl(int num_points, float *xyz, float *cholesky,
     const int sb = knob(21) == 64 || knob(21) == 128 || knob(21) == 192 || knob(21) == 512
                        ? knob(21)
                        : 256;
-    // two waves per 64 splats (splat_step_split) unless A/B knob 34 = 1 or
-    // another workgroup size
     // (1: the carry in the geometry wave; A/B knob 36 = 2: both waves project and
     // share its stores -- measured equal, 9.92-10.0 vs 9.85-9.98 us, not kept;
     // 3: the xyz elements on the colour wave)
+    // two waves per 64 splats (splat_step_split) unless A/B knob 34 = 1 or
+    // another workgroup size (nine lanes per splat, one per parameter element,
+    // was measured, round 6: 18.6 vs 10.5 us, profiles/r06/splat_elem/)
     P.split = sb == 256 && knob(34) != 1 ? 1 : 0;
     const int per_block = P.split ? sb / 2 : sb;
     const int blocks = (num_points > 0 ? ceil_div(num_points, per_block) : 0) + 1;

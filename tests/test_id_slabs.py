@@ -1,5 +1,7 @@
 """GPU suite: the single-frame render over 4-byte id slabs (the product
-default for sparse frames) against the render over 48-byte
+default for sparse frames; raster_render_ids_kernel, two
+one-tile waves per workgroup, against the generic kernel: A/B knob 38 = 1)
+against the render over 48-byte
 slab records (A/B knob 24 = 1, diagnostic library) and the banded kernel
 (knob 0 = 2, records).  Same entries per tile, same id order, same blend: the
 images must be bit-identical, including tiles past 256 entries (the id
@@ -34,6 +36,7 @@ def _frame(n, seed, chol, dev, cluster=0.0):
     (20000, 360, 640, 1.0, 0.2),   # tiles past 256 entries
     (20000, 360, 640, 1.0, 0.03),  # past 256 but within the record slabs' overflow ids (1024)
     (3000, 250, 333, 1.0, 0.0),    # ragged edge tiles
+    (3000, 200, 300, 1.0, 0.0),    # an odd tile count (247): the last two-tile workgroup's second wave idle
     (500, 128, 128, 0.0, 0.0),     # L = 0 (no bound): no intersections, the background
 ])
 def test_id_slab_render_bit_identical(cuda, oracle, n, H, W, chol, cluster):
@@ -43,8 +46,9 @@ def test_id_slab_render_bit_identical(cuda, oracle, n, H, W, chol, cluster):
     bg = torch.tensor([0.3, 0.6, 0.9], device=cuda)
     ref = [render_frame_sum(xyz, c, f, H, W, bg, cholesky_bound=bound) for _ in range(2)]
     got = []
-    # records; banded; the order at any density
-    for pair in ((24, 1), (0, 2), (27, 1)):
+    # records; banded; the order at any density; the generic one-wave kernel
+    # instead of raster_render_ids_kernel
+    for pair in ((24, 1), (0, 2), (27, 1), (38, 1)):
         with knobs(pair):
             got += [render_frame_sum(xyz, c, f, H, W, bg, cholesky_bound=bound) for _ in range(3)]
     torch.cuda.synchronize()
@@ -84,7 +88,7 @@ def test_needle_splats_every_route(cuda, oracle):
     bg = torch.tensor([0.3, 0.6, 0.9], device=cuda)
     ref = render_frame_sum(xyz, c, f, H, W, bg, cholesky_bound=bound)
     got = []
-    for pair in ((24, 1), (0, 2), (0, 1)):  # records; banded; sparse records
+    for pair in ((24, 1), (0, 2), (0, 1), (38, 1)):  # records; banded; sparse records; generic kernel
         with knobs(pair):
             got.append(render_frame_sum(xyz, c, f, H, W, bg, cholesky_bound=bound))
     torch.cuda.synchronize()

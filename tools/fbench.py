@@ -49,6 +49,9 @@ def main():
                     help="also run the timestamped one-wave kernel (mode 7) and print phases")
     ap.add_argument("--stamps-out", default=None,
                     help="with --stamps: save the raw per-tile stamps (us) and entry counts (npz)")
+    ap.add_argument("--id-stamps", default=None, const="-", nargs="?",
+                    help="stamp the production id-slab composite (knob 39) and print its phases "
+                         "by entry count; optional npz path for the raw stamps")
     ap.add_argument("--proj-stamps", action="store_true",
                     help="also stamp the projection kernel's waves (knob 5) and print phases")
     args = ap.parse_args()
@@ -175,6 +178,38 @@ def main():
                 counts = (bins[:, 1] - bins[:, 0]).clamp(min=0).cpu().numpy()
                 np.savez_compressed(args.stamps_out, stamps_us=t - t0, counts=counts,
                                     tbx=tbs[0], tby=tbs[1])
+        if args.id_stamps:
+            import numpy as np
+            ntiles = ((W + 15) // 16) * ((H + 15) // 16)
+            st = torch.zeros((ntiles, 8), dtype=torch.int64, device=dev)
+            lib.gsvc_debug_set_ptr(ctypes.c_void_p(st.data_ptr()))
+            lib.gsvc_debug_set(39, 1)
+            for _ in range(5):
+                frame()
+            torch.cuda.synchronize()
+            lib.gsvc_debug_set(39, 0)
+            lib.gsvc_debug_set_ptr(None)
+            raw = st.cpu().numpy()
+            cnt = raw[:, 5].copy()
+            t = raw[:, :5].astype(np.float64) * 0.01  # 100 MHz ticks -> us
+            t0 = t[:, 0].min()
+            q = lambda x: [round(float(np.percentile(x, p)), 2) for p in (0, 10, 50, 90, 99, 100)]  # noqa
+            # a phase a tile skips (no entries: no ids / staging stamps) reads 0
+            ok = (t[:, 1] > 0) & (t[:, 2] > 0)
+            print(json.dumps(dict(N=n, id_stamps="percentiles 0/10/50/90/99/100 (us)",
+                                  tiles=int(ntiles), staged_tiles=int(ok.sum()),
+                                  start=q(t[:, 0] - t0),
+                                  ids=q((t[ok, 1] - t[ok, 0])), records=q(t[ok, 2] - t[ok, 1]),
+                                  blend=q(t[ok, 3] - t[ok, 2]), drain=q(t[:, 4] - t[:, 3]),
+                                  end=q(t[:, 4] - t0))), flush=True)
+            end = t[:, 4] - t0
+            for lo, hi in ((0, 0), (1, 4), (5, 16), (17, 64), (65, 256), (257, 1 << 30)):
+                m = (cnt >= lo) & (cnt <= hi)
+                if m.any():
+                    print(json.dumps(dict(count=[lo, hi], tiles=int(m.sum()),
+                                          start=q(t[m, 0] - t0), end=q(end[m]))), flush=True)
+            if args.id_stamps != "-":
+                np.savez_compressed(args.id_stamps, stamps_us=t - t0, counts=cnt)
         if args.proj_stamps:
             import numpy as np
             waves = (n + 63) // 64

@@ -23,6 +23,7 @@ import os
 from collections import defaultdict
 
 KERNELS = {"raster_sum_fwd_kernel": "rasterize_sum_forward",
+           "raster_render_ids_kernel": "rasterize_sum_forward",
            "frame_project_ordered_kernel": "frame_project_ordered",
            "train_tile_wave_kernel": "train_tile",
            "train_tile_band_kernel": "train_tile",
