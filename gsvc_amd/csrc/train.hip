@@ -63,7 +63,8 @@ struct TrainTileArgs {
                       // blending, 8 no backward pixel work, 16 no run sums, 32 no atomics;
                       // 64 (A/B, exact): items in entry order, not longest first;
                       // 128 (A/B, exact): the carried candidates ranked by a
-                      // readlane loop instead of LDS broadcast reads
+                      // readlane loop instead of LDS broadcast reads; 256 no v_out
+                      // reads (wrong)
     float *out;       // optional [3, H, W] clamped render
     long long *stamps;  // diagnostic: int64[ntiles][8]
     // GSVC_TRAIN_DETERMINISTIC (band kernel): the (splat, tile) sums go to
@@ -1256,10 +1257,17 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                             s2 = fmaf(vdx, dx, s2);
                         }
                     };
-                    if (bcut)
+                    // (pixel PAIRS with packed math -- 3 two-word LDS reads, 2 exps
+                    // and ~23 VALU per pair instead of ~34 per two pixels -- were
+                    // measured, round 6: 49.8 vs 45.9 us per tile-kernel launch in
+                    // bench.py, product libraries swapped on one box; 64 VGPRs with
+                    // 60-72 B of spills, or 72 VGPRs at 7 waves per SIMD: 48.2;
+                    // profiles/r06/tile_pairs/)
+                    if (bcut) {
                         walk(std::true_type{});
-                    else
+                    } else {
                         walk(std::false_type{});
+                    }
                     const float hdy = 0.5f * dy;
                     g[0] = fmaf(2.0f * eha, s1, bdy * s0);
                     g[1] = fmaf(eb, s1, ((2.0f * C.x) * dy) * s0);

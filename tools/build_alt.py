@@ -25,6 +25,9 @@ def main():
     ap.add_argument("name")
     ap.add_argument("--ref", default=None, help="git ref of gsvc_amd/csrc and include/ (default: working tree)")
     ap.add_argument("--define", action="append", default=[])
+    ap.add_argument("--product", action="store_true",
+                    help="the product library (no -DGSVC_DIAG) as alt/NAME/libgsvc_amd.so, for "
+                         "tools/ab_product.sh (bench.py with the library swapped)")
     a = ap.parse_args()
     out = os.path.join(REPO, "gsvc_amd", "lib", "alt", a.name)
     os.makedirs(out, exist_ok=True)
@@ -42,15 +45,16 @@ def main():
         objs = []
         for f in sorted(glob.glob(os.path.join(csrc, "*.hip"))):
             o = os.path.join(tmp, os.path.basename(f) + ".o")
-            cmd = [B.HIPCC, *B.FLAGS, "-DGSVC_DIAG", *a.define, f"-I{os.path.join(src, 'include')}",
+            cmd = [B.HIPCC, *B.FLAGS, *([] if a.product else ["-DGSVC_DIAG"]), *a.define, f"-I{os.path.join(src, 'include')}",
                    "-c", f, "-o", o]
             r = subprocess.run(cmd, capture_output=True, text=True)
             if r.returncode:
                 sys.exit(f"hipcc failed for {f}:\n{r.stderr}")
             objs.append(o)
-        lib = os.path.join(out, "libgsvc_amd_diag.so")
+        name = "libgsvc_amd.so" if a.product else "libgsvc_amd_diag.so"
+        lib = os.path.join(out, name)
         subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC",
-                        "-Wl,-soname,libgsvc_amd_diag.so", "-o", lib, *objs], check=True)
+                        f"-Wl,-soname,{name}", "-o", lib, *objs], check=True)
     print(lib)
 
 
