@@ -1181,6 +1181,9 @@ __global__ __launch_bounds__(kSBThreads, 8) void raster_sum_bwd_kernel(
                             const float vis = exp_neg(sgm);
                             float al;
                             if constexpr (decltype(kcut)::value) {
+                                // (the training tile kernel's select in place of this
+                                // branch was measured here, round 6: 41.8-42.3 vs
+                                // 41.2-41.3 us, profiles/r06/select_cut/op_*; not kept)
                                 if (__float_as_uint(sgm) > kSigmaCutBits) continue;
                                 al = vis;  // opacity 1
                             } else {
