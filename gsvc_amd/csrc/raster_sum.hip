@@ -717,7 +717,10 @@ __device__ __forceinline__ void write_sorted_ids(const SumFwdArgs &A, int tile, 
 }
 
 // kModeSparse launches 64-thread workgroups (one wave per tile); every other
-// mode 128-thread workgroups (two waves per tile).
+// mode 128-thread workgroups (two waves per tile).  (Two one-tile waves per
+// workgroup, as raster_render_ids_kernel, measured for the op path's
+// kModeSparseIds, round 6: 24.6-25.1 vs 24.3-24.5 us; not kept,
+// profiles/r06/generic_w2/.)
 // kIdx: final_idx is written (the autograd forward); the render paths launch
 // the kIdx = false instance, which tracks no indices.
 // (2 and 4 one-tile waves per workgroup were measured, round 5: within +-2 %,

@@ -13,6 +13,7 @@
 #   pmc_valu TAG                       VALU / LDS / SALU / VMEM instruction counts of
 #                                      the trained composite and training tile kernel
 #   pmc_sq TAG                         SQ busy / wait / LDS-conflict cycles of the same
+#   pmc_final TAG                      both, for train50k and render10k -> pmc_valu.json
 #   ablate TAG "bits" [tbench args]    training tile kernel diagnostic bits (knob 13)
 #                                      on frozen trained-density steps
 #   fbench_ab TAG [fbench args]        composite A/B by fbench + kernel trace
@@ -105,6 +106,14 @@ for sub in ("sqa", "sqb"):
 print(json.dumps({k: {c: round(sum(v[-50:]) / len(v[-50:])) for c, v in d.items()} for k, d in by.items()}, indent=1))
 PY
   ;;
+pmc_final)
+  # the round's instruction counters (VALU / SALU / LDS / VMEM and the SQ wait
+  # buckets) of the tile kernels on the bench's workloads; merged locally by
+  # tools/pmc_merge.py gpurun_out/TAG > profiles/pmc_valu.json (bench.py reads it)
+  for wl in train50k render10k; do
+    pmc "$wl/valu" SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE -- python3 tools/pmc_workloads.py $wl
+    pmc "$wl/sq" SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_SMEM -- python3 tools/pmc_workloads.py $wl
+  done ;;
 ablate)
   BITS=${1:-"0 1 2 4 8 16 32 6"}; shift
   for b in $BITS; do
