@@ -3,8 +3,8 @@
 
   train50k   GaussianVideoFrame at 1920x1080 / 50k splats: --settle training
              iterations, then --iters more (the bench's trained state), then
-             --iters renders of the trained model (configs[2] render);
-  render10k  --iters renders of a random-init 10k-splat frame (configs[1]);
+             --warm + --iters renders of the trained model (configs[2] render);
+  render10k  --warm + --iters renders of a random-init 10k-splat frame (configs[1]);
   decode8    --iters batched renders of a GOP of 8 distinct 10k-splat frame
              models (bench.py ``video_decode``: one gsvc_render_frames_sum call);
   oppath     train50k's trained state, then --iters forward + backward calls of
@@ -30,6 +30,10 @@ def main():
     ap.add_argument("mode", choices=["train50k", "render10k", "decode8", "oppath", "alpha50k"])
     ap.add_argument("--settle", type=int, default=2000)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--warm", type=int, default=200,
+                    help="renders before the --iters summarised ones (bench.py times its renders "
+                         "after warm-up; the first calls include the unordered projection and a "
+                         "cold clock)")
     a = ap.parse_args()
     from gsvc_amd.frame import make_frame_model, synthetic_gt
     dev = torch.device("cuda:0")
@@ -89,7 +93,7 @@ def main():
         model = make_frame_model(H, W, 10000, dev, seed=1000)
         model.eval()
     with torch.no_grad():
-        for _ in range(a.iters):
+        for _ in range(a.warm + a.iters):
             model()
     torch.cuda.synchronize()
     print("done", a.mode, flush=True)
