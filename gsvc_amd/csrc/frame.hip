@@ -229,7 +229,8 @@ __global__ __launch_bounds__(kProjThreads) void frame_project_ordered_kernel(
     // ids in place of records: the carried bins' candidate lists, or the
     // render's id slabs (both 256 slots per tile)
     const int hits = slab_insert_window(S, x0, y0, x1, y1, tbx, tby, counts, slab, s_cnt, s_box, st,
-                                        carry_ids ? carry_ids : id_slab, kCarryCap,
+                                        carry_ids ? carry_ids : id_slab,
+                                        carry_ids ? kTrainCarryCap : kCarryCap,
                                         carry_ids || id_slab ? nullptr : ovf);
     if (kStamp) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

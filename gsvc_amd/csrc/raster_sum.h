@@ -8,8 +8,13 @@ namespace gsvc {
 // Output layouts: kLayoutHWC is the reference's [H, W, 3] image (+ final_idx);
 // kLayoutCHWClamped writes torch.clamp(img, 0, 1) as planes [3, H, W], i.e. the
 // epilogue of GaussianSplats_Represent.py:88-89 (clamp, view, permute,
-// contiguous) fused into the store.
-enum { kLayoutHWC = 0, kLayoutCHWClamped = 1 };
+// contiguous) fused into the store; kLayoutCHW the same planes unclamped (the op
+// path's [H, W, 3] image with strides (W, 1, H*W): GSVC's clamp + permute +
+// contiguous then read it without a copy).
+enum { kLayoutHWC = 0, kLayoutCHWClamped = 1, kLayoutCHW = 2 };
+__host__ __device__ inline bool layout_planes(int layout) {
+    return layout == kLayoutCHWClamped || layout == kLayoutCHW;
+}
 
 struct SumFwdArgs {
     int tbx, img_w, img_h, ntiles, sparse_max, layout;

@@ -254,6 +254,11 @@ __device__ __forceinline__ float clamp01(float x) {
     return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x);
 }
 
+// A plane value: clamped for the render's layout, as blended for the op path's
+__device__ __forceinline__ float plane_val(const SumFwdArgs &A, float x) {
+    return A.layout == kLayoutCHWClamped ? clamp01(x) : x;
+}
+
 // A tile's first pixel coordinate as a float, converted where it is used (the
 // asm keeps the compiler from hoisting the conversion to the kernel entry and
 // holding -- and, at 64 VGPRs, spilling -- the value across the blend loops).
@@ -282,11 +287,11 @@ __device__ __forceinline__ void load_splat(const SumFwdArgs &A, int g, float4 &g
 // Scalar store of one pixel in either layout.
 __device__ __forceinline__ void store_pixel(const SumFwdArgs &A, size_t p, float r, float g, float b,
                                             int l) {
-    if (A.layout == kLayoutCHWClamped) {
+    if (layout_planes(A.layout)) {
         const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
-        A.out[p] = clamp01(r);
-        A.out[hw + p] = clamp01(g);
-        A.out[2 * hw + p] = clamp01(b);
+        A.out[p] = plane_val(A, r);
+        A.out[hw + p] = plane_val(A, g);
+        A.out[2 * hw + p] = plane_val(A, b);
     } else {
         A.out[3 * p] = r;
         A.out[3 * p + 1] = g;
@@ -478,14 +483,16 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
     const float r0 = ar01.x, r1 = ar01.y, r2 = ar23.x, r3 = ar23.y;
     const float g0 = ag01.x, g1 = ag01.y, g2 = ag23.x, g3 = ag23.y;
     const float b0 = ab01.x, b1 = ab01.y, b2 = ab23.x, b3 = ab23.y;
-    if (A.layout == kLayoutCHWClamped && A.vec_chw && (tx + 1) * kTile <= A.img_w) {
+    if (layout_planes(A.layout) && A.vec_chw && (tx + 1) * kTile <= A.img_w) {
         // 4 lanes write a 64-byte row segment of each plane
         if (pi < A.img_h && !(kDiag && (A.ablate & 2))) {
             const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
             float *o = A.out + (size_t)pi * (size_t)A.img_w + (size_t)pj;
-            st_f4(o, clamp01(r0), clamp01(r1), clamp01(r2), clamp01(r3), A.store_policy);
-            st_f4(o + hw, clamp01(g0), clamp01(g1), clamp01(g2), clamp01(g3), A.store_policy);
-            st_f4(o + 2 * hw, clamp01(b0), clamp01(b1), clamp01(b2), clamp01(b3), A.store_policy);
+            st_f4(o, plane_val(A, r0), plane_val(A, r1), plane_val(A, r2), plane_val(A, r3), A.store_policy);
+            st_f4(o + hw, plane_val(A, g0), plane_val(A, g1), plane_val(A, g2), plane_val(A, g3),
+                  A.store_policy);
+            st_f4(o + 2 * hw, plane_val(A, b0), plane_val(A, b1), plane_val(A, b2), plane_val(A, b3),
+                  A.store_policy);
             if (A.final_idx)
                 *reinterpret_cast<int4 *>(A.final_idx + (o - A.out)) = make_int4(l0, l1, l2, l3);
         }
@@ -658,13 +665,13 @@ __device__ __forceinline__ void sum_fwd_band(const SumFwdArgs &A, int tile, int 
                      "v"(l1));
         return;
     }
-    if (A.layout == kLayoutCHWClamped && A.vec_chw && (tx + 1) * kTile <= A.img_w) {
+    if (layout_planes(A.layout) && A.vec_chw && (tx + 1) * kTile <= A.img_w) {
         if (pi < A.img_h) {
             const size_t hw = (size_t)A.img_w * (size_t)A.img_h;
             float *o = A.out + (size_t)pi * (size_t)A.img_w + (size_t)pj;
-            st_f2(o, clamp01(ar.x), clamp01(ar.y), A.store_policy);
-            st_f2(o + hw, clamp01(ag.x), clamp01(ag.y), A.store_policy);
-            st_f2(o + 2 * hw, clamp01(ab.x), clamp01(ab.y), A.store_policy);
+            st_f2(o, plane_val(A, ar.x), plane_val(A, ar.y), A.store_policy);
+            st_f2(o + hw, plane_val(A, ag.x), plane_val(A, ag.y), A.store_policy);
+            st_f2(o + 2 * hw, plane_val(A, ab.x), plane_val(A, ab.y), A.store_policy);
             if (A.final_idx) *reinterpret_cast<int2 *>(A.final_idx + (o - A.out)) = make_int2(l0, l1);
         }
         return;
@@ -1693,7 +1700,7 @@ extern "C" int gsvc_rasterize_sum_forward_ex(
     (void)tbz; (void)block_z; (void)img_depth;
     int rc = check_tiles("rasterize_sum_forward", block_x, block_y, tbx, tby, img_width, img_height);
     if (rc) return rc;
-    if (out_layout != kLayoutHWC && out_layout != kLayoutCHWClamped)
+    if (out_layout != kLayoutHWC && !layout_planes(out_layout))
         return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: unknown output layout %d", out_layout);
     if (num_intersects_dev && !background)
         return set_error(GSVC_ERR_ARG, "rasterize_sum_forward: background required with a device count");
@@ -1795,7 +1802,7 @@ static int forward_slabs_impl(
     A.img_w = (int)img_width;
     A.img_h = (int)img_height;
     A.ntiles = ntiles;
-    A.layout = kLayoutHWC;
+    A.layout = (order_flags & GSVC_SLABS_PLANES) ? kLayoutCHW : kLayoutHWC;
     A.m_dev = m_slots + par;
     A.meta_out = meta;
     A.bg = background;
@@ -1847,7 +1854,7 @@ extern "C" int gsvc_rasterize_sum_forward_slabs_ordered(
     int *gaussian_ids, int *tile_bins, int *meta, float *grad_records_zero, float *out_img,
     int *final_idx, void *stream, void *order_workspace, size_t order_workspace_bytes,
     int order_flags) {
-    if (order_flags & ~(GSVC_TRAIN_ORDER | GSVC_TRAIN_ORDER_REFRESH | GSVC_SLABS_WIDE))
+    if (order_flags & ~(GSVC_TRAIN_ORDER | GSVC_TRAIN_ORDER_REFRESH | GSVC_SLABS_WIDE | GSVC_SLABS_PLANES))
         return set_error(GSVC_ERR_ARG, "rasterize_sum_forward_slabs_ordered: unknown flags");
     if ((order_flags & (GSVC_TRAIN_ORDER | GSVC_TRAIN_ORDER_REFRESH)) && !order_workspace)
         return set_error(GSVC_ERR_WORKSPACE, "rasterize_sum_forward_slabs_ordered: no order workspace");

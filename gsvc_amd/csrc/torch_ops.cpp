@@ -252,6 +252,20 @@ void slab_ws_ready(SlabWs &w, const Tensor &like, int ntiles) {
     }
 }
 
+// The op path's image as channel planes (GSVC_SLABS_PLANES): out_img is the
+// [H, W, 3] image with strides (W, 1, H*W).  GSVC's epilogue -- clamp, view(-1,
+// H, W, 3), permute(0, 3, 1, 2), contiguous (GaussianSplats_Represent.py:88-89,
+// GaussianSplats_Compress.py:68,82,162,177) -- then finds its NCHW result
+// already contiguous (no 25 MB copy per 1080p forward), and the backward's
+// gradient arrives in the same planes.  Values are the reference's; only the
+// strides differ, so a caller that views the image as (-1, 3) needs
+// .contiguous() first.  GSVC_OP_PLANAR=0 returns the contiguous [H, W, 3]
+// (read per call, so a process can switch).
+bool op_planar_enabled() {
+    const char *e = std::getenv("GSVC_OP_PLANAR");
+    return !(e && e[0] == '0');
+}
+
 bool capturing(void *stream) {
     if (stream == nullptr) return false;  // the legacy default stream never captures (errors.hip)
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -288,7 +302,9 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
         Tensor bins = at::empty({nt, 2}, i);
         // no final_idx: the backward (raster_sum_bwd_kernel) does not read it --
         // an entry past a pixel's final index fails the alpha test there anyway
-        Tensor meta = at::empty({2}, i), out = at::empty({H, W, 3}, f);
+        const bool planar = op_planar_enabled();
+        Tensor meta = at::empty({2}, i);
+        Tensor out = planar ? at::empty({3, H, W}, f).permute({1, 2, 0}) : at::empty({H, W, 3}, f);
         Tensor rec;
         if (capture) {
             // Graph capture: the slab workspace's parity is host state a replay
@@ -309,7 +325,8 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
             check(gsvc_rasterize_sum_forward_ex(tbx, tby, 1, 16, 16, 1, (unsigned)W, (unsigned)H, 1,
                                                 ip(gids), ip(bins), fp(xys), fp(conics), fp(colors),
                                                 fp(opacity), fp(background), ip(meta),
-                                                hint_cached(xys.device().index()), 0, fp(out),
+                                                hint_cached(xys.device().index()), planar ? 2 : 0,
+                                                fp(out),
                                                 nullptr, nullptr, st),
                   "gsvc_rasterize_sum_forward_ex");
         } else {
@@ -324,7 +341,7 @@ struct RasterSumFn : public torch::autograd::Function<RasterSumFn> {
                 (unsigned)H, (unsigned)W, ws.calls, hint, ws.buf.data_ptr(),
                 4 * (size_t)ws.buf.numel(), ip(gids), ip(bins), ip(meta), fp(rec), fp(out), nullptr,
                 st, oflags ? ws.order.data_ptr() : nullptr, oflags ? (size_t)ws.order.numel() : 0,
-                oflags | GSVC_SLABS_WIDE);
+                oflags | GSVC_SLABS_WIDE | (planar ? GSVC_SLABS_PLANES : 0));
             if (rc != 0) ws.tiles = -1;  // counters and order in an unknown state: rebuild
             check(rc, "gsvc_rasterize_sum_forward_slabs_ordered");
             ++ws.calls;

@@ -605,7 +605,7 @@ __device__ __forceinline__ void publish_loss(const float2 *err, int ntiles, doub
 }
 
 
-// Carried bins of a tile with 256 < n <= kCarryCap candidates (wave 0): the
+// Carried bins of a tile with 256 < n <= kTrainCarryCap candidates (wave 0): the
 // ascending ids of the candidates whose current box holds the tile -- the
 // first <= 256 members -- into s_out, by the id-window bitmap (tile_ids.h).
 // Ids are unique within a tile's candidates.  Per lane a mask of which of its
@@ -614,9 +614,10 @@ __device__ __forceinline__ void publish_loss(const float2 *err, int ntiles, doub
 __device__ int wave_sorted_members(const int *cand, int n, const uint2 *cbox, unsigned tx,
                                    unsigned ty, int *s_out, unsigned *bm) {
     const int lane = threadIdx.x & 63;
-    constexpr int kRows = kCarryCap / 64, kQ = 4;
-    n = min(n, kCarryCap);
-    unsigned mem = 0u;
+    constexpr int kRows = kTrainCarryCap / 64, kQ = 4;
+    static_assert(kRows <= 64, "one membership bit per row in a 64-bit mask");
+    n = min(n, kTrainCarryCap);
+    unsigned long long mem = 0ull;
     int lo = 0x7fffffff, hi = -1;
     for (int k0 = 0; k0 < kRows && 64 * k0 < n; k0 += kQ) {
         int id[kQ];
@@ -628,7 +629,7 @@ __device__ int wave_sorted_members(const int *cand, int n, const uint2 *cbox, un
 #pragma unroll
         for (int q = 0; q < kQ; ++q) {
             if (lane + 64 * (k0 + q) < n && box_has(b[q], tx, ty)) {
-                mem |= 1u << (k0 + q);
+                mem |= 1ull << (k0 + q);
                 lo = min(lo, id[q]);
                 hi = max(hi, id[q]);
             }
@@ -648,7 +649,7 @@ __device__ int wave_sorted_members(const int *cand, int n, const uint2 *cbox, un
             for (int q = 0; q < kQ; ++q) id[q] = cand[min(lane + 64 * (k0 + q), n - 1)];
 #pragma unroll
             for (int q = 0; q < kQ; ++q)
-                if ((mem >> (k0 + q)) & 1u) bitmap_set(bm, (long long)id[q] - base);
+                if ((mem >> (k0 + q)) & 1ull) bitmap_set(bm, (long long)id[q] - base);
         }
         wave_lds_sync();
         written = bitmap_emit(bm, base, written, s_out);
@@ -717,7 +718,7 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
     const unsigned srt_raw = kCarry && A.csorted ? A.csorted[tile] : 0u;
     float4 r0, r1, r2;
     int cid = 0;  // carried bins: the lane's candidate id
-    int *tcids = carry ? A.cids + (size_t)tile * kCarryCap : nullptr;
+    int *tcids = carry ? A.cids + (size_t)tile * kTrainCarryCap : nullptr;
     if (carry) {
         cid = tcids[tid < spec_of(A) ? tid : 0];
     } else {
@@ -838,10 +839,10 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
         }
     } else if (brute) {
         if (w == 0) {
-            // carried bins of <= kCarryCap candidates: the members sorted from
-            // the list (the bbox rebuild over every splat costs ~0.6 ms)
+            // carried bins of <= kTrainCarryCap candidates: the members sorted
+            // from the list (the bbox rebuild over every splat costs ~0.6 ms)
             unsigned *bm = reinterpret_cast<unsigned *>(&S.part[4][0]);
-            if (carry && n_all <= kCarryCap) {
+            if (carry && n_all <= kTrainCarryCap) {
                 n = wave_sorted_members(tcids, n_all, A.cbox, (unsigned)tx, (unsigned)ty, s_key, bm);
             } else if (!carry && A.ovf && n_all <= kCarryCap) {
                 // record slab + its overflow ids: the first 256 ids sorted from both
@@ -1430,7 +1431,7 @@ __device__ __forceinline__ int carry_splat(const TrainSplatArgs &A, int i, const
                 if (hv && x >= hx0 && x < hx1 && y >= hy0 && y < hy1) continue;
                 const unsigned t = y * (unsigned)A.tbx + x;
                 const unsigned sl = atomicAdd(A.ccount + t, 1u);
-                if (sl < (unsigned)kCarryCap) A.cids[(size_t)t * kCarryCap + sl] = i;
+                if (sl < (unsigned)kTrainCarryCap) A.cids[(size_t)t * kTrainCarryCap + sl] = i;
             }
         A.chull[i] = pack_box(ux0, uy0, ux1, uy1);
     }
@@ -1893,7 +1894,7 @@ static TrainWs train_ws(char *base, int n, int ntiles) {
     };
     w.grad = (float4 *)take(sizeof(float4) * 4 * nn);
     w.err = (float2 *)take(sizeof(float2) * nt);
-    w.cids = (int *)take(sizeof(int) * kCarryCap * nt);
+    w.cids = (int *)take(sizeof(int) * kTrainCarryCap * nt);
     w.ccount = (unsigned *)take(sizeof(unsigned) * 2 * nt);  // ccount[T], csorted[T]
     w.csorted = w.ccount ? w.ccount + nt : nullptr;
     w.cbox = (uint2 *)take(sizeof(uint2) * nn);

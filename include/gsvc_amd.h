@@ -275,6 +275,8 @@ int gsvc_rasterize_sum_forward(
  *   out_layout          0: out_img [H,W,3] as the reference;
  *                       1: out_img [3,H,W] = torch.clamp(img, 0, 1) permuted,
  *                       the caller epilogue of GaussianSplats_Represent.py:88-89;
+ *                       2: out_img as channel planes [3,H,W], unclamped: the
+ *                       [H,W,3] image with strides (W, 1, H*W) (GSVC_SLABS_PLANES);
  *   final_idx, final_Ts may be NULL (not written). */
 int gsvc_rasterize_sum_forward_ex(
     int tile_bounds_x, int tile_bounds_y, int tile_bounds_z,
@@ -321,9 +323,14 @@ int gsvc_rasterize_sum_forward_slabs(
  * or without an order): gaussian_ids holds GSVC_SLABS_WIDE_IDS ids per tile
  * ([T * 1024], tile t's at t * 1024, tile_bins [t * 1024, t * 1024 + n)): a
  * tile of up to 1024 entries sorts its first 256 from its slab instead of
- * rebuilding them from every splat's bbox (dense content).  Not part of the
- * reference. */
+ * rebuilding them from every splat's bbox (dense content).  order_flags
+ * GSVC_SLABS_PLANES: out_img is written as channel planes [3, H, W] (unclamped;
+ * the same values as the [H, W, 3] image, element (i, j, c) at c*H*W + i*W + j)
+ * -- the layout GSVC's own epilogue (clamp, view, permute(0, 3, 1, 2),
+ * contiguous; GaussianSplats_Represent.py:88-89) reads without a copy.  Not
+ * part of the reference. */
 #define GSVC_SLABS_WIDE 0x80000
+#define GSVC_SLABS_PLANES 0x100000
 #define GSVC_SLABS_WIDE_IDS 1024
 size_t gsvc_rasterize_sum_order_workspace_bytes(int num_points);
 int gsvc_rasterize_sum_forward_slabs_ordered(

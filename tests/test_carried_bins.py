@@ -62,13 +62,15 @@ def test_carried_equals_reprojected_through_rebuilds(cuda, deterministic):
     _same(_run(cuda, True, 256, 256, 2000, 70), _run(cuda, False, 256, 256, 2000, 70))
 
 
-@pytest.mark.parametrize("every", [4, 12])
+@pytest.mark.parametrize("every", [1, 2, 4, 12])
 def test_carried_fast_motion_and_overflow(cuda, deterministic, every):
     """lr 0.05: splats jump tiles every step (many appends, hulls growing
-    across the image); every 4th of 6000 splats piled on one spot overflows
-    that tile's kCarryCap = 1024 candidates (the bbox rebuild path), every 12th
-    (500) passes 256 but not 1024 (the members sorted from the candidate list,
-    train.hip wave_sorted_members); no rebuild for 40 steps."""
+    across the image); all 6000 splats piled on one spot overflow that tile's
+    kTrainCarryCap = 4096 candidates (the bbox rebuild path); every 2nd (3000)
+    and every 4th (1500) pass round 5's 1024 but not 4096, every 12th (500)
+    passes 256 -- the members sorted from the candidate list
+    (train.hip wave_sorted_members), against the re-projected steps whose
+    record slabs rebuild past 1024; no rebuild for 40 steps."""
     def pile(m):
         with torch.no_grad():
             sel = torch.arange(0, m._xyz.shape[0], every, device=m._xyz.device)
@@ -143,3 +145,49 @@ def test_carried_bins_through_prune_and_densify(cuda, deterministic, tmp_path):
             T.CARRY_BINS = old
     a, b = ([(r["num_gaussians"], r["psnr"]) for r in x["frames"]] for x in out)
     assert a == b
+
+
+def test_dense_tiles_past_1024_match_oracle(cuda, oracle, deterministic):
+    """VERDICT r5 item 8 at 1080p: 20000 splats of which 3000 sit on one 5-px
+    spot -- a few tiles of ~3000 candidates, past round 5's 1024 and inside
+    kTrainCarryCap -- so the fused step sorts those tiles' members from the
+    carried lists instead of scanning every splat's bbox.  The first step's loss
+    (the forward: each tile's first 256 entries by id, the reference's
+    truncation) against the C oracle's train_iter_sum, the second step's
+    within the Adan-step envelope, and 6 carried steps bitwise equal to
+    re-projected ones (whose record slabs take the bbox rebuild past 1024)."""
+    import numpy as np
+    from gsvc_amd.frame import synthetic_gt
+    H, W, n, k = 1080, 1920, 20000, 3000
+
+    def pile(m):
+        with torch.no_grad():
+            sel = torch.linspace(0, n - 1, k, device=m._xyz.device).long()
+            g = torch.Generator(device=m._xyz.device).manual_seed(3)
+            m._xyz[sel] = torch.atanh(torch.full((k, 2), -0.25, device=m._xyz.device)
+                                      + 0.005 * torch.rand(k, 2, device=m._xyz.device, generator=g))
+            m._cholesky[sel] = torch.tensor([2.5, 0.3, 1.5], device=m._xyz.device)
+    a = _run(cuda, True, H, W, n, 6, edit=pile)
+    b = _run(cuda, False, H, W, n, 6, edit=pile)
+    _same(a, b)
+    # the oracle from the same initial parameters
+    from gsvc_amd.frame import make_frame_model
+    m0 = make_frame_model(H, W, n, cuda, seed=3)
+    pile(m0)
+    params = {kk: getattr(m0, kk).detach().cpu().numpy().copy()
+              for kk in ("_xyz", "_cholesky", "_features_dc")}
+    gt = synthetic_gt(H, W, 4, cuda).cpu().numpy().reshape(3, H, W)
+    oracle.set_threads(8)
+    try:
+        r = oracle.render_sum(np.tanh(params["_xyz"]).astype(np.float32),
+                              (params["_cholesky"] + np.array([0.5, 0.0, 0.5], np.float32)).astype(np.float32),
+                              params["_features_dc"], np.ones((n, 1), np.float32), H, W)
+        state = {}
+        out = [oracle.train_iter_sum(params, gt, H, W, state, s + 1) for s in range(2)]
+    finally:
+        oracle.set_threads(1)
+    per_tile = (r["bins"][:, 1] - r["bins"][:, 0]).max()
+    assert 1024 < per_tile <= 4096, per_tile
+    la = a[1]
+    assert abs(la[0] - out[0][0]) <= 2e-6 * out[0][0], (la[0], out[0][0])
+    assert abs(la[1] - out[1][0]) <= 1e-4 * out[1][0], (la[1], out[1][0])

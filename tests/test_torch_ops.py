@@ -72,6 +72,57 @@ def test_cpp_functions_match_python_functions(cuda, n, H, W, chol):
         assert float((a - b).abs().max()) <= 1e-5 * max(scale, 1e-30)
 
 
+def _gsvc_epilogue(out, H, W):
+    """GaussianSplats_Represent.py:88-89 as written."""
+    return torch.clamp(out, 0, 1).view(-1, H, W, 3).permute(0, 3, 1, 2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,H,W", [(4000, 256, 320), (300, 37, 53), (50000, 1080, 1920)])
+def test_cpp_function_planar_output(cuda, monkeypatch, n, H, W):
+    """GSVC_SLABS_PLANES (the default): the image as channel planes, strides
+    (W, 1, H*W) -- the same values bit for bit as the contiguous [H, W, 3]
+    route (GSVC_OP_PLANAR=0), GSVC's clamp + view + permute already contiguous
+    (its .contiguous() copies nothing), the M < 1 background in the same
+    layout, and the gradients through GSVC's epilogue and L2 loss equal within
+    the float atomics' order."""
+    from gsplat.project_gaussians_2d import project_gaussians_2d
+    from gsplat.rasterize_sum import rasterize_gaussians_sum
+    means, L, col = _inputs(n, H, W, 7 + n, cuda)
+    gt = torch.rand(1, 3, H, W, generator=torch.Generator().manual_seed(5)).to(cuda)
+    tb = ((W + 15) // 16, (H + 15) // 16, 1)
+
+    def go(planar, shift=0.0):
+        monkeypatch.setenv("GSVC_OP_PLANAR", "1" if planar else "0")
+        m = (means + shift).clone().requires_grad_(True)
+        l = L.clone().requires_grad_(True)
+        c = col.clone().requires_grad_(True)
+        o = torch.ones(n, 1, device=cuda)
+        xys, depths, radii, conics, nth = project_gaussians_2d(m, l, H, W, tb)
+        out = rasterize_gaussians_sum(xys, depths, radii, conics, nth, c, o, H, W, 16, 16,
+                                      background=torch.tensor([0.2, 0.5, 0.7], device=cuda))
+        img = _gsvc_epilogue(out, H, W)
+        contiguous_already = img.is_contiguous()
+        img = img.contiguous()
+        torch.nn.functional.mse_loss(img, gt).backward()
+        torch.cuda.synchronize()
+        return out.detach(), contiguous_already, (m.grad, l.grad, c.grad)
+
+    hwc, c0, g0 = go(False)
+    pl, c1, g1 = go(True)
+    assert hwc.is_contiguous() and not c0
+    assert pl.shape == (H, W, 3) and pl.stride() == (W, 1, H * W) and c1
+    assert torch.equal(pl, hwc)
+    for a, b in zip(g1, g0):
+        scale = float(b.abs().max())
+        assert float((a - b).abs().max()) <= 1e-5 * max(scale, 1e-30)
+    # every splat off-screen: M = 0, the background in both layouts
+    bg_h, _, _ = go(False, shift=50.0)
+    bg_p, _, _ = go(True, shift=50.0)
+    assert torch.equal(bg_p, bg_h)
+    assert torch.equal(bg_p[0, 0], torch.tensor([0.2, 0.5, 0.7], device=cuda))
+
+
 @pytest.mark.gpu
 def test_cpp_function_return_alpha_and_background(cuda):
     """return_alpha (1 - final_Ts: 0 with intersections) and the M < 1 branch

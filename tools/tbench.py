@@ -56,6 +56,10 @@ def main():
                     help="start from a saved model (tools/tile_counts.py --save, or a frame "
                          "exported from a video checkpoint: xyz, cholesky, features) against "
                          "frame FRAME of the textured synthetic video (dense content)")
+    ap.add_argument("--pile", type=int, default=0,
+                    help="move this many splats (evenly spread over the ids) onto one 5-px spot "
+                         "before the warmup: a few tiles with that many candidates (the carried "
+                         "lists' capacity cliff, train.hip kTrainCarryCap)")
     ap.add_argument("--channels", action="store_true",
                     help="also print HIP-event kernel averages (us) over 200 extra iterations")
     a = ap.parse_args()
@@ -90,6 +94,13 @@ def main():
         model = make_frame_model(H, W, a.splats, dev, seed=7,
                                  fused_train=False if a.op_by_op else None)
         gt = synthetic_gt(H, W, 8, dev)
+    if a.pile:
+        with torch.no_grad():
+            sel = torch.linspace(0, a.splats - 1, a.pile, device=dev).long()
+            g = torch.Generator(device=dev).manual_seed(3)
+            model._xyz[sel] = torch.atanh(torch.full((a.pile, 2), -0.25, device=dev)
+                                          + 0.005 * torch.rand(a.pile, 2, device=dev, generator=g))
+            model._cholesky[sel] = torch.tensor([2.5, 0.3, 1.5], device=dev)
     for it in range(1, a.warmup + 1):
         model.train_iter(gt, it)
     torch.cuda.synchronize()
