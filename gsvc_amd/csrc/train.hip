@@ -605,31 +605,35 @@ __device__ __forceinline__ void publish_loss(const float2 *err, int ntiles, doub
 }
 
 
-// Carried bins of a tile with 256 < n <= kTrainCarryCap candidates (wave 0): the
+// Carried bins of a tile with 256 < n <= kTrainCarryCap candidates (every
+// thread of the workgroup calls it; the same return value in each): the
 // ascending ids of the candidates whose current box holds the tile -- the
 // first <= 256 members -- into s_out, by the id-window bitmap (tile_ids.h).
-// Ids are unique within a tile's candidates.  Per lane a mask of which of its
-// candidates (lane + 64 k) are members; each window re-reads the candidate
-// ids (L2-resident) four rows at a time.
-__device__ int wave_sorted_members(const int *cand, int n, const uint2 *cbox, unsigned tx,
-                                   unsigned ty, int *s_out, unsigned *bm) {
-    const int lane = threadIdx.x & 63;
-    constexpr int kRows = kTrainCarryCap / 64, kQ = 4;
-    static_assert(kRows <= 64, "one membership bit per row in a 64-bit mask");
+// Ids are unique within a tile's candidates.  Thread t owns candidates
+// t + kBThreads k (a 32-bit mask of which are members); the gathers go 8 per
+// thread per round trip (ids, then their boxes), and each id window re-reads the
+// thread's ids 16 at a time (L2-resident).  Both waves set bits in the shared
+// bitmap, wave 0 emits.  ``s_misc``: 4 ints of scratch.
+template <int kThreads>
+__device__ int wg_sorted_members(const int *cand, int n, const uint2 *cbox, unsigned tx,
+                                 unsigned ty, int *s_out, unsigned *bm, int *s_misc) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr int kPer = kTrainCarryCap / kThreads, kQ = 4, kR = 4;
+    static_assert(kPer <= 32 && kPer % kQ == 0 && kPer % kR == 0, "membership mask layout");
     n = min(n, kTrainCarryCap);
-    unsigned long long mem = 0ull;
+    unsigned mem = 0u;
     int lo = 0x7fffffff, hi = -1;
-    for (int k0 = 0; k0 < kRows && 64 * k0 < n; k0 += kQ) {
+    for (int k0 = 0; k0 < kPer && kThreads * k0 < n; k0 += kQ) {
         int id[kQ];
         uint2 b[kQ];
 #pragma unroll
-        for (int q = 0; q < kQ; ++q) id[q] = cand[min(lane + 64 * (k0 + q), n - 1)];
+        for (int q = 0; q < kQ; ++q) id[q] = cand[min(tid + kThreads * (k0 + q), n - 1)];
 #pragma unroll
         for (int q = 0; q < kQ; ++q) b[q] = cbox[id[q]];
 #pragma unroll
         for (int q = 0; q < kQ; ++q) {
-            if (lane + 64 * (k0 + q) < n && box_has(b[q], tx, ty)) {
-                mem |= 1ull << (k0 + q);
+            if (tid + kThreads * (k0 + q) < n && box_has(b[q], tx, ty)) {
+                mem |= 1u << (k0 + q);
                 lo = min(lo, id[q]);
                 hi = max(hi, id[q]);
             }
@@ -640,19 +644,33 @@ __device__ int wave_sorted_members(const int *cand, int n, const uint2 *cbox, un
         lo = min(lo, __shfl_xor(lo, off, 64));
         hi = max(hi, __shfl_xor(hi, off, 64));
     }
+    if (lane == 0) {
+        s_misc[2 * w] = lo;
+        s_misc[2 * w + 1] = hi;
+    }
+    __syncthreads();
+    lo = min(s_misc[0], s_misc[2]);
+    hi = max(s_misc[1], s_misc[3]);
     int written = 0;
     for (long long base = lo; base <= hi && written < kTilePix; base += 32 * kSortWords) {
-        bitmap_clear(bm);
-        for (int k0 = 0; k0 < kRows && 64 * k0 < n; k0 += kQ) {
-            int id[kQ];
+        for (int k = tid; k < kSortWords; k += kThreads) bm[k] = 0u;
+        __syncthreads();
+        for (int k0 = 0; k0 < kPer && kThreads * k0 < n; k0 += kR) {
+            int id[kR];
 #pragma unroll
-            for (int q = 0; q < kQ; ++q) id[q] = cand[min(lane + 64 * (k0 + q), n - 1)];
+            for (int q = 0; q < kR; ++q) id[q] = cand[min(tid + kThreads * (k0 + q), n - 1)];
 #pragma unroll
-            for (int q = 0; q < kQ; ++q)
-                if ((mem >> (k0 + q)) & 1ull) bitmap_set(bm, (long long)id[q] - base);
+            for (int q = 0; q < kR; ++q)
+                if ((mem >> (k0 + q)) & 1u) bitmap_set(bm, (long long)id[q] - base);
         }
-        wave_lds_sync();
-        written = bitmap_emit(bm, base, written, s_out);
+        __syncthreads();
+        if (w == 0) {
+            written = bitmap_emit(bm, base, written, s_out);
+            if (lane == 0) s_misc[0] = written;
+        }
+        __syncthreads();
+        written = s_misc[0];
+        __syncthreads();  // (s_misc and the bitmap are rewritten by the next window)
     }
     return min(written, kTilePix);
 }
@@ -838,13 +856,16 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
             S.ro[rank] = ellipse_rect(r0.x, r0.y, 2.0f * r0.z, r0.w, 2.0f * r1.x, 1.0f, tx0, ty0);
         }
     } else if (brute) {
-        if (w == 0) {
+        unsigned *bm = reinterpret_cast<unsigned *>(&S.part[4][0]);
+        if (carry && n_all <= kTrainCarryCap) {
             // carried bins of <= kTrainCarryCap candidates: the members sorted
-            // from the list (the bbox rebuild over every splat costs ~0.6 ms)
-            unsigned *bm = reinterpret_cast<unsigned *>(&S.part[4][0]);
-            if (carry && n_all <= kTrainCarryCap) {
-                n = wave_sorted_members(tcids, n_all, A.cbox, (unsigned)tx, (unsigned)ty, s_key, bm);
-            } else if (!carry && A.ovf && n_all <= kCarryCap) {
+            // from the list by both waves (the bbox rebuild over every splat
+            // costs ~0.1-0.6 ms)
+            const int nm = wg_sorted_members<kBThreads>(tcids, n_all, A.cbox, (unsigned)tx,
+                                                        (unsigned)ty, s_key, bm, S.misc);
+            if (tid == 0) S.nsel = nm;
+        } else if (w == 0) {
+            if (!carry && A.ovf && n_all <= kCarryCap) {
                 // record slab + its overflow ids: the first 256 ids sorted from both
                 SegIds seg;
                 seg.ids = nullptr;

@@ -69,7 +69,7 @@ def test_carried_fast_motion_and_overflow(cuda, deterministic, every):
     kTrainCarryCap = 4096 candidates (the bbox rebuild path); every 2nd (3000)
     and every 4th (1500) pass round 5's 1024 but not 4096, every 12th (500)
     passes 256 -- the members sorted from the candidate list
-    (train.hip wave_sorted_members), against the re-projected steps whose
+    (train.hip wg_sorted_members), against the re-projected steps whose
     record slabs rebuild past 1024; no rebuild for 40 steps."""
     def pile(m):
         with torch.no_grad():
