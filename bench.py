@@ -581,20 +581,25 @@ def op_path_block(model, gt, device, steps=200, warmup=20):
     assert not op.fused_train and not op.fused_render
 
     def timed(fn, k, w):
-        # w calls and at least 50 ms of them: the first block timed after the
-        # model's setup otherwise caught the clocks still ramping (one box's
-        # forward read 159.8 us against 72.6 on the next, profiles/r06/final)
+        # w calls and at least 0.3 s of them, then the median of three blocks
+        # of k: right after the model's setup the host side ran slow for ~0.5 s
+        # (forward + backward 310-330 us, then 180-200, tools/planar_ab.py,
+        # profiles/r06/planar_op/), and one box's first forward block read
+        # 159.8 us against 72.6 on the next (profiles/r06/final)
         t_w = time.perf_counter()
-        for j in range(10 ** 6):
+        for j in range(10 ** 7):
             fn()
-            if j + 1 >= w and time.perf_counter() - t_w > 0.05:
+            if j + 1 >= w and time.perf_counter() - t_w > 0.3:
                 break
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(k):
-            fn()
-        torch.cuda.synchronize()
-        return (time.perf_counter() - t0) / k
+        blocks = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(k):
+                fn()
+            torch.cuda.synchronize()
+            blocks.append((time.perf_counter() - t0) / k)
+        return sorted(blocks)[1]
 
     def fwd():
         op.forward()
@@ -645,7 +650,8 @@ def op_path_block(model, gt, device, steps=200, warmup=20):
             "render_fps": round(1.0 / t_render, 1),
             "train_iters_per_s": round(1.0 / t_train, 1),
             "train_iters_per_s_foreach_adan": round(1.0 / t_train_fe, 1),
-            "timing": f"wall clock over {steps} calls after {warmup} warm-ups, synchronized",
+            "timing": f"wall clock, median of 3 blocks of {steps} calls after >= {warmup} "
+                      "warm-up calls and >= 0.3 s, synchronized",
             "host_us_per_call": host,
             "kernels": {
                 "raster_sum_fwd": roofline("raster_sum_fwd_kernel (op path: id slabs, sorted-id write-back)",
