@@ -371,6 +371,7 @@ def rasterize_sum_forward(tile_bounds, block, img_size, gaussian_ids_sorted, til
 
 LAYOUT_HWC = 0
 LAYOUT_CHW_CLAMPED = 1
+LAYOUT_CHW = 2  # channel planes, unclamped (the op path's GSVC_SLABS_PLANES image)
 
 
 def rasterize_sum_forward_ex(tile_bounds, block, img_size, gaussian_ids_sorted, tile_bins, xys,

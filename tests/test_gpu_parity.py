@@ -205,6 +205,26 @@ def test_raster_sum_forward_golden(cuda, name):
     _check_final_idx(N(idx), z["final_idx"], z["alpha_margin"])
 
 
+@pytest.mark.parametrize("name", SUM_CASES)
+def test_raster_sum_forward_every_layout(cuda, name):
+    """gsvc_rasterize_sum_forward_ex's three output layouts on every fixture:
+    the [H, W, 3] image within 1e-5 of the golden output, the unclamped planes
+    (2: the op path's GSVC_SLABS_PLANES image) its exact transpose, the
+    clamped planes (1: the render's) exactly torch.clamp of it."""
+    from gsvc_amd import ops
+    z = load_golden(name)
+    H, W = int(z["H"]), int(z["W"])
+    args = (_tb(H, W), (16, 16, 1), (W, H, 1), T(z["gaussian_ids_sorted"]), T(z["tile_bins"]),
+            T(z["xys"]), T(z["conics"]), T(z["colors"]), T(z["opacity"]), T(np.ones(3, np.float32)))
+    hwc, _ = ops.rasterize_sum_forward_ex(*args, layout=ops.LAYOUT_HWC, want_idx=False)
+    planes, _ = ops.rasterize_sum_forward_ex(*args, layout=ops.LAYOUT_CHW, want_idx=False)
+    clamped, _ = ops.rasterize_sum_forward_ex(*args, layout=ops.LAYOUT_CHW_CLAMPED, want_idx=False)
+    np.testing.assert_allclose(N(hwc), z["out_img"], rtol=1e-6, atol=1e-5)
+    assert tuple(planes.shape) == (3, H, W)
+    assert torch.equal(planes, hwc.permute(2, 0, 1))
+    assert torch.equal(clamped, torch.clamp(hwc, 0, 1).permute(2, 0, 1))
+
+
 @pytest.mark.parametrize("name", [c for c in SUM_CASES if "empty" not in c])
 def test_raster_sum_backward_vs_oracle(cuda, oracle, name):
     from gsvc_amd import ops
