@@ -221,8 +221,12 @@ def test_raster_sum_forward_every_layout(cuda, name):
     clamped, _ = ops.rasterize_sum_forward_ex(*args, layout=ops.LAYOUT_CHW_CLAMPED, want_idx=False)
     np.testing.assert_allclose(N(hwc), z["out_img"], rtol=1e-6, atol=1e-5)
     assert tuple(planes.shape) == (3, H, W)
-    assert torch.equal(planes, hwc.permute(2, 0, 1))
-    assert torch.equal(clamped, torch.clamp(hwc, 0, 1).permute(2, 0, 1))
+    bits = lambda t: t.contiguous().view(torch.int32)  # noqa: E731 (NaN colours: bitwise)
+    assert torch.equal(bits(planes), bits(hwc.permute(2, 0, 1)))
+    ref = torch.clamp(hwc, 0, 1).permute(2, 0, 1)
+    nan = torch.isnan(ref)
+    assert torch.equal(torch.isnan(clamped), nan)
+    assert torch.equal(clamped[~nan], ref[~nan])
 
 
 @pytest.mark.parametrize("name", [c for c in SUM_CASES if "empty" not in c])
