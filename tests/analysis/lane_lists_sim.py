@@ -120,3 +120,95 @@ print(dict(backward_rounds_per_band=int(rounds_sep), backward_rounds_pooled=int(
 print(dict(backward_pixel_iters_used=int(used), lane_iters_paid_classes=int(paid),
            lane_iters_paid_exact_sort=int(paid_exact), util_classes=round(used / paid, 3),
            util_exact=round(used / paid_exact, 3)))
+
+# adaptive split: within a band-chunk, split the longest items in halves while
+# the split items still fit the same number of 64-lane rounds
+import heapq  # noqa: E402
+paid_split = paid_base = 0
+for t, ids in enumerate(tiles):
+    ids = sorted(ids)[:256]
+    if not ids:
+        continue
+    ty, tx = divmod(t, tbx)
+    ids = np.array(ids)
+    X0 = np.maximum(np.ceil(xys[ids, 0] - ex[ids] - 16 * tx), 0)
+    X1 = np.minimum(np.floor(xys[ids, 0] + ex[ids] - 16 * tx), 15)
+    Y0 = np.maximum(np.ceil(xys[ids, 1] - ey[ids] - 16 * ty), 0)
+    Y1 = np.minimum(np.floor(xys[ids, 1] + ey[ids] - 16 * ty), 15)
+    ok = (X0 <= X1) & (Y0 <= Y1)
+    X0, X1, Y0, Y1 = X0[ok], X1[ok], Y0[ok], Y1[ok]
+    for c0 in range(0, len(X0), 64):
+        for band in range(2):
+            lo, hi = 8 * band, 8 * band + 7
+            seq = []
+            for e in range(c0, min(c0 + 64, len(X0))):
+                r0, r1 = max(Y0[e], lo), min(Y1[e], hi)
+                if r0 <= r1:
+                    seq += [int(X1[e] - X0[e] + 1)] * int(r1 - r0 + 1)
+            if not seq:
+                continue
+            s = sorted(seq, reverse=True)
+            paid_base += sum(64 * s[b] for b in range(0, len(s), 64))
+            rounds = (len(s) + 63) // 64
+            h = [-x for x in s]
+            heapq.heapify(h)
+            while len(h) < 64 * rounds and -h[0] > 1:
+                x = -heapq.heappop(h)
+                heapq.heappush(h, -((x + 1) // 2))
+                heapq.heappush(h, -(x // 2))
+            s2 = sorted((-x for x in h), reverse=True)
+            paid_split += sum(64 * s2[b] for b in range(0, len(s2), 64))
+print(dict(exact_sort_paid=int(paid_base), adaptive_split_paid=int(paid_split),
+           util_split=round(used / paid_split, 3)))
+
+# the kernel's own form: rows wider than a per-band-chunk brun split in two
+# halves (once), brun the smallest (>= 2) that keeps the round count; the
+# class layout (4 length classes) as now
+def paid_of(items_len):
+    cl = classes(np.array(items_len))
+    order = np.argsort(-cl, kind="stable")
+    s = np.array(items_len)[order]
+    return sum(64 * s[b:b + 64].max() for b in range(0, len(s), 64))
+
+
+paid_now = paid_adapt = 0
+for t, ids in enumerate(tiles):
+    ids = sorted(ids)[:256]
+    if not ids:
+        continue
+    ty, tx = divmod(t, tbx)
+    ids = np.array(ids)
+    X0 = np.maximum(np.ceil(xys[ids, 0] - ex[ids] - 16 * tx), 0)
+    X1 = np.minimum(np.floor(xys[ids, 0] + ex[ids] - 16 * tx), 15)
+    Y0 = np.maximum(np.ceil(xys[ids, 1] - ey[ids] - 16 * ty), 0)
+    Y1 = np.minimum(np.floor(xys[ids, 1] + ey[ids] - 16 * ty), 15)
+    ok = (X0 <= X1) & (Y0 <= Y1)
+    X0, X1, Y0, Y1 = X0[ok], X1[ok], Y0[ok], Y1[ok]
+    for c0 in range(0, len(X0), 64):
+        for band in range(2):
+            lo, hi = 8 * band, 8 * band + 7
+            ents = []
+            for e in range(c0, min(c0 + 64, len(X0))):
+                r0, r1 = max(Y0[e], lo), min(Y1[e], hi)
+                if r0 <= r1:
+                    ents.append((int(r1 - r0 + 1), int(X1[e] - X0[e] + 1)))
+            if not ents:
+                continue
+
+            def layout(brun):
+                out = []
+                for nr, w in ents:  # entry order, an entry's items together
+                    out += ([(w + 1) // 2] * 2 if w > brun else [w]) * nr
+                return out
+            base = layout(16)
+            paid_now += paid_of(base)
+            rounds = (len(base) + 63) // 64
+            best = base
+            for brun in range(15, 1, -1):
+                cand = layout(brun)
+                if (len(cand) + 63) // 64 > rounds:
+                    break
+                best = cand
+            paid_adapt += paid_of(best)
+print(dict(paid_now=int(paid_now), paid_adaptive_brun=int(paid_adapt),
+           util_now=round(used / paid_now, 3), util_adaptive=round(used / paid_adapt, 3)))
