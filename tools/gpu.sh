@@ -51,6 +51,7 @@ pmc() {  # pmc NAME COUNTERS... -- CMD: one counter pass, killed hard at its lim
   while [ "$1" != "--" ]; do ctrs+=("$1"); shift; done
   shift
   echo "== pmc $name: ${ctrs[*]}"
+  mkdir -p "$(dirname "$OUT/$name.log")"
   timeout -s KILL 200 rocprofv3 --pmc "${ctrs[@]}" -d "$OUT/$name" -o p --output-format csv -- "$@" \
     > "$OUT/$name.log" 2>&1 || { echo "pmc $name failed"; tail -5 "$OUT/$name.log"; exit 1; }
 }
