@@ -309,7 +309,7 @@ __device__ __forceinline__ int wave_brute_tile_ids(const SumFwdArgs &A, int tile
 }
 
 // Sparse path: one wave blends the whole 16x16 tile, 4 pixels per lane.
-template <int kMode, bool kIdx>
+template <int kMode, bool kIdx, bool kSplit = false>
 __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, int2 range, int n,
                                                float4 *s_slice, float3 init, bool ids_in_lds,
                                                const int *s_ids, const float4 *seg_rec,
@@ -471,11 +471,27 @@ __device__ __forceinline__ void sum_fwd_sparse(const SumFwdArgs &A, int tile, in
         if (base == 0) phase_stamp<kMode>(A, tile, 1, 2);
         // the lane's 4x4 block of the tile
         const unsigned char *ml = s_list + (((lane >> 4) << 2) | (lane & 3));
-        for (int it = 0; it < maxlen; ++it) {
-            if (!kIdx && cut)
-                blend(ml[16 * it], std::true_type{});
-            else
-                blend(ml[16 * it], std::false_type{});
+        if constexpr (kSplit) {
+            // one loop per variant: no accumulator moves between the two bodies'
+            // registers each trip (6 v_mov_b64 of ~40 VALU), at the cost of a
+            // few spilled registers around the loops -- the dense render's
+            // instance (raster_render_ids_kernel<W, true>, chosen by the density
+            // hint): trained 1080p / 50k composite 20.3 -> 19.2 us, 10k frames
+            // keep the single loop (7.9 vs 8.1 us; profiles/r06/render_split/)
+            if (!kIdx && cut) {
+#pragma unroll 1
+                for (int it = 0; it < maxlen; ++it) blend(ml[16 * it], std::true_type{});
+            } else {
+#pragma unroll 1
+                for (int it = 0; it < maxlen; ++it) blend(ml[16 * it], std::false_type{});
+            }
+        } else {
+            for (int it = 0; it < maxlen; ++it) {
+                if (!kIdx && cut)
+                    blend(ml[16 * it], std::true_type{});
+                else
+                    blend(ml[16 * it], std::false_type{});
+            }
         }
         wave_lds_sync();
     }
@@ -925,7 +941,7 @@ raster_sum_fwd_kernel(SumFwdArgs A) {
 // per wave with every tile's loads issued before the first blends (K = 2, 4):
 // slower (12.7 vs 12.0 us; 4: 26 vs 20 us per frame).  A/B knob 38 = 1: the
 // generic kernel.
-template <int W>
+template <int W, bool kSplit>
 __global__ __launch_bounds__(64 * W, 8) void raster_render_ids_kernel(SumFwdArgs A) {
     __shared__ float4 s_bufw[W][kSlice];
     __shared__ int s_idsw[W][kTilePix];
@@ -964,7 +980,7 @@ __global__ __launch_bounds__(64 * W, 8) void raster_render_ids_kernel(SumFwdArgs
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     if (n <= kChunk) {
         // <= 64 entries: the records gathered by id and ranked into the staging
-        sum_fwd_sparse<kModeSparseIds, false>(A, tile, range, n, s_buf, init, false, s_ids,
+        sum_fwd_sparse<kModeSparseIds, false, kSplit>(A, tile, range, n, s_buf, init, false, s_ids,
                                               n > 0 ? A.rec : nullptr, nullptr, z, z, z, 0, spec_id);
         return;
     }
@@ -975,7 +991,7 @@ __global__ __launch_bounds__(64 * W, 8) void raster_render_ids_kernel(SumFwdArgs
     seg.head = nullptr;
     n = n_all > kCarryCap ? wave_brute_tile_ids(A, tile, s_ids)
                           : wave_sorted_tile_ids(seg, n_all, s_ids, reinterpret_cast<unsigned *>(s_buf));
-    sum_fwd_sparse<kModeSparseIds, false>(A, tile, range, n, s_buf, init, true, s_ids, nullptr, nullptr, z,
+    sum_fwd_sparse<kModeSparseIds, false, kSplit>(A, tile, range, n, s_buf, init, true, s_ids, nullptr, nullptr, z,
                                           z, z, 0, spec_id);
 }
 
@@ -1642,8 +1658,13 @@ int sum_forward_launch(SumFwdArgs &A, int density_hint, hipStream_t s) {
         // the generic kernel)
         const bool render = A.frames == 1 && !A.bins_out && !A.final_idx && A.m_dev &&
                             A.ids_cap == kCarryCap && A.layout == kLayoutCHWClamped && A.rec && A.sort_ids;
-        if (render && knob(38) != 1)
-            launch_fwd(raster_render_ids_kernel<2>, dim3((A.ntiles + 1) / 2), dim3(128), s, tev, A);
+        if (render && knob(38) != 1) {
+            // more than 8 entries per tile on average: the split-loop instance
+            if ((long long)density_hint > 8ll * A.ntiles)
+                launch_fwd(raster_render_ids_kernel<2, true>, dim3((A.ntiles + 1) / 2), dim3(128), s, tev, A);
+            else
+                launch_fwd(raster_render_ids_kernel<2, false>, dim3((A.ntiles + 1) / 2), dim3(128), s, tev, A);
+        }
         else
             launch_fwd(raster_sum_fwd_kernel<kModeSparseIds, false>, grid, dim3(64), s, tev, A);
     } else if constexpr (kDiag) {

@@ -120,3 +120,31 @@ def test_id_slab_batched_render_bit_identical(cuda):
     torch.cuda.synchronize()
     for g in got:
         assert torch.equal(g, ref)
+
+
+@pytest.mark.parametrize("n,chol", [(50000, 3.0), (50000, 1.5)])
+def test_render_split_loop_instance_bit_identical(cuda, n, chol):
+    """raster_render_ids_kernel's two instances -- the lane-group loop with the
+    cut / generic branch inside (frames of <= 8 entries per tile by the density
+    hint) and one loop per variant (denser frames) -- give the same bits: the
+    first render of a workspace runs with hint 0, later ones with the frame's M
+    once the lazy count has read it back."""
+    from gsvc_amd import render as R
+    H, W = 1080, 1920
+    xyz, c, f = _frame(n, 11 + n, chol, cuda)
+    bound = torch.tensor([0.5, 0.0, 0.5], device=cuda)
+    bg = torch.tensor([0.3, 0.6, 0.9], device=cuda)
+    R._workspaces.clear()
+    first = R.render_frame_sum(xyz, c, f, H, W, bg, cholesky_bound=bound)
+    fw = R._workspaces[(cuda.index, R._raw_stream(cuda.index))]
+    assert fw.hint.value == 0  # the first call: the single-loop instance
+    ntiles = ((W + 15) // 16) * ((H + 15) // 16)
+    for _ in range(64):
+        torch.cuda.synchronize()
+        last = R.render_frame_sum(xyz, c, f, H, W, bg, cholesky_bound=bound)
+        if fw.hint.value > 8 * ntiles:
+            break
+    assert fw.hint.value > 8 * ntiles, fw.hint.value
+    last = R.render_frame_sum(xyz, c, f, H, W, bg, cholesky_bound=bound)  # the split instance
+    torch.cuda.synchronize()
+    assert torch.equal(first, last)
