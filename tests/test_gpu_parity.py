@@ -205,7 +205,7 @@ def test_raster_sum_forward_golden(cuda, name):
     _check_final_idx(N(idx), z["final_idx"], z["alpha_margin"])
 
 
-@pytest.mark.parametrize("name", SUM_CASES)
+@pytest.mark.parametrize("name", [c for c in SUM_CASES if "empty" not in c])
 def test_raster_sum_forward_every_layout(cuda, name):
     """gsvc_rasterize_sum_forward_ex's three output layouts on every fixture:
     the [H, W, 3] image within 1e-5 of the golden output, the unclamped planes
