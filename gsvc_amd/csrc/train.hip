@@ -1198,24 +1198,28 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
         const int total = __builtin_amdgcn_readlane(incl, 63);
 #pragma unroll
         for (int c = 0; c < 8; ++c) eacc[c * kBChunk + lane] = 0.0f;
-        for (int base = 0; base < total; base += 64) {
-            // the entry of item base + lane: the last entry whose first item is <= it
-            wown[lane] = -1;
-            __builtin_amdgcn_wave_barrier();
-            if (sitems > 0 && off >= base && off < base + 64) wown[off - base] = (signed char)lane;
-            const int straddle = __popcll(__ballot(lane < gn && off <= base)) - 1;
-            __builtin_amdgcn_wave_barrier();
-            int slot = max((int)wown[lane], straddle);
-            slot = wave_scan_dpp<true>(slot, -2147483647 - 1);  // sorted slot of item base + lane
-            const int item = base + lane;
-            // the entry, its first item and rectangle
-            const int own = __shfl(ent, slot, 64);
-            const int eoff = __shfl(off, slot, 64);
-            const unsigned ro = (unsigned)__shfl((int)rc, own, 64);
-            float g[8];
-#pragma unroll
-            for (int c = 0; c < 8; ++c) g[c] = 0.0f;
-            if (item < total) {
+        // One round loop per alpha-cut variant (bcut: the chunk's, wave-uniform),
+        // and the lanes without pixel work -- past the last item, or a row below
+        // the image -- walking an empty range and selecting zeros: with the
+        // variant branch and the validity branches inside the loop, the
+        // compiler kept the two walks' sums and the zero-filled sums in
+        // different registers and moved them back every round (ISA: 83
+        // v_mov_b32 of 337 VALU per round).  Same sums bit for bit.
+        auto rounds = [&](auto kcut) {
+            for (int base = 0; base < total; base += 64) {
+                // the entry of item base + lane: the last entry whose first item is <= it
+                wown[lane] = -1;
+                __builtin_amdgcn_wave_barrier();
+                if (sitems > 0 && off >= base && off < base + 64) wown[off - base] = (signed char)lane;
+                const int straddle = __popcll(__ballot(lane < gn && off <= base)) - 1;
+                __builtin_amdgcn_wave_barrier();
+                int slot = max((int)wown[lane], straddle);
+                slot = wave_scan_dpp<true>(slot, -2147483647 - 1);  // sorted slot of item base + lane
+                const int item = base + lane;
+                // the entry, its first item and rectangle
+                const int own = __shfl(ent, slot, 64);
+                const int eoff = __shfl(off, slot, 64);
+                const unsigned ro = (unsigned)__shfl((int)rc, own, 64);
                 const float4 G = S.geo[own], C = S.col[own];
                 const int j = item - eoff;  // item index within the entry
                 const int rx0 = (int)(ro & 15u), rx1 = (int)((ro >> 4) & 15u);
@@ -1227,113 +1231,114 @@ __global__ __launch_bounds__(kBThreads, 8) void train_tile_band_kernel(TrainTile
                 const int cs = ipr == 1 ? rx0 : rx0 + half * (j & 1);
                 const int ce = min(ipr == 1 ? rx1 : min(cs + half - 1, rx1), A.img_w - 1 - (int)tx0);
                 const float pyf = ty0 + (float)row;
-                if ((int)pyf < A.img_h && !(kDiag && (A.diag & 8))) {  // diag 8: no pixel work
-                    const float ex = G.x, eha = G.z, eb = G.w;
-                    const float dy = G.y - pyf;
-                    const float cq = (C.x * dy) * dy;  // splat_sigma_h's row terms
-                    const float bdy = eb * dy;
-                    // dy is constant along the item's row, so the per-pixel sums of
-                    // backward.cu:822-848 factor: v_conic = 1/2 (S2, dy S1, dy^2 S0),
-                    // v_xy = (2 ha S1 + b dy S0, b S1 + 2 c dy S0) with S_k = sum
-                    // v_sigma dx^k -- 4 VALU per pixel instead of 11
-                    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
-                    // walk the row by its v_out word (the planes at fixed LDS
-                    // offsets) with dx stepping by -1 (exact: ex - px is exact
-                    // or, far off, rounds alike)
-                    const float *vp = &S.v[0][0] + row * kVRow + cs;
-                    const float *const ve = &S.v[0][0] + row * kVRow + ce;
-                    float dx = ex - (tx0 + (float)cs);
-                    // kCut: the chunk's geometry is finite, so the alpha cut is
-                    // the sigma threshold and alpha = vis (kSigmaCutBits); else
-                    // the reference's test as written
-                    auto walk = [&](auto kcut) {
-                        for (; vp <= ve; ++vp, dx -= 1.0f) {
-                            float Px, Py, Pz;
-                            if (kDiag && (A.diag & 256)) {  // diag 256: no v_out reads (wrong)
-                                Px = dx;
-                                Py = 0.5f * dx;
-                                Pz = bdy;
-                            } else {
-                                Px = vp[0];
-                                Py = vp[kTile * kVRow];
-                                Pz = vp[2 * kTile * kVRow];
-                            }
-                            const float sgm = fmaf(fmaf(eha, dx, bdy), dx, cq);
-                            const float vis = exp_neg(sgm);
-                            float al;
-                            if constexpr (decltype(kcut)::value) {
-                                // a failing pixel adds exact zeros (a select, not a branch:
-                                // the same sums bit for bit, without the exec-mask
-                                // bookkeeping per pixel -- bench.py 18.39k vs 18.21k
-                                // it/s, tile kernel 45.5 vs 45.8 us, product libraries
-                                // swapped on one box, profiles/r06/select_cut/)
-                                al = __float_as_uint(sgm) <= kSigmaCutBits ? vis : 0.0f;
-                                const float v_alpha = fmaf(C.w, Pz, fmaf(C.z, Py, C.y * Px));
-                                const float v_sigma = (-al) * v_alpha;
-                                g[5] = fmaf(al, Px, g[5]);
-                                g[6] = fmaf(al, Py, g[6]);
-                                g[7] = fmaf(al, Pz, g[7]);
-                                s0 += v_sigma;
-                                const float vdx = v_sigma * dx;
-                                s1 += vdx;
-                                s2 = fmaf(vdx, dx, s2);
-                                continue;
-                            } else {
-                                al = fminf(1.0f, vis);  // opacity 1
-                                if (sgm < 0.0f || al < kAlphaMin) continue;
-                            }
-                            const float v_alpha = fmaf(C.w, Pz, fmaf(C.z, Py, C.y * Px));
-                            const float v_sigma = (-vis) * v_alpha;  // (-opacity * vis) * v_alpha
-                            g[5] = fmaf(al, Px, g[5]);
-                            g[6] = fmaf(al, Py, g[6]);
-                            g[7] = fmaf(al, Pz, g[7]);
-                            s0 += v_sigma;
-                            const float vdx = v_sigma * dx;
-                            s1 += vdx;
-                            s2 = fmaf(vdx, dx, s2);
-                        }
-                    };
-                    // (pixel PAIRS with packed math -- 3 two-word LDS reads, 2 exps
-                    // and ~23 VALU per pair instead of ~34 per two pixels -- were
-                    // measured, round 6: 49.8 vs 45.9 us per tile-kernel launch in
-                    // bench.py, product libraries swapped on one box; 64 VGPRs with
-                    // 60-72 B of spills, or 72 VGPRs at 7 waves per SIMD: 48.2;
-                    // profiles/r06/tile_pairs/)
-                    if (bcut) {
-                        walk(std::true_type{});
+                // diag 8: no pixel work
+                const bool rowok = item < total && (int)pyf < A.img_h && !(kDiag && (A.diag & 8));
+                const float ex = G.x, eha = G.z, eb = G.w;
+                const float dy = G.y - pyf;
+                const float cq = (C.x * dy) * dy;  // splat_sigma_h's row terms
+                const float bdy = eb * dy;
+                // dy is constant along the item's row, so the per-pixel sums of
+                // backward.cu:822-848 factor: v_conic = 1/2 (S2, dy S1, dy^2 S0),
+                // v_xy = (2 ha S1 + b dy S0, b S1 + 2 c dy S0) with S_k = sum
+                // v_sigma dx^k -- 4 VALU per pixel instead of 11
+                float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
+                float g[8];
+                g[5] = 0.0f;
+                g[6] = 0.0f;
+                g[7] = 0.0f;
+                // walk the row by its v_out word (the planes at fixed LDS
+                // offsets) with dx stepping by -1 (exact: ex - px is exact or,
+                // far off, rounds alike); a lane without pixel work: no trip
+                const float *vp = &S.v[0][0] + row * kVRow + cs;
+                const float *const ve = rowok ? &S.v[0][0] + row * kVRow + ce : vp - 1;
+                float dx = ex - (tx0 + (float)cs);
+                // kCut: the chunk's geometry is finite, so the alpha cut is the
+                // sigma threshold and alpha = vis (kSigmaCutBits); else the
+                // reference's test as written
+                for (; vp <= ve; ++vp, dx -= 1.0f) {
+                    float Px, Py, Pz;
+                    if (kDiag && (A.diag & 256)) {  // diag 256: no v_out reads (wrong)
+                        Px = dx;
+                        Py = 0.5f * dx;
+                        Pz = bdy;
                     } else {
-                        walk(std::false_type{});
+                        Px = vp[0];
+                        Py = vp[kTile * kVRow];
+                        Pz = vp[2 * kTile * kVRow];
                     }
-                    const float hdy = 0.5f * dy;
-                    g[0] = fmaf(2.0f * eha, s1, bdy * s0);
-                    g[1] = fmaf(eb, s1, ((2.0f * C.x) * dy) * s0);
-                    g[2] = 0.5f * s2;
-                    g[3] = hdy * s1;
-                    g[4] = (hdy * dy) * s0;
+                    const float sgm = fmaf(fmaf(eha, dx, bdy), dx, cq);
+                    const float vis = exp_neg(sgm);
+                    float al;
+                    if constexpr (decltype(kcut)::value) {
+                        // a failing pixel adds exact zeros (a select, not a branch:
+                        // the same sums bit for bit, without the exec-mask
+                        // bookkeeping per pixel -- bench.py 18.39k vs 18.21k it/s,
+                        // tile kernel 45.5 vs 45.8 us, product libraries swapped on
+                        // one box, profiles/r06/select_cut/)
+                        al = __float_as_uint(sgm) <= kSigmaCutBits ? vis : 0.0f;
+                        const float v_alpha = fmaf(C.w, Pz, fmaf(C.z, Py, C.y * Px));
+                        const float v_sigma = (-al) * v_alpha;
+                        g[5] = fmaf(al, Px, g[5]);
+                        g[6] = fmaf(al, Py, g[6]);
+                        g[7] = fmaf(al, Pz, g[7]);
+                        s0 += v_sigma;
+                        const float vdx = v_sigma * dx;
+                        s1 += vdx;
+                        s2 = fmaf(vdx, dx, s2);
+                        continue;
+                    } else {
+                        al = fminf(1.0f, vis);  // opacity 1
+                        if (sgm < 0.0f || al < kAlphaMin) continue;
+                    }
+                    const float v_alpha = fmaf(C.w, Pz, fmaf(C.z, Py, C.y * Px));
+                    const float v_sigma = (-vis) * v_alpha;  // (-opacity * vis) * v_alpha
+                    g[5] = fmaf(al, Px, g[5]);
+                    g[6] = fmaf(al, Py, g[6]);
+                    g[7] = fmaf(al, Pz, g[7]);
+                    s0 += v_sigma;
+                    const float vdx = v_sigma * dx;
+                    s1 += vdx;
+                    s2 = fmaf(vdx, dx, s2);
                 }
-            }
-            // segmented sums over the runs of items of one entry: the last item
-            // of an entry's run holds the run's sum (fixed tree order) and adds it
-            // to the entry's (a fixed order: rounds in sequence).  Measured
-            // alternatives: every item adding its sums with LDS float atomics
-            // (2.9x slower kernel: the LDS serialises an entry's items); a packed
-            // two-pixel loop (80 VGPRs, 6 waves per SIMD: 64.0 vs 58.5 us)
-            // an entry has at most 8 items in a band unless rows split in two
-            // (brun < 16): runs of <= 8 lanes need no row_shr:8 step (a run
-            // crossing a 16-lane row still takes the row broadcast)
-            if (!(kDiag && (A.diag & 16))) {  // diag 16: no run sums (wrong)
-                if (brun_of(A) < 16)
-                    wave_seg_sums<8, true>(g, own);
-                else
-                    wave_seg_sums<8, false>(g, own);
-            }
-            const int own_next = __shfl_down(own, 1, 64);
-            if (item < total && (lane == 63 || item + 1 == total || own_next != own)) {
+                // (pixel PAIRS with packed math -- 3 two-word LDS reads, 2 exps and
+                // ~23 VALU per pair instead of ~34 per two pixels -- were measured,
+                // round 6: 49.8 vs 45.9 us per tile-kernel launch in bench.py,
+                // product libraries swapped on one box; 64 VGPRs with 60-72 B of
+                // spills, or 72 VGPRs at 7 waves per SIMD: 48.2;
+                // profiles/r06/tile_pairs/)
+                const float hdy = 0.5f * dy;
+                g[0] = rowok ? fmaf(2.0f * eha, s1, bdy * s0) : 0.0f;
+                g[1] = rowok ? fmaf(eb, s1, ((2.0f * C.x) * dy) * s0) : 0.0f;
+                g[2] = rowok ? 0.5f * s2 : 0.0f;
+                g[3] = rowok ? hdy * s1 : 0.0f;
+                g[4] = rowok ? (hdy * dy) * s0 : 0.0f;
+                // segmented sums over the runs of items of one entry: the last item
+                // of an entry's run holds the run's sum (fixed tree order) and adds
+                // it to the entry's (a fixed order: rounds in sequence).  Measured
+                // alternatives: every item adding its sums with LDS float atomics
+                // (2.9x slower kernel: the LDS serialises an entry's items); a
+                // packed two-pixel loop (80 VGPRs, 6 waves per SIMD: 64.0 vs 58.5
+                // us).  An entry has at most 8 items in a band unless rows split
+                // in two (brun < 16): runs of <= 8 lanes need no row_shr:8 step (a
+                // run crossing a 16-lane row still takes the row broadcast)
+                if (!(kDiag && (A.diag & 16))) {  // diag 16: no run sums (wrong)
+                    if (brun_of(A) < 16)
+                        wave_seg_sums<8, true>(g, own);
+                    else
+                        wave_seg_sums<8, false>(g, own);
+                }
+                const int own_next = __shfl_down(own, 1, 64);
+                if (item < total && (lane == 63 || item + 1 == total || own_next != own)) {
 #pragma unroll
-                for (int c = 0; c < 8; ++c) eacc[c * kBChunk + own] += g[c];
+                    for (int c = 0; c < 8; ++c) eacc[c * kBChunk + own] += g[c];
+                }
+                __builtin_amdgcn_wave_barrier();
             }
-            __builtin_amdgcn_wave_barrier();
-        }
+        };
+        if (bcut)
+            rounds(std::true_type{});
+        else
+            rounds(std::false_type{});
         __syncthreads();
         // 8 lanes per entry add the entry's sums (band 0 + band 1) into the
         // splat's gradient record
