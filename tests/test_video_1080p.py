@@ -15,7 +15,8 @@ op-by-op path that GSVC's unchanged GaussianSplats_Represent.py runs): the
 splat counts the controls leave must be identical and the per-frame PSNRs
 close (float atomics in the backward make the two trajectories differ in the
 last bits, which Adan's normalisation amplifies, so PSNR is compared with a
-tolerance rather than bit for bit).
+tolerance rather than bit for bit); and the last frame's checkpointed model,
+rendered by the C oracle, must score the PSNR the loop logged.
 """
 import functools
 
@@ -53,6 +54,48 @@ def test_config4_two_gops_1080p_50k(cuda, tmp_path):
     np.testing.assert_allclose(p, q, atol=0.05)
     assert [r["num_gaussians"] for r in res["frames"]] == [50000] * 4
     assert res["average"]["psnr"] == pytest.approx(float(p.mean()), rel=1e-9)
+    _check_last_frame_against_oracle(tmp_path / "fused", argv, res)
+
+
+def _check_last_frame_against_oracle(root, argv, res):
+    """An oracle anchor for the video loop: the last
+    frame's model as the checkpoint holds it (train_video_Represent.py:379,384;
+    torch.load weights_only), rendered by the C oracle from its own activations
+    (GaussianSplats_Represent.py:57-70), scored against the video's frame --
+    the PSNR the fused loop logged for that frame, within 1e-4 dB."""
+    import math
+    import os
+    import sys
+    from gsvc_amd import video as V
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "oracle"))
+    import oracle as O
+    vargs = V.parse_args(argv + ["--root", str(root)])
+    mdir = os.path.join(str(root), vargs.savdir_m, vargs.data_name,
+                        f"{vargs.model_name}_{vargs.iterations}_{vargs.num_points}")
+    models = torch.load(os.path.join(mdir, "gmodels_state_dict.pth"), weights_only=True,
+                        map_location="cpu")
+    last = res["frames"][-1]
+    sd = models[f"frame_{last['frame']}"]
+    H, W = vargs.height, vargs.width
+    xyz, chol, feat = (sd[k].numpy() for k in ("_xyz", "_cholesky", "_features_dc"))
+    rgbw = sd["rgb_W"].numpy() if "rgb_W" in sd else np.ones((xyz.shape[0], 1), np.float32)
+    means = torch.tanh(torch.from_numpy(xyz)).numpy()  # the kernels' tanhf == torch.tanh
+    L = (chol + np.array([0.5, 0.0, 0.5], np.float32)).astype(np.float32)
+    colors = (feat * rgbw).astype(np.float32)
+    O.lib()
+    O.set_threads(8)
+    try:
+        r = O.render_sum(means, L, colors, np.ones((xyz.shape[0], 1), np.float32), H, W)
+    finally:
+        O.set_threads(1)
+    img = np.clip(r["out"], 0, 1).transpose(2, 0, 1)
+    gen = V.synthetic_video(vargs.synthetic, H, W, int(vargs.seed), vargs.cut_every,
+                            device=torch.device("cuda:0"))
+    gt = gen(last["frame"] - 1).cpu().numpy().reshape(3, H, W)
+    mse = float(np.mean((img.astype(np.float64) - gt.astype(np.float64)) ** 2))
+    assert abs(10 * math.log10(1.0 / mse) - last["psnr"]) <= 1e-4, (10 * math.log10(1.0 / mse),
+                                                                     last["psnr"])
 
 
 def test_config5_removal_and_densify_1080p_100k(cuda, tmp_path):
@@ -78,3 +121,4 @@ def test_config5_removal_and_densify_1080p_100k(cuda, tmp_path):
     np.testing.assert_allclose(p[0], q[0], rtol=0.005)
     np.testing.assert_allclose(p[1:], q[1:], rtol=0.02)
     assert all(r["iterations"] == 1100 for r in res["frames"])
+    _check_last_frame_against_oracle(tmp_path / "fused", argv, res)
