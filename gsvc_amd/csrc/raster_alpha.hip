@@ -39,24 +39,26 @@ __device__ __forceinline__ void alpha_blend4(float4 G, float4 C, float blu, floa
     const float dy = G.y - py;
     const float cq = (C.x * dy) * dy;
     const float bdy = G.w * dy;
+    // every pixel evaluated and the updates selected (no per-pixel branches: a
+    // lane's skipped pixel cost its wave the same slots anyway, and the
+    // branches' joins moved the accumulators between registers each trip --
+    // 18 v_mov of 57 VALU); a done or failing pixel keeps its state bit for bit
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        if (done[q]) continue;
         const float dx = G.x - (float)(pj + q);
         const float s = fmaf(fmaf(G.z, dx, bdy), dx, cq);
         const float al = fminf(0.999f, C.y * exp_neg(s));
-        if (s < 0.0f || al < kAlphaMin) continue;
+        const bool act = !done[q] && !(s < 0.0f) && !(al < kAlphaMin);
         const float next_T = T[q] * (1.0f - al);
-        if (next_T <= 1e-4f) {
-            done[q] = true;
-            continue;
-        }
+        const bool stop = next_T <= 1e-4f;
+        const bool upd = act && !stop;
+        done[q] = done[q] || (act && stop);
         const float vis = al * T[q];
-        ar[q] = fmaf(C.z, vis, ar[q]);
-        ag[q] = fmaf(C.w, vis, ag[q]);
-        ab[q] = fmaf(blu, vis, ab[q]);
-        T[q] = next_T;
-        last[q] = k;
+        ar[q] = upd ? fmaf(C.z, vis, ar[q]) : ar[q];
+        ag[q] = upd ? fmaf(C.w, vis, ag[q]) : ag[q];
+        ab[q] = upd ? fmaf(blu, vis, ab[q]) : ab[q];
+        T[q] = upd ? next_T : T[q];
+        last[q] = upd ? k : last[q];
     }
 }
 
